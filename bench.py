@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Throughput of the embed + match hot path (BASELINE.json metric), one JSON line.
+
+Workload at N=1 (BASELINE.json configs[2]): IR-101 AdaFace embed + cosine top-5
+match of a batch of 256 synthetic 112x112 crops per GPU against a 1k-row
+gallery.  One "step" = one ``fr_embed_match`` over the rank's batch, inputs
+already resident in HBM.  For N>1 (torchrun, one rank per GPU) rank 0 embeds
+the gallery and broadcasts it over RCCL (the path's only exchange step); each
+rank then processes its own probes independently (weak scaling).
+
+Also reported:
+  roofline      conv_mfma kernel family (every 3x3 / 1x1 conv and the FC, >99%
+                of the path's FLOPs): algorithmic FLOP / summed HIP-event time
+                of those launches inside the timed region, vs the 157.3 TF
+                dense fp32 MFMA peak.
+  cpu_baseline  the oracle (PyTorch-CPU IR-101 + reference-style per-probe
+                search) on rank 0's host cores, on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from facerecognitionpipeline_amd import weights as W  # noqa: E402
+from facerecognitionpipeline_amd.arch import flop_per_face  # noqa: E402
+
+METRIC = "faces/sec embed+match (IR-101, 112×112, gallery=1k) at 1/2/4/8 GPU"
+FP32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--arch", default="ir_101")
+    ap.add_argument("--batch", type=int, default=256, help="crops per GPU per step")
+    ap.add_argument("--gallery", type=int, default=1000)
+    ap.add_argument("--topk", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per conv launch (optional)")
+    return ap.parse_args()
+
+
+def cpu_baseline(arch, sd, gallery_np, crops, budget_s):
+    """Oracle (reference CPU path restated) on a bounded sample: batch-32 embed + per-probe search."""
+    from oracle.adaface_net import load_oracle
+    from oracle import reference_path as rp
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    model = load_oracle(arch, sd)
+    ids = [f"S{i}" for i in range(gallery_np.shape[0])]
+    names = {s: s for s in ids}
+    rp.extract_embeddings_batch(model, list(crops[:32]))  # warm-up batch
+    done, t0 = 0, time.perf_counter()
+    while done < len(crops):
+        e = rp.extract_embeddings_batch(model, list(crops[done:done + 32]), batch_size=32)
+        for q in e:
+            gal = np.vstack([gallery_np[i] for i in range(gallery_np.shape[0])])  # per-query vstack, as the reference
+            rp.search(gal, ids, names, q, top_k=5)
+        done += len(e)
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 3), "unit": "faces/s", "cores": threads, "kind": "port",
+            "sample": f"{done} crops of the bench workload ({arch}, batch 32, G={gallery_np.shape[0]} per-probe "
+                      f"vstack+sgemv+argsort search), {dt:.1f} s on {threads} host threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    sd = W.synthetic_state_dict(args.arch)
+    emb = FaceEmbedder(architecture=args.arch, state_dict=sd, device=dev, max_batch=args.batch)
+
+    # gallery: rank 0 embeds G synthetic gallery crops on its GPU, RCCL broadcast to the others
+    G = args.gallery
+    gallery = torch.empty((G, 512), dtype=torch.float32, device=dev)
+    gal_crops = W.synthetic_crops(G, W.CROP_SEED_GALLERY)
+    if rank == 0:
+        emb.embed_tensor(torch.from_numpy(gal_crops).to(dev), out=gallery)
+    if world > 1:
+        dist.broadcast(gallery, src=0)
+    emb.model.gallery_set(gallery)
+
+    # probes resident in HBM: noisy copies of gallery crops (rank-dependent)
+    probes_np = W.probe_crops(gal_crops, args.batch, seed=W.CROP_SEED_PROBE + rank)
+    rgb = torch.from_numpy(probes_np).to(dev)
+    k = args.topk
+    idx = torch.empty((args.batch, k), dtype=torch.int32, device=dev)
+    score = torch.empty((args.batch, k), dtype=torch.float32, device=dev)
+    e_out = torch.empty((args.batch, 512), dtype=torch.float32, device=dev)
+
+    for _ in range(args.warmup):
+        emb.model.embed_match(rgb, k, idx, score, e_out)
+    torch.cuda.synchronize()
+    emb.model.profile_enable(True)
+    emb.model.profile_read()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        emb.model.embed_match(rgb, k, idx, score, e_out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = emb.model.profile_read()
+    emb.model.profile_enable(False)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    tmax = t.item()
+
+    # sanity: probes are noisy copies of gallery rows i % G
+    top1_ok = float((idx[:, 0].cpu().numpy() == np.arange(args.batch) % G).mean())
+
+    if rank == 0:
+        faces = world * args.batch * args.steps
+        conv_tflops = prof["conv_flop"] / (prof["conv_ms"] * 1e-3) / 1e12 if prof["conv_ms"] > 0 else 0.0
+        per_launch_flop = prof["conv_flop"] / max(prof["conv_launches"], 1)
+        traffic = None
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            with open(args.traffic_json) as f:
+                traffic = json.load(f).get("hbm_bytes_per_conv_launch")
+        out = {
+            "metric": METRIC,
+            "value": round(faces / tmax, 2),
+            "unit": "faces/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded uint8 crops; seeded random-init AdaFace weights)",
+            "config": {"workload": f"C3: {args.arch.upper().replace('_', '-')} AdaFace embed + cosine top-{k} match "
+                                   f"vs {G}-row gallery, batch {args.batch}/GPU, 112x112 uint8 RGB",
+                       "arch": args.arch, "batch_per_gpu": args.batch, "global_batch": args.batch * world,
+                       "gallery": G, "top_k": k, "parallelism": f"dp{world}",
+                       "gallery_exchange": "rccl broadcast" if world > 1 else "none"},
+            "flop_per_face": flop_per_face(args.arch, G),
+            "top1_self_match": top1_ok,
+            "roofline": {"bound": "mfma", "kernel": "conv_mfma_kernel (all conv/FC launches)",
+                         "achieved": round(conv_tflops, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(conv_tflops / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "launches": prof["conv_launches"], "flop_per_launch": per_launch_flop,
+                         "avg_launch_ms": round(prof["conv_ms"] / max(prof["conv_launches"], 1), 5),
+                         "conv_share_of_step": round(prof["conv_ms"] / max(prof["total_ms"], 1e-9), 4)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sample = W.probe_crops(gal_crops, 256, seed=W.CROP_SEED_PROBE)
+            out["cpu_baseline"] = cpu_baseline(args.arch, sd, gallery.cpu().numpy(), sample, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+"""ctypes binding of libfrhip.so (the C ABI of include/frhip.h).
+
+The library is loaded AFTER ``import torch`` so that it binds to the same HIP
+runtime instance (SONAME libamdhip64.so.7) PyTorch-ROCm already loaded: device
+pointers and streams are then shared with torch tensors.  There is no CPU
+fallback anywhere: if the library is missing or no GPU is present, every
+entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch  # noqa: F401  (must precede the CDLL load, see module doc)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfrhip.so")
+
+FR_OK = 0
+FR_ERR_INVALID_ARGUMENT = -1
+FR_ERR_MISSING_PARAM = -2
+FR_ERR_HIP = -3
+FR_ERR_STATE = -4
+FR_ERR_UNSUPPORTED = -5
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_SIGNATURES = {
+    "fr_create": (_I, [ctypes.c_char_p, ctypes.c_char_p, _I, _I, ctypes.POINTER(_P)]),
+    "fr_destroy": (_I, [_P]),
+    "fr_set_param": (_I, [_P, ctypes.c_char_p, _P, ctypes.c_int64]),
+    "fr_finalize": (_I, [_P]),
+    "fr_embed": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
+    "fr_embed_host": (_I, [_P, _P, _I, _I, _I, _P, _I]),
+    "fr_gallery_set": (_I, [_P, _P, _I, _I, _I, _P]),
+    "fr_gallery_size": (_I, [_P, ctypes.POINTER(_I)]),
+    "fr_match_topk": (_I, [_P, _P, _I, _I, _P, _P, _P]),
+    "fr_match_topk_host": (_I, [_P, _P, _I, _I, _P, _P]),
+    "fr_embed_match": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
+    "fr_profile_enable": (_I, [_P, _I]),
+    "fr_profile_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
+    "fr_last_error": (ctypes.c_char_p, [_P]),
+    "fr_version": (ctypes.c_char_p, []),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+class FrHipError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libfrhip.so once; raise loudly if it is not built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise FrHipError(f"{LIB_PATH} is not built: run `python -m facerecognitionpipeline_amd.build` "
+                                 "(the HIP path has no CPU fallback)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, handle=None) -> None:
+    """Map a status code to the reference's exception types (SURVEY.md §8(b) Errors)."""
+    if rc == FR_OK:
+        return
+    msg = load().fr_last_error(handle)
+    msg = msg.decode() if msg else f"frhip error {rc}"
+    if rc == FR_ERR_INVALID_ARGUMENT:
+        raise ValueError(msg)
+    if rc == FR_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise FrHipError(msg)
+
+
+def ptr(t) -> Optional[int]:
+    """Raw data pointer of a torch tensor (or None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_of(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Handle:
+    """Owns one ``fr_handle``: a model (after ``load_state_dict``) and/or a gallery."""
+
+    def __init__(self, architecture: str, model_type: str, device: torch.device, max_batch: int = 256):
+        if device.type != "cuda":
+            raise RuntimeError("facerecognitionpipeline_amd runs on a HIP device only (no CPU fallback); "
+                               f"got device={device}")
+        if not torch.cuda.is_available():
+            raise RuntimeError("no HIP device available: the MI355X hot path has no CPU fallback")
+        self.device = device
+        self._lib = load()
+        h = _P()
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        check(self._lib.fr_create(architecture.encode(), model_type.encode(), idx, int(max_batch), ctypes.byref(h)))
+        self.h = h
+
+    def close(self) -> None:
+        if getattr(self, "h", None) and self._lib is not None:
+            self._lib.fr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- model -------------------------------------------------------------
+    def load_state_dict(self, state_dict) -> None:
+        import numpy as np
+        for k, v in state_dict.items():
+            a = np.ascontiguousarray(np.asarray(v.detach().cpu().numpy() if hasattr(v, "detach") else v),
+                                     dtype=np.float32)
+            check(self._lib.fr_set_param(self.h, k.encode(), a.ctypes.data, a.size), self.h)
+        check(self._lib.fr_finalize(self.h), self.h)
+
+    def embed(self, rgb: torch.Tensor, out: torch.Tensor, normalize: bool = True) -> None:
+        n = rgb.shape[0]
+        check(self._lib.fr_embed(self.h, ptr(rgb), n, rgb.shape[1], rgb.shape[2], ptr(out), int(normalize),
+                                 stream_of(self.device)), self.h)
+
+    # -- gallery -----------------------------------------------------------
+    def gallery_set(self, E: torch.Tensor) -> None:
+        G = E.shape[0] if E.numel() else 0
+        D = E.shape[1] if E.dim() == 2 else 512
+        check(self._lib.fr_gallery_set(self.h, ptr(E) if G else None, G, D, 1, stream_of(self.device)), self.h)
+
+    def match(self, Q: torch.Tensor, k: int, idx: torch.Tensor, score: torch.Tensor) -> None:
+        check(self._lib.fr_match_topk(self.h, ptr(Q), Q.shape[0], int(k), ptr(idx), ptr(score),
+                                      stream_of(self.device)), self.h)
+
+    def embed_match(self, rgb: torch.Tensor, k: int, idx: torch.Tensor, score: torch.Tensor,
+                    emb: Optional[torch.Tensor] = None) -> None:
+        check(self._lib.fr_embed_match(self.h, ptr(rgb), rgb.shape[0], int(k), ptr(idx), ptr(score), ptr(emb),
+                                       stream_of(self.device)), self.h)
+
+    # -- profiling ---------------------------------------------------------
+    def profile_enable(self, on: bool = True) -> None:
+        check(self._lib.fr_profile_enable(self.h, int(on)), self.h)
+
+    def profile_read(self) -> dict:
+        cms, cfl, tms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        cn = ctypes.c_int64()
+        check(self._lib.fr_profile_read(self.h, ctypes.byref(cms), ctypes.byref(cfl), ctypes.byref(cn),
+                                        ctypes.byref(tms)), self.h)
+        return {"conv_ms": cms.value, "conv_flop": cfl.value, "conv_launches": cn.value, "total_ms": tms.value}

@@ -1,0 +1,70 @@
+"""Build recipe for libfrhip.so (gfx950 only), in-tree.
+
+``python -m facerecognitionpipeline_amd.build`` or ``__graft_entry__.build()``.
+Each source compiles to an object under ``build/`` (skipped when its content
+hash and flags are unchanged), then everything links into
+``facerecognitionpipeline_amd/libfrhip.so`` next to this file, so the built
+library travels with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(REPO, "build", "frhip")
+LIB = os.path.join(PKG, "libfrhip.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = "gfx950"
+SOURCES = ["conv_mfma.hip", "embed_misc.hip", "frhip_runtime.cpp"]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+          "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
+LDFLAGS = ["-shared", f"--offload-arch={ARCH}", f"-Wl,-rpath,{ROCM}/lib", "-Wl,--no-undefined"]
+
+
+def _digest(path: str) -> str:
+    h = hashlib.sha256()
+    for p in [path, os.path.join(CSRC, "frhip_kernels.h"), os.path.join(REPO, "include", "frhip.h")]:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(CFLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def _compile(src: str) -> str:
+    path = os.path.join(CSRC, src)
+    obj = os.path.join(BUILD, f"{src}.{_digest(path)}.o")
+    if not os.path.exists(obj):
+        cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", path, "-o", obj + ".tmp"]
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(verbose: bool = True) -> str:
+    """Compile every HIP source for gfx950 and link libfrhip.so; return its path."""
+    os.makedirs(BUILD, exist_ok=True)
+    jobs = min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8")))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    stamp = hashlib.sha256("".join(objs).encode()).hexdigest()[:16]
+    stamp_file = os.path.join(BUILD, "libfrhip.stamp")
+    if os.path.exists(LIB) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:
+        return LIB
+    subprocess.run([HIPCC, *LDFLAGS, *objs, "-o", LIB + ".tmp"], check=True)
+    os.replace(LIB + ".tmp", LIB)
+    with open(stamp_file, "w") as f:
+        f.write(stamp)
+    if verbose:
+        print(f"built {LIB}", file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build()

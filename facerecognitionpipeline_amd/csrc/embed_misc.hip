@@ -1,0 +1,207 @@
+// Stem, head and match-side kernels of the embed + match hot path (gfx950).
+//
+//   stem_kernel        FaceEmbedder.preprocess (face_embedder.py:97-104: RGB->BGR,
+//                      (x/255-0.5)/0.5 in f64 -> f32) fused with net input_layer
+//                      (Conv3x3 3->64 + BN2d + PReLU).  uint8 in, NHWC f32 out.
+//   head_reduce_kernel split-K sum of the Linear(25088,512) partials + bias ->
+//                      BN1d(affine=False) -> x/||x|| (net forward tail) -> optional
+//                      e/(||e||+1e-8) (face_embedder.py:133-134, 177-180).
+//   l2norm_rows_kernel q/(||q||+1e-8) (gallery_manager.py:195).
+//   topk_kernel        argsort(S)[::-1][:k] (gallery_manager.py:197) with the
+//                      documented tie policy: score desc, then index asc.
+#include "frhip_kernels.h"
+
+#include <float.h>
+
+namespace frhip {
+
+constexpr int IMG = 112;
+constexpr int STEM_C = 64;
+
+// One block per (image, output row).  LDS: three LUT-normalised input rows with
+// a zero halo ([3][IMG+2][3] floats) and the [27][64] weights.  Thread t owns 4
+// output channels (t&15) of pixels (t>>4) + 16j: a wave writes 4 pixels x 256 B
+// contiguous, and the weight float4 reads of a wave cover all 64 banks once.
+__global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, const float* __restrict__ lut,
+                                                   const float* __restrict__ w27x64,
+                                                   const float* __restrict__ bn_scale,
+                                                   const float* __restrict__ bn_shift,
+                                                   const float* __restrict__ prelu, float* __restrict__ y) {
+  __shared__ float s_lut[256];
+  __shared__ __attribute__((aligned(16))) float s_w[27 * STEM_C];
+  __shared__ float s_in[3][IMG + 2][3];
+  const int b = blockIdx.x / IMG;
+  const int oy = blockIdx.x - b * IMG;
+  const int tid = threadIdx.x;
+  s_lut[tid] = lut[tid];
+  for (int i = tid; i < 27 * STEM_C; i += 256) s_w[i] = w27x64[i];
+  __syncthreads();
+  for (int i = tid; i < 3 * (IMG + 2) * 3; i += 256) {
+    const int r = i / ((IMG + 2) * 3);
+    const int rem = i - r * (IMG + 2) * 3;
+    const int xx = rem / 3;
+    const int c = rem - xx * 3;
+    const int iy = oy + r - 1, ix = xx - 1;
+    float v = 0.f;
+    if ((unsigned)iy < IMG && (unsigned)ix < IMG) v = s_lut[img[(((long long)b * IMG + iy) * IMG + ix) * 3 + c]];
+    s_in[r][xx][c] = v;
+  }
+  __syncthreads();
+  const int cg = tid & 15;
+  const float4 sc = *reinterpret_cast<const float4*>(bn_scale + 4 * cg);
+  const float4 sh = *reinterpret_cast<const float4*>(bn_shift + 4 * cg);
+  const float4 al = *reinterpret_cast<const float4*>(prelu + 4 * cg);
+  for (int px = tid >> 4; px < IMG; px += 16) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float v = s_in[ky][px + kx][c];
+          const float4 w = *reinterpret_cast<const float4*>(s_w + ((ky * 3 + kx) * 3 + c) * STEM_C + 4 * cg);
+          acc.x = fmaf(v, w.x, acc.x);
+          acc.y = fmaf(v, w.y, acc.y);
+          acc.z = fmaf(v, w.z, acc.z);
+          acc.w = fmaf(v, w.w, acc.w);
+        }
+    float4 o;
+    o.x = acc.x * sc.x + sh.x;
+    o.y = acc.y * sc.y + sh.y;
+    o.z = acc.z * sc.z + sh.z;
+    o.w = acc.w * sc.w + sh.w;
+    o.x = o.x > 0.f ? o.x : o.x * al.x;
+    o.y = o.y > 0.f ? o.y : o.y * al.y;
+    o.z = o.z > 0.f ? o.z : o.z * al.z;
+    o.w = o.w > 0.f ? o.w : o.w * al.w;
+    *reinterpret_cast<float4*>(y + (((long long)b * IMG + oy) * IMG + px) * STEM_C + 4 * cg) = o;
+  }
+}
+
+hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, const float* bn_scale,
+                       const float* bn_shift, const float* prelu, float* y, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(stem_kernel, dim3(B * IMG), dim3(256), 0, s, img, lut, w27x64, bn_scale, bn_shift, prelu, y);
+  return hipGetLastError();
+}
+
+// Block-wide sum over 256 threads (4 waves of 64).
+__device__ __forceinline__ float block_sum_256(float v, float* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int wid = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[wid] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// One block (256 threads, 2 columns each) per embedding row, D = 512.
+__global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restrict__ partial, int nsplit,
+                                                          long long split_stride, const float* __restrict__ fc_bias,
+                                                          const float* __restrict__ bn_scale,
+                                                          const float* __restrict__ bn_shift, float* __restrict__ emb,
+                                                          int normalize) {
+  __shared__ float red[4];
+  const int row = blockIdx.x;
+  const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
+  float v0 = 0.f, v1 = 0.f;
+  const float* p = partial + (long long)row * 512;
+  for (int s = 0; s < nsplit; ++s) {
+    v0 += p[(long long)s * split_stride + c0];
+    v1 += p[(long long)s * split_stride + c1];
+  }
+  v0 += fc_bias[c0];
+  v1 += fc_bias[c1];
+  v0 = v0 * bn_scale[c0] + bn_shift[c0];
+  v1 = v1 * bn_scale[c1] + bn_shift[c1];
+  const float norm = sqrtf(block_sum_256(v0 * v0 + v1 * v1, red));
+  v0 = v0 / norm;
+  v1 = v1 / norm;
+  if (normalize) {
+    const float n2 = sqrtf(block_sum_256(v0 * v0 + v1 * v1, red)) + 1e-8f;
+    v0 = v0 / n2;
+    v1 = v1 / n2;
+  }
+  emb[(long long)row * 512 + c0] = v0;
+  emb[(long long)row * 512 + c1] = v1;
+}
+
+hipError_t launch_head_reduce(const float* partial, int nsplit, long long split_stride, const float* fc_bias,
+                              const float* bn_scale, const float* bn_shift, float* emb, int n, int normalize,
+                              hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(n), dim3(256), 0, s, partial, nsplit, split_stride, fc_bias, bn_scale,
+                     bn_shift, emb, normalize);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void l2norm_rows_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                          int d) {
+  __shared__ float red[4];
+  const float* r = q + (long long)blockIdx.x * d;
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < d; c += 256) ss += r[c] * r[c];
+  const float nrm = sqrtf(block_sum_256(ss, red)) + 1e-8f;
+  for (int c = threadIdx.x; c < d; c += 256) out[(long long)blockIdx.x * d + c] = r[c] / nrm;
+}
+
+hipError_t launch_l2norm_rows(const float* q, float* out, int n, int d, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(l2norm_rows_kernel, dim3(n), dim3(256), 0, s, q, out, d);
+  return hipGetLastError();
+}
+
+// (score, index) total order: a before b  <=>  a.s > b.s || (a.s == b.s && a.i < b.i).
+__device__ __forceinline__ bool ranks_before(float sa, int ia, float sb, int ib) {
+  return sa > sb || (sa == sb && ia < ib);
+}
+
+// One wave per score row; k selection passes, each a strided scan for the best
+// element ranked strictly after the previous pick, then a wave arg-reduction.
+// Exact and order-independent (the result never depends on scan order).
+__global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ scores, int n, int G, int k,
+                                                   int32_t* __restrict__ idx, float* __restrict__ val) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const int lane = threadIdx.x & 63;
+  const float* r = scores + (long long)row * G;
+  float prev_s = INFINITY;
+  int prev_i = -1;
+  for (int t = 0; t < k; ++t) {
+    float bs = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int g = lane; g < G; g += 64) {
+      const float s = r[g];
+      if (s != s) continue;  // NaN never ranks
+      if (ranks_before(prev_s, prev_i, s, g) && ranks_before(s, g, bs, bi)) {
+        bs = s;
+        bi = g;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float os = __shfl_xor(bs, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ranks_before(os, oi, bs, bi)) {
+        bs = os;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      idx[(long long)row * k + t] = bi == 0x7fffffff ? -1 : bi;
+      val[(long long)row * k + t] = bs;
+    }
+    prev_s = bs;
+    prev_i = bi;
+  }
+}
+
+hipError_t launch_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, hipStream_t s) {
+  if (n <= 0 || k <= 0) return hipSuccess;
+  hipLaunchKernelGGL(topk_kernel, dim3((n + 3) / 4), dim3(256), 0, s, scores, n, G, k, idx, val);
+  return hipGetLastError();
+}
+
+}  // namespace frhip

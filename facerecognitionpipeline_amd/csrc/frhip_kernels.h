@@ -1,0 +1,61 @@
+// Internal kernel launch interface for libfrhip (not part of the public C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace frhip {
+
+// Epilogue of the implicit-GEMM conv kernel.
+enum Epi : int {
+  EPI_AFFINE = 0,        // y = acc*scale + shift                      (shortcut conv1x1 + BN)
+  EPI_AFFINE_PRELU = 1,  // y = prelu(acc*scale + shift)               (conv1 + BN + PReLU)
+  EPI_AFFINE_RES = 2,    // y = acc*scale + shift + res[m]             (conv2 + BN + identity / conv shortcut)
+  EPI_AFFINE_RES_SUB = 3,// y = acc*scale + shift + res[b, 2oy, 2ox]   (conv2 + BN + MaxPool2d(1,2) shortcut)
+  EPI_RAW = 4,           // y[split] = acc                             (split-K partial / gallery scores)
+};
+
+// One convolution (or GEMM, as a 1x1 conv over a 1x1 image) in NHWC f32.
+//   x   [B][H][W][Cin]         w [Cout][KH][KW][Cin]        y [B][Ho][Wo][Cout]
+// pre_scale/pre_shift: per-Cin affine applied to in-bounds input taps only (the
+// pre-activation BatchNorm in front of a zero-padded conv), may be null.
+struct ConvParams {
+  const float* x;
+  const float* w;
+  float* y;
+  const float* pre_scale;
+  const float* pre_shift;
+  const float* post_scale;
+  const float* post_shift;
+  const float* prelu;
+  const float* res;
+  int B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad;
+  int res_H, res_W;
+  int M;                 // B*Ho*Wo
+  int steps_total;       // KH*KW*Cin / 32
+  int steps_per_split;   // K-steps per blockIdx.y slice
+  long long split_stride;// elements between split-K partial slabs
+  int mtiles, ntiles;
+};
+
+// Tile family of a conv launch.
+enum ConvTile : int { TILE_256x64 = 0, TILE_128x128 = 1 };
+
+hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s);
+
+// uint8 RGB HWC 112x112 -> (BGR, LUT normalise) -> conv3x3 3->64 -> BN -> PReLU, NHWC f32.
+hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64,
+                       const float* bn_scale, const float* bn_shift, const float* prelu,
+                       float* y, hipStream_t s);
+
+// Sum split-K partials + FC bias -> BN1d(affine=False) -> x/||x|| -> optional e/(||e||+1e-8).
+hipError_t launch_head_reduce(const float* partial, int nsplit, long long split_stride,
+                              const float* fc_bias, const float* bn_scale, const float* bn_shift,
+                              float* emb, int n, int normalize, hipStream_t s);
+
+// q / (||q|| + 1e-8) row-wise over D=512 rows.
+hipError_t launch_l2norm_rows(const float* q, float* out, int n, int d, hipStream_t s);
+
+// Per row of a [n][G] score matrix: top-k by (score desc, index asc).
+hipError_t launch_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, hipStream_t s);
+
+}  // namespace frhip

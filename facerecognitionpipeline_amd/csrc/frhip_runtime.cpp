@@ -1,0 +1,796 @@
+// libfrhip runtime: handle, state-dict ingestion + BatchNorm folding, the IR
+// forward executor and the gallery matcher behind the C ABI of include/frhip.h.
+//
+// Host-side C++ (compiled by hipcc for the HIP runtime API only).  What it
+// replaces in the reference:
+//   FaceEmbedder.__init__/load_state_dict   face_embedder.py:27-62
+//   FaceEmbedder.extract_embeddings_batch   face_embedder.py:137-182 (A3)
+//   GalleryManager.get_gallery_embeddings   gallery_manager.py:177-187 (A10)
+//   GalleryManager.search                   gallery_manager.py:189-205 (A11)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/frhip.h"
+#include "../../include/frhip_testing.h"
+#include "frhip_kernels.h"
+
+using namespace frhip;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct BlockSpec {
+  int cin, depth, stride;
+};
+
+std::vector<BlockSpec> block_specs(const std::string& arch, bool* ok) {
+  int units[4];
+  *ok = true;
+  if (arch == "ir_50") {
+    int u[4] = {3, 4, 14, 3};
+    memcpy(units, u, sizeof(u));
+  } else if (arch == "ir_101") {
+    int u[4] = {3, 13, 30, 3};
+    memcpy(units, u, sizeof(u));
+  } else if (arch == "ir_34") {
+    int u[4] = {3, 4, 6, 3};
+    memcpy(units, u, sizeof(u));
+  } else if (arch == "ir_18") {
+    int u[4] = {2, 2, 2, 2};
+    memcpy(units, u, sizeof(u));
+  } else {
+    *ok = false;
+    return {};
+  }
+  const int widths[4] = {64, 128, 256, 512};
+  std::vector<BlockSpec> v;
+  int in = 64;
+  for (int s = 0; s < 4; ++s) {
+    v.push_back({in, widths[s], 2});
+    for (int u = 1; u < units[s]; ++u) v.push_back({widths[s], widths[s], 1});
+    in = widths[s];
+  }
+  return v;
+}
+
+// Device-side folded parameters of one conv.
+struct ConvW {
+  float* w = nullptr;  // [Cout][KH][KW][Cin]
+  float* pre_scale = nullptr;
+  float* pre_shift = nullptr;
+  float* post_scale = nullptr;
+  float* post_shift = nullptr;
+  float* prelu = nullptr;
+  int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
+};
+
+struct BlockW {
+  BlockSpec spec;
+  ConvW conv1, conv2, sc;
+  bool has_sc_conv = false;
+};
+
+struct ProfEvent {
+  hipEvent_t a, b;
+  double flop;
+  bool conv;
+};
+
+}  // namespace
+
+struct fr_handle {
+  std::mutex mu;
+  std::string arch, model_type, err;
+  int device = 0;
+  int max_batch = 256;
+  bool finalized = false;
+  std::vector<BlockSpec> specs;
+  std::map<std::string, size_t> expected;  // key -> numel
+  std::map<std::string, std::vector<float>> params;
+
+  // device arena with every folded weight
+  float* arena = nullptr;
+  size_t arena_floats = 0;
+  float *lut = nullptr, *stem_w = nullptr, *stem_scale = nullptr, *stem_shift = nullptr, *stem_prelu = nullptr;
+  std::vector<BlockW> blocks;
+  ConvW head;  // BN2d pre-affine + FC as 7x7 valid conv
+  float *fc_bias = nullptr, *bn1d_scale = nullptr, *bn1d_shift = nullptr;
+
+  // workspace
+  float *act[3] = {nullptr, nullptr, nullptr};
+  float* sc_buf = nullptr;
+  float* partial = nullptr;
+  int head_split = 49;
+  uint8_t* in_stage = nullptr;
+  float* emb_stage = nullptr;
+
+  // gallery + match workspace
+  float* gallery = nullptr;
+  int G = 0;
+  size_t gallery_cap = 0;
+  float* qn = nullptr;
+  size_t qn_cap = 0;
+  float* scores = nullptr;
+  size_t scores_cap = 0;
+  void* match_io = nullptr;
+  size_t match_io_cap = 0;
+
+  // profiling
+  bool prof = false;
+  std::vector<ProfEvent> events;
+  std::vector<hipEvent_t> pool;
+
+  ~fr_handle() {
+    for (auto& e : events) {
+      (void)hipEventDestroy(e.a);
+      (void)hipEventDestroy(e.b);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+    (void)hipFree(arena);
+    for (auto p : act) (void)hipFree(p);
+    (void)hipFree(sc_buf);
+    (void)hipFree(partial);
+    (void)hipFree(in_stage);
+    (void)hipFree(emb_stage);
+    (void)hipFree(gallery);
+    (void)hipFree(qn);
+    (void)hipFree(scores);
+    (void)hipFree(match_io);
+  }
+};
+
+namespace {
+
+int fail(fr_handle* h, int code, const std::string& msg) {
+  if (h)
+    h->err = msg;
+  else
+    g_create_error = msg;
+  return code;
+}
+
+#define FR_HIP(h, call)                                                                          \
+  do {                                                                                           \
+    hipError_t e_ = (call);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return fail(h, FR_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));             \
+  } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+void add_bn(std::map<std::string, size_t>& m, const std::string& p, int c, bool affine = true) {
+  if (affine) {
+    m[p + ".weight"] = c;
+    m[p + ".bias"] = c;
+  }
+  m[p + ".running_mean"] = c;
+  m[p + ".running_var"] = c;
+  m[p + ".num_batches_tracked"] = 1;
+}
+
+std::map<std::string, size_t> schema(const std::vector<BlockSpec>& specs) {
+  std::map<std::string, size_t> m;
+  m["input_layer.0.weight"] = 64 * 3 * 9;
+  add_bn(m, "input_layer.1", 64);
+  m["input_layer.2.weight"] = 64;
+  add_bn(m, "output_layer.0", 512);
+  m["output_layer.3.weight"] = (size_t)512 * 512 * 49;
+  m["output_layer.3.bias"] = 512;
+  add_bn(m, "output_layer.4", 512, false);
+  for (size_t i = 0; i < specs.size(); ++i) {
+    const auto& s = specs[i];
+    const std::string p = "body." + std::to_string(i) + ".";
+    if (s.cin != s.depth) {
+      m[p + "shortcut_layer.0.weight"] = (size_t)s.depth * s.cin;
+      add_bn(m, p + "shortcut_layer.1", s.depth);
+    }
+    add_bn(m, p + "res_layer.0", s.cin);
+    m[p + "res_layer.1.weight"] = (size_t)s.depth * s.cin * 9;
+    add_bn(m, p + "res_layer.2", s.depth);
+    m[p + "res_layer.3.weight"] = s.depth;
+    m[p + "res_layer.4.weight"] = (size_t)s.depth * s.depth * 9;
+    add_bn(m, p + "res_layer.5", s.depth);
+  }
+  return m;
+}
+
+// Host staging of every folded tensor before one upload into the arena.
+struct Packer {
+  std::vector<float> buf;
+  std::vector<std::pair<float**, size_t>> fix;  // (destination pointer, float offset)
+  void put(float** dst, const std::vector<float>& v) {
+    size_t off = (buf.size() + 3) & ~size_t(3);  // 16-B alignment for float4 loads
+    buf.resize(off);
+    buf.insert(buf.end(), v.begin(), v.end());
+    fix.push_back({dst, off});
+  }
+};
+
+// PyTorch CPU eval BatchNorm computes alpha = gamma/sqrt(var+eps), beta = bias - mean*alpha
+// in the input dtype and applies x*alpha + beta (ATen batch_norm_cpu_collect_linear_and_constant_terms).
+void bn_fold(const std::vector<float>* gamma, const std::vector<float>* beta, const std::vector<float>& mean,
+             const std::vector<float>& var, std::vector<float>& scale, std::vector<float>& shift) {
+  const size_t c = mean.size();
+  scale.resize(c);
+  shift.resize(c);
+  for (size_t i = 0; i < c; ++i) {
+    const float invstd = 1.0f / std::sqrt(var[i] + 1e-5f);
+    const float g = gamma ? (*gamma)[i] : 1.0f;
+    const float b = beta ? (*beta)[i] : 0.0f;
+    scale[i] = invstd * g;
+    shift[i] = b - mean[i] * scale[i];
+  }
+}
+
+// [O][I][kh][kw] -> [O][kh][kw][I]
+std::vector<float> repack_oihw(const std::vector<float>& w, int O, int I, int kh, int kw) {
+  std::vector<float> r((size_t)O * I * kh * kw);
+  for (int o = 0; o < O; ++o)
+    for (int i = 0; i < I; ++i)
+      for (int y = 0; y < kh; ++y)
+        for (int x = 0; x < kw; ++x)
+          r[(((size_t)o * kh + y) * kw + x) * I + i] = w[(((size_t)o * I + i) * kh + y) * kw + x];
+  return r;
+}
+
+int ensure_buf(fr_handle* h, void** p, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return FR_OK;
+  if (*p) FR_HIP(h, hipFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  FR_HIP(h, hipMalloc(p, bytes));
+  *cap = bytes;
+  return FR_OK;
+}
+
+hipEvent_t take_event(fr_handle* h) {
+  if (!h->pool.empty()) {
+    hipEvent_t e = h->pool.back();
+    h->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+struct ProfScope {
+  fr_handle* h;
+  hipStream_t s;
+  ProfEvent ev{};
+  bool on;
+  ProfScope(fr_handle* h_, hipStream_t s_, double flop, bool conv) : h(h_), s(s_), on(h_->prof) {
+    if (!on) return;
+    ev.a = take_event(h);
+    ev.b = take_event(h);
+    ev.flop = flop;
+    ev.conv = conv;
+    if (!ev.a || !ev.b) {
+      on = false;
+      return;
+    }
+    (void)hipEventRecord(ev.a, s);
+  }
+  ~ProfScope() {
+    if (!on) return;
+    (void)hipEventRecord(ev.b, s);
+    h->events.push_back(ev);
+  }
+};
+
+int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
+             const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s) {
+  ConvParams p{};
+  p.x = x;
+  p.w = cw.w;
+  p.y = y;
+  p.pre_scale = cw.pre_scale;
+  p.pre_shift = cw.pre_shift;
+  p.post_scale = cw.post_scale;
+  p.post_shift = cw.post_shift;
+  p.prelu = cw.prelu;
+  p.res = res;
+  p.B = B;
+  p.H = H;
+  p.W = W;
+  p.Cin = cw.cin;
+  p.Cout = cw.cout;
+  p.KH = cw.kh;
+  p.KW = cw.kw;
+  p.stride = cw.stride;
+  p.pad = cw.pad;
+  p.Ho = (H + 2 * cw.pad - cw.kh) / cw.stride + 1;
+  p.Wo = (W + 2 * cw.pad - cw.kw) / cw.stride + 1;
+  p.res_H = res_H;
+  p.res_W = res_W;
+  p.M = B * p.Ho * p.Wo;
+  p.steps_total = cw.kh * cw.kw * cw.cin / 32;
+  p.steps_per_split = (p.steps_total + nsplit - 1) / nsplit;
+  p.split_stride = split_stride;
+  const double flop = 2.0 * p.M * (double)p.Cout * cw.kh * cw.kw * cw.cin;
+  const ConvTile tile = cw.cout <= 64 ? TILE_256x64 : TILE_128x128;
+  ProfScope ps(h, s, flop, true);
+  hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s);
+  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+// One forward of up to max_batch crops: rgb (device) -> out (device) [n][512].
+int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int normalize, hipStream_t s) {
+  {
+    ProfScope ps(h, s, 2.0 * n * 112.0 * 112.0 * 64 * 27, false);
+    hipError_t e = launch_stem(rgb, n, h->lut, h->stem_w, h->stem_scale, h->stem_shift, h->stem_prelu, h->act[0], s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("stem launch: ") + hipGetErrorString(e));
+  }
+  int cur = 0, HW = 112;
+  for (const auto& b : h->blocks) {
+    const int nxt = cur == 0 ? 1 : 0;
+    float* x = h->act[cur];
+    float* r = h->act[2];
+    float* y = h->act[nxt];
+    int rc = run_conv(h, b.conv1, x, r, n, HW, HW, EPI_AFFINE_PRELU, nullptr, 0, 0, 1, 0, s);
+    if (rc) return rc;
+    const int Ho = HW / b.spec.stride;
+    if (b.has_sc_conv) {
+      rc = run_conv(h, b.sc, x, h->sc_buf, n, HW, HW, EPI_AFFINE, nullptr, 0, 0, 1, 0, s);
+      if (rc) return rc;
+      rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES, h->sc_buf, Ho, Ho, 1, 0, s);
+    } else if (b.spec.stride == 1) {
+      rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES, x, HW, HW, 1, 0, s);
+    } else {
+      rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES_SUB, x, HW, HW, 1, 0, s);
+    }
+    if (rc) return rc;
+    cur = nxt;
+    HW = Ho;
+  }
+  const long long split_stride = (long long)n * 512;
+  int rc = run_conv(h, h->head, h->act[cur], h->partial, n, 7, 7, EPI_RAW, nullptr, 0, 0, h->head_split,
+                    split_stride, s);
+  if (rc) return rc;
+  ProfScope ps(h, s, 0.0, false);
+  hipError_t e = launch_head_reduce(h->partial, h->head_split, split_stride, h->fc_bias, h->bn1d_scale,
+                                    h->bn1d_shift, out, n, normalize, s);
+  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("head launch: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+int embed_device(fr_handle* h, const uint8_t* rgb, int n, float* out, int normalize, hipStream_t s) {
+  for (int off = 0; off < n; off += h->max_batch) {
+    const int bn = std::min(h->max_batch, n - off);
+    int rc = forward_chunk(h, rgb + (size_t)off * 112 * 112 * 3, bn, out + (size_t)off * 512, normalize, s);
+    if (rc) return rc;
+  }
+  return FR_OK;
+}
+
+int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float* score, hipStream_t s) {
+  if (h->G <= 0) return fail(h, FR_ERR_STATE, "gallery is empty (fr_gallery_set first)");
+  if (k < 1 || k > h->G) return fail(h, FR_ERR_INVALID_ARGUMENT, "k must be in [1, G]");
+  if (n <= 0) return FR_OK;
+  int rc = ensure_buf(h, (void**)&h->qn, &h->qn_cap, (size_t)n * 512 * sizeof(float));
+  if (rc) return rc;
+  rc = ensure_buf(h, (void**)&h->scores, &h->scores_cap, (size_t)n * h->G * sizeof(float));
+  if (rc) return rc;
+  {
+    ProfScope ps(h, s, 0.0, false);
+    hipError_t e = launch_l2norm_rows(Q, h->qn, n, 512, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("l2norm launch: ") + hipGetErrorString(e));
+  }
+  ConvW g;
+  g.w = h->gallery;
+  g.cin = 512;
+  g.cout = h->G;
+  g.kh = g.kw = 1;
+  g.stride = 1;
+  g.pad = 0;
+  rc = run_conv(h, g, h->qn, h->scores, n, 1, 1, EPI_RAW, nullptr, 0, 0, 1, 0, s);
+  if (rc) return rc;
+  ProfScope ps(h, s, 0.0, false);
+  hipError_t e = launch_topk(h->scores, n, h->G, k, idx, score, s);
+  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("topk launch: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+const std::vector<float>* getp(fr_handle* h, const std::string& k) {
+  auto it = h->params.find(k);
+  return it == h->params.end() ? nullptr : &it->second;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fr_create(const char* architecture, const char* model_type, int device, int max_batch, fr_handle** out) {
+  if (!out) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  const std::string arch = architecture ? architecture : "";
+  const std::string mt = model_type ? model_type : "";
+  bool ok = false;
+  auto specs = block_specs(arch, &ok);
+  if (!ok)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT,
+                "Unknown architecture: " + arch + ". Available: ['ir_50', 'ir_101']");
+  if (mt == "arcface")
+    return fail(nullptr, FR_ERR_UNSUPPORTED, "model_type 'arcface' (ONNX/onnxruntime path) is not implemented");
+  if (mt != "adaface")
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "Unknown model_type: " + mt + ". Must be 'adaface' or 'arcface'");
+  if (max_batch < 1 || max_batch > 2048)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "max_batch must be in [1, 2048]");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(nullptr, FR_ERR_HIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "device index out of range");
+  auto h = std::make_unique<fr_handle>();
+  h->arch = arch;
+  h->model_type = mt;
+  h->device = device;
+  h->max_batch = max_batch;
+  h->specs = specs;
+  h->expected = schema(specs);
+  *out = h.release();
+  return FR_OK;
+}
+
+int fr_destroy(fr_handle* h) {
+  if (!h) return FR_OK;
+  {
+    DeviceGuard g(h->device);
+    (void)hipDeviceSynchronize();
+    delete h;
+  }
+  return FR_OK;
+}
+
+int fr_set_param(fr_handle* h, const char* name, const float* host_data, int64_t numel) {
+  if (!h || !name) return fail(h, FR_ERR_INVALID_ARGUMENT, "NULL argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  const std::string k = name;
+  auto it = h->expected.find(k);
+  if (it == h->expected.end()) return fail(h, FR_ERR_INVALID_ARGUMENT, "Unexpected key(s) in state_dict: \"" + k + "\"");
+  if (k.size() > 20 && k.compare(k.size() - 20, 20, ".num_batches_tracked") == 0) return FR_OK;
+  if (numel != (int64_t)it->second || (!host_data && numel > 0))
+    return fail(h, FR_ERR_INVALID_ARGUMENT,
+                "size mismatch for " + k + ": expected " + std::to_string(it->second) + " elements, got " +
+                    std::to_string(numel));
+  h->params[k].assign(host_data, host_data + numel);
+  h->finalized = false;
+  return FR_OK;
+}
+
+int fr_finalize(fr_handle* h) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  std::string missing;
+  for (const auto& kv : h->expected) {
+    if (kv.first.size() > 20 && kv.first.compare(kv.first.size() - 20, 20, ".num_batches_tracked") == 0) continue;
+    if (!h->params.count(kv.first)) missing += (missing.empty() ? "\"" : ", \"") + kv.first + "\"";
+  }
+  if (!missing.empty()) return fail(h, FR_ERR_MISSING_PARAM, "Missing key(s) in state_dict: " + missing);
+  DeviceGuard dg(h->device);
+
+  Packer pk;
+  std::vector<float> sc, sh;
+  auto P = [&](const std::string& k) -> const std::vector<float>& { return *getp(h, k); };
+  auto bn = [&](const std::string& p, float** dsc, float** dsh, bool affine = true) {
+    bn_fold(affine ? &P(p + ".weight") : nullptr, affine ? &P(p + ".bias") : nullptr, P(p + ".running_mean"),
+            P(p + ".running_var"), sc, sh);
+    pk.put(dsc, sc);
+    pk.put(dsh, sh);
+  };
+
+  // preprocessing LUT: float32((v/255.0 - 0.5)/0.5) in float64 (face_embedder.py:99-101)
+  std::vector<float> lut(256);
+  for (int v = 0; v < 256; ++v) lut[v] = (float)((v / 255.0 - 0.5) / 0.5);
+  pk.put(&h->lut, lut);
+  // stem: [64][3][3][3] (BGR channel order) -> [ky][kx][c_rgb][64]
+  {
+    const auto& w = P("input_layer.0.weight");
+    std::vector<float> r(27 * 64);
+    for (int o = 0; o < 64; ++o)
+      for (int c = 0; c < 3; ++c)
+        for (int y = 0; y < 3; ++y)
+          for (int x = 0; x < 3; ++x) r[((y * 3 + x) * 3 + (2 - c)) * 64 + o] = w[((o * 3 + c) * 3 + y) * 3 + x];
+    pk.put(&h->stem_w, r);
+    bn("input_layer.1", &h->stem_scale, &h->stem_shift);
+    pk.put(&h->stem_prelu, P("input_layer.2.weight"));
+  }
+  h->blocks.assign(h->specs.size(), BlockW{});
+  for (size_t i = 0; i < h->specs.size(); ++i) {
+    const auto& s = h->specs[i];
+    BlockW& b = h->blocks[i];
+    b.spec = s;
+    const std::string p = "body." + std::to_string(i) + ".";
+    b.conv1.cin = s.cin;
+    b.conv1.cout = s.depth;
+    b.conv1.kh = b.conv1.kw = 3;
+    b.conv1.stride = 1;
+    b.conv1.pad = 1;
+    pk.put(&b.conv1.w, repack_oihw(P(p + "res_layer.1.weight"), s.depth, s.cin, 3, 3));
+    bn(p + "res_layer.0", &b.conv1.pre_scale, &b.conv1.pre_shift);
+    bn(p + "res_layer.2", &b.conv1.post_scale, &b.conv1.post_shift);
+    pk.put(&b.conv1.prelu, P(p + "res_layer.3.weight"));
+    b.conv2.cin = s.depth;
+    b.conv2.cout = s.depth;
+    b.conv2.kh = b.conv2.kw = 3;
+    b.conv2.stride = s.stride;
+    b.conv2.pad = 1;
+    pk.put(&b.conv2.w, repack_oihw(P(p + "res_layer.4.weight"), s.depth, s.depth, 3, 3));
+    bn(p + "res_layer.5", &b.conv2.post_scale, &b.conv2.post_shift);
+    if (s.cin != s.depth) {
+      b.has_sc_conv = true;
+      b.sc.cin = s.cin;
+      b.sc.cout = s.depth;
+      b.sc.kh = b.sc.kw = 1;
+      b.sc.stride = s.stride;
+      b.sc.pad = 0;
+      pk.put(&b.sc.w, P(p + "shortcut_layer.0.weight"));  // [O][I][1][1] == [O][1][1][I]
+      bn(p + "shortcut_layer.1", &b.sc.post_scale, &b.sc.post_shift);
+    }
+  }
+  // head: BN2d(512) as pre-affine; Linear(25088,512) with NCHW-flatten columns
+  // (c*49 + y*7 + x) permuted to NHWC taps ((y*7 + x)*512 + c).
+  {
+    h->head.cin = 512;
+    h->head.cout = 512;
+    h->head.kh = h->head.kw = 7;
+    h->head.stride = 1;
+    h->head.pad = 0;
+    const auto& w = P("output_layer.3.weight");
+    std::vector<float> r((size_t)512 * 25088);
+    for (int o = 0; o < 512; ++o)
+      for (int c = 0; c < 512; ++c)
+        for (int t = 0; t < 49; ++t) r[(size_t)o * 25088 + (size_t)t * 512 + c] = w[(size_t)o * 25088 + (size_t)c * 49 + t];
+    pk.put(&h->head.w, r);
+    bn("output_layer.0", &h->head.pre_scale, &h->head.pre_shift);
+    pk.put(&h->fc_bias, P("output_layer.3.bias"));
+    bn("output_layer.4", &h->bn1d_scale, &h->bn1d_shift, false);
+  }
+
+  if (h->arena) FR_HIP(h, hipFree(h->arena));
+  h->arena = nullptr;
+  FR_HIP(h, hipMalloc((void**)&h->arena, pk.buf.size() * sizeof(float)));
+  FR_HIP(h, hipMemcpy(h->arena, pk.buf.data(), pk.buf.size() * sizeof(float), hipMemcpyHostToDevice));
+  h->arena_floats = pk.buf.size();
+  for (auto& f : pk.fix) *f.first = h->arena + f.second;
+
+  // workspace for max_batch crops
+  const size_t mb = h->max_batch;
+  if (!h->act[0]) {
+    for (auto& a : h->act) FR_HIP(h, hipMalloc((void**)&a, mb * 112 * 112 * 64 * sizeof(float)));
+    FR_HIP(h, hipMalloc((void**)&h->sc_buf, mb * 28 * 28 * 128 * sizeof(float)));
+    FR_HIP(h, hipMalloc((void**)&h->partial, (size_t)h->head_split * mb * 512 * sizeof(float)));
+    FR_HIP(h, hipMalloc((void**)&h->in_stage, mb * 112 * 112 * 3));
+    FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
+  }
+  h->finalized = true;
+  return FR_OK;
+}
+
+int fr_embed(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize,
+             void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
+  if (height != 112 || width != 112)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "input must be 112x112x3 (resize is done by the caller)");
+  if (n < 0 || (n > 0 && (!rgb || !out))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
+  DeviceGuard dg(h->device);
+  return embed_device(h, rgb, n, out, normalize, (hipStream_t)stream);
+}
+
+int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
+  if (height != 112 || width != 112)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "input must be 112x112x3 (resize is done by the caller)");
+  if (n < 0 || (n > 0 && (!rgb || !out))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
+  DeviceGuard dg(h->device);
+  hipStream_t s = nullptr;
+  for (int off = 0; off < n; off += h->max_batch) {
+    const int bn = std::min(h->max_batch, n - off);
+    FR_HIP(h, hipMemcpyAsync(h->in_stage, rgb + (size_t)off * 112 * 112 * 3, (size_t)bn * 112 * 112 * 3,
+                             hipMemcpyHostToDevice, s));
+    int rc = forward_chunk(h, h->in_stage, bn, h->emb_stage, normalize, s);
+    if (rc) return rc;
+    FR_HIP(h, hipMemcpyAsync(out + (size_t)off * 512, h->emb_stage, (size_t)bn * 512 * sizeof(float),
+                             hipMemcpyDeviceToHost, s));
+  }
+  FR_HIP(h, hipStreamSynchronize(s));
+  return FR_OK;
+}
+
+int fr_gallery_set(fr_handle* h, const float* E, int G, int D, int src_is_device, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (G < 0 || (G > 0 && !E)) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad gallery");
+  if (G > 0 && D != 512) return fail(h, FR_ERR_INVALID_ARGUMENT, "gallery rows must be 512-d");
+  DeviceGuard dg(h->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (G == 0) {
+    h->G = 0;
+    return FR_OK;
+  }
+  void* p = h->gallery;
+  int rc = ensure_buf(h, &p, &h->gallery_cap, (size_t)G * 512 * sizeof(float));
+  h->gallery = (float*)p;
+  if (rc) return rc;
+  FR_HIP(h, hipMemcpyAsync(h->gallery, E, (size_t)G * 512 * sizeof(float),
+                           src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  if (!src_is_device) FR_HIP(h, hipStreamSynchronize(s));
+  h->G = G;
+  return FR_OK;
+}
+
+int fr_gallery_size(fr_handle* h, int* G) {
+  if (!h || !G) return fail(h, FR_ERR_INVALID_ARGUMENT, "NULL argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  *G = h->G;
+  return FR_OK;
+}
+
+int fr_match_topk(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float* score, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < 0 || (n > 0 && (!Q || !idx || !score))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
+  DeviceGuard dg(h->device);
+  return match_device(h, Q, n, k, idx, score, (hipStream_t)stream);
+}
+
+int fr_match_topk_host(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float* score) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < 0 || (n > 0 && (!Q || !idx || !score))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
+  if (n == 0) return FR_OK;
+  if (k < 1 || k > h->G) return fail(h, FR_ERR_INVALID_ARGUMENT, "k must be in [1, G]");
+  DeviceGuard dg(h->device);
+  hipStream_t s = nullptr;
+  const size_t qb = (size_t)n * 512 * sizeof(float), rb = (size_t)n * k * 4;
+  int rc = ensure_buf(h, &h->match_io, &h->match_io_cap, qb + 2 * rb);
+  if (rc) return rc;
+  char* base = (char*)h->match_io;
+  float* dq = (float*)base;
+  int32_t* di = (int32_t*)(base + qb);
+  float* ds = (float*)(base + qb + rb);
+  FR_HIP(h, hipMemcpyAsync(dq, Q, qb, hipMemcpyHostToDevice, s));
+  rc = match_device(h, dq, n, k, di, ds, s);
+  if (rc) return rc;
+  FR_HIP(h, hipMemcpyAsync(idx, di, rb, hipMemcpyDeviceToHost, s));
+  FR_HIP(h, hipMemcpyAsync(score, ds, rb, hipMemcpyDeviceToHost, s));
+  FR_HIP(h, hipStreamSynchronize(s));
+  return FR_OK;
+}
+
+int fr_embed_match(fr_handle* h, const uint8_t* rgb, int n, int k, int32_t* idx, float* score, float* emb_out,
+                   void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
+  if (n < 0 || (n > 0 && (!rgb || !idx || !score))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
+  if (h->G <= 0) return fail(h, FR_ERR_STATE, "gallery is empty (fr_gallery_set first)");
+  DeviceGuard dg(h->device);
+  hipStream_t s = (hipStream_t)stream;
+  float* emb = emb_out;
+  if (!emb) {
+    int rc = ensure_buf(h, &h->match_io, &h->match_io_cap, (size_t)n * 512 * sizeof(float));
+    if (rc) return rc;
+    emb = (float*)h->match_io;
+  }
+  int rc = embed_device(h, rgb, n, emb, 1, s);
+  if (rc) return rc;
+  return match_device(h, emb, n, k, idx, score, s);
+}
+
+int fr_profile_enable(fr_handle* h, int enable) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->prof = enable != 0;
+  return FR_OK;
+}
+
+int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* conv_launches, double* total_ms) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  DeviceGuard dg(h->device);
+  double cms = 0, cfl = 0, tms = 0;
+  int64_t cn = 0;
+  for (auto& e : h->events) {
+    FR_HIP(h, hipEventSynchronize(e.b));
+    float ms = 0.f;
+    FR_HIP(h, hipEventElapsedTime(&ms, e.a, e.b));
+    tms += ms;
+    if (e.conv) {
+      cms += ms;
+      cfl += e.flop;
+      ++cn;
+    }
+    h->pool.push_back(e.a);
+    h->pool.push_back(e.b);
+  }
+  h->events.clear();
+  if (conv_ms) *conv_ms = cms;
+  if (conv_flop) *conv_flop = cfl;
+  if (conv_launches) *conv_launches = cn;
+  if (total_ms) *total_ms = tms;
+  return FR_OK;
+}
+
+const char* fr_last_error(fr_handle* h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+const char* fr_version(void) { return "frhip 0.1 gfx950 fp32-mfma"; }
+
+int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout, int kh, int kw,
+               int stride, int pad, const float* pre_scale, const float* pre_shift, const float* post_scale,
+               const float* post_shift, const float* prelu, const float* res, int res_h, int res_w, int epi,
+               int nsplit, int tile, void* stream) {
+  if (epi < 0 || epi > 4 || nsplit < 1 || (nsplit > 1 && epi != EPI_RAW) || (tile != 0 && tile != 1) ||
+      stride < 1 || kh < 1 || kw < 1 || B < 1)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d: bad arguments");
+  ConvParams p{};
+  p.x = x;
+  p.w = w;
+  p.y = y;
+  p.pre_scale = pre_scale;
+  p.pre_shift = pre_shift;
+  p.post_scale = post_scale;
+  p.post_shift = post_shift;
+  p.prelu = prelu;
+  p.res = res;
+  p.B = B;
+  p.H = H;
+  p.W = W;
+  p.Cin = cin;
+  p.Cout = cout;
+  p.KH = kh;
+  p.KW = kw;
+  p.stride = stride;
+  p.pad = pad;
+  p.Ho = (H + 2 * pad - kh) / stride + 1;
+  p.Wo = (W + 2 * pad - kw) / stride + 1;
+  p.res_H = res_h;
+  p.res_W = res_w;
+  p.M = B * p.Ho * p.Wo;
+  p.steps_total = kh * kw * cin / 32;
+  p.steps_per_split = (p.steps_total + nsplit - 1) / nsplit;
+  p.split_stride = (long long)p.M * cout;
+  hipError_t e = launch_conv(p, (ConvTile)tile, pre_scale != nullptr, (Epi)epi, nsplit, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+int frt_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, const float* bn_scale,
+             const float* bn_shift, const float* prelu, float* y, void* stream) {
+  hipError_t e = launch_stem(img, B, lut, w27x64, bn_scale, bn_shift, prelu, y, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_stem: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, void* stream) {
+  if (k < 1 || k > G) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_topk: k must be in [1, G]");
+  hipError_t e = launch_topk(scores, n, G, k, idx, val, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_topk: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,151 @@
+"""Drop-in ``FaceEmbedder`` backed by the gfx950 HIP path (libfrhip).
+
+Mirrors the reference class ``face_embedder.FaceEmbedder``
+(``face_embedder.py:26-225``): same constructor arguments, method names,
+return types and exceptions.  The forward runs entirely on the GPU: the
+uint8 crops go to HBM once, the stem kernel fuses the BGR flip and the
+``(x/255-0.5)/0.5`` normalisation, and the embedding comes back already
+L2-normalised the way the reference's ``normalize=True`` path leaves it.
+
+Differences (documented in DESIGN.md): inputs must already be 112x112 (the
+reference would ``cv2.resize`` them, face_embedder.py:94-96; cv2 is absent
+here), ``model_type='arcface'`` (onnxruntime) raises NotImplementedError, and
+``device`` must be a HIP device — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .arch import INPUT_SIZE, block_specs
+from .weights import load_checkpoint_state_dict, synthetic_state_dict
+
+SCRIPT_DIR = Path(__file__).resolve().parent
+
+# Same registry layout as face_embedder.py:16-24.
+ADAFACE_MODELS = {
+    "ir_50": str(SCRIPT_DIR / "pretrained" / "adaface_ir50_ms1mv2.ckpt"),
+    "ir_101": str(SCRIPT_DIR / "pretrained" / "adaface_ir101_ms1mv3.ckpt"),
+}
+ARCFACE_MODELS = {
+    "ir_50": str(SCRIPT_DIR / "pretrained" / "arcface_ir50_ms1mv3.onnx"),
+    "ir_101": str(SCRIPT_DIR / "pretrained" / "arcface_ir101_ms1mv3.onnx"),
+}
+
+SYNTHETIC = "synthetic"  # model_path value selecting the seeded weights of weights.py
+
+
+def _as_device(device) -> torch.device:
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+    return torch.device(device)
+
+
+class FaceEmbedder:
+    def __init__(self, architecture: str = "ir_101", model_path: Optional[str] = None,
+                 model_type: str = "adaface", device=None, max_batch: int = 256,
+                 state_dict=None, weight_seed: Optional[int] = None):
+        self.device = _as_device(device)
+        self.model_type = model_type
+        self.architecture = architecture
+        if model_type == "adaface":
+            if architecture not in ADAFACE_MODELS:
+                raise ValueError(f"Unknown architecture: {architecture}. "
+                                 f"Available: {list(ADAFACE_MODELS.keys())}")
+            if state_dict is None:
+                if model_path == SYNTHETIC or weight_seed is not None:
+                    state_dict = (synthetic_state_dict(architecture) if weight_seed is None
+                                  else synthetic_state_dict(architecture, weight_seed))
+                else:
+                    if model_path is None:
+                        model_path = ADAFACE_MODELS[architecture]
+                    if not os.path.exists(model_path):
+                        raise FileNotFoundError(f"AdaFace checkpoint not found at: {model_path}")
+                    state_dict = load_checkpoint_state_dict(model_path)
+            block_specs(architecture)
+            self.model = _lib.Handle(architecture, model_type, self.device, max_batch)
+            self.model.load_state_dict(state_dict)
+            self.input_size = INPUT_SIZE
+            self.mean = 0.5
+            self.std = 0.5
+            self.is_onnx = False
+        elif model_type == "arcface":
+            raise NotImplementedError("ArcFace (onnxruntime) path is not part of the MI355X hot path yet; "
+                                      "its parity is unpinned (no onnxruntime, no .onnx files)")
+        else:
+            raise ValueError(f"Unknown model_type: {model_type}. Must be 'adaface' or 'arcface'")
+
+    # -- reference API -------------------------------------------------------
+    def preprocess(self, face_image: np.ndarray) -> torch.Tensor:
+        """Host tensor exactly as face_embedder.py:93-104 builds it (for API parity;
+        the GPU path does the same arithmetic inside the stem kernel)."""
+        self._check_shape(face_image)
+        bgr = face_image[:, :, ::-1]
+        bgr = (bgr / 255.0 - self.mean) / self.std
+        return torch.from_numpy(bgr.transpose(2, 0, 1).copy()).float().unsqueeze(0)
+
+    def extract_embedding(self, face_image: np.ndarray, normalize: bool = True) -> np.ndarray:
+        return self.extract_embeddings_batch([face_image], normalize=normalize)[0]
+
+    def extract_embeddings_batch(self, face_images: List[np.ndarray], normalize: bool = True,
+                                 batch_size: int = 32) -> np.ndarray:
+        """``batch_size`` is accepted for signature parity; the device forward is
+        batch-invariant and chunks by the handle's max_batch instead."""
+        if len(face_images) == 0:
+            return np.array([])
+        for f in face_images:
+            self._check_shape(f)
+        host = np.ascontiguousarray(np.stack(face_images).astype(np.uint8, copy=False))
+        rgb = torch.from_numpy(host).to(self.device, non_blocking=False)
+        out = self.embed_tensor(rgb, normalize=normalize)
+        return out.cpu().numpy()
+
+    def compute_similarity(self, embedding1: np.ndarray, embedding2: np.ndarray) -> float:
+        e1 = embedding1 / (np.linalg.norm(embedding1) + 1e-8)
+        e2 = embedding2 / (np.linalg.norm(embedding2) + 1e-8)
+        return np.dot(e1, e2)
+
+    def compute_similarity_batch(self, embedding: np.ndarray, gallery_embeddings: np.ndarray) -> np.ndarray:
+        e = embedding / (np.linalg.norm(embedding) + 1e-8)
+        g = gallery_embeddings / (np.linalg.norm(gallery_embeddings, axis=1, keepdims=True) + 1e-8)
+        return np.dot(g, e)
+
+    def aggregate_embeddings(self, embeddings: np.ndarray, method: str = "mean") -> np.ndarray:
+        if len(embeddings) == 0:
+            raise ValueError("Cannot aggregate empty embeddings")
+        if len(embeddings) == 1:
+            return embeddings[0]
+        if method == "mean":
+            agg = np.mean(embeddings, axis=0)
+        elif method == "median":
+            agg = np.median(embeddings, axis=0)
+        elif method == "weighted_mean":
+            w = np.mean(np.dot(embeddings, embeddings.T), axis=1)
+            agg = np.sum(embeddings * (w / np.sum(w))[:, np.newaxis], axis=0)
+        else:
+            raise ValueError(f"Unknown aggregation method: {method}")
+        return agg / (np.linalg.norm(agg) + 1e-8)
+
+    # -- device-resident API (no host round trip) ----------------------------
+    def embed_tensor(self, rgb: torch.Tensor, normalize: bool = True,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """uint8 [N,112,112,3] RGB on the handle's device -> float32 [N,512] on device."""
+        if rgb.device != self.device or rgb.dtype != torch.uint8 or rgb.dim() != 4 or rgb.shape[3] != 3:
+            raise ValueError("expected a uint8 [N,112,112,3] tensor on " + str(self.device))
+        rgb = rgb.contiguous()
+        if out is None:
+            out = torch.empty((rgb.shape[0], 512), dtype=torch.float32, device=self.device)
+        self.model.embed(rgb, out, normalize)
+        return out
+
+    def _check_shape(self, face_image: np.ndarray) -> None:
+        if face_image.ndim != 3 or face_image.shape[2] != 3:
+            raise ValueError(f"expected an HxWx3 RGB crop, got shape {face_image.shape}")
+        if face_image.shape[:2] != self.input_size:
+            raise ValueError(f"crop is {face_image.shape[:2]}, expected {self.input_size}: resize to 112x112 first "
+                             "(cv2.resize INTER_LINEAR in the reference, face_embedder.py:94-96)")

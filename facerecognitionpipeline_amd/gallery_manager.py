@@ -1,0 +1,298 @@
+"""Drop-in ``GalleryManager`` whose ``search`` runs on the gfx950 matcher.
+
+Mirrors ``gallery_manager.GalleryManager`` (``gallery_manager.py:53-330``):
+student records, template construction (quality filter + mean / median /
+weighted_mean + L2) and the ``search(query, top_k) -> [(sid, name, score)]``
+contract.  What changes is where the match runs: the reference rebuilds the
+G x 512 matrix with ``np.vstack`` on every query (``:177-187``) and sorts all
+G scores (``:197``); here the template matrix lives in HBM (uploaded once per
+gallery version) and one kernel sequence does renormalise -> fp32 GEMM ->
+top-k.  ``search_batch`` exposes the batched form used by the throughput path.
+
+Persistence uses JSON + ``.npz`` (no pickle); ``load_backup`` reads the
+reference's ``export_for_backup`` JSON (``:246-270``).
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+from dataclasses import dataclass, field
+from datetime import datetime
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+SCRIPT_DIR = Path(__file__).resolve().parent
+
+
+@dataclass
+class StudentRecord:
+    student_id: str
+    name: str
+    embeddings: np.ndarray
+    template_embedding: np.ndarray
+    num_samples: int
+    enrollment_date: str
+    last_updated: str
+    metadata: Dict = field(default_factory=dict)
+
+    def to_dict(self) -> Dict:
+        return {"student_id": self.student_id, "name": self.name,
+                "embeddings": np.asarray(self.embeddings).tolist(),
+                "template_embedding": np.asarray(self.template_embedding).tolist(),
+                "num_samples": self.num_samples, "enrollment_date": self.enrollment_date,
+                "last_updated": self.last_updated, "metadata": self.metadata or {}}
+
+    @classmethod
+    def from_dict(cls, d: Dict) -> "StudentRecord":
+        return cls(student_id=d["student_id"], name=d["name"], embeddings=np.array(d["embeddings"]),
+                   template_embedding=np.array(d["template_embedding"]), num_samples=d["num_samples"],
+                   enrollment_date=d["enrollment_date"], last_updated=d["last_updated"],
+                   metadata=d.get("metadata", {}) or {})
+
+
+def _slice_len(n: int, top_k: int) -> int:
+    """How many rows ``argsort(...)[::-1][:top_k]`` keeps (Python slice semantics)."""
+    return len(range(n)[:top_k])
+
+
+class GalleryManager:
+    def __init__(self, gallery_path: Optional[str] = None, aggregation_method: str = "mean", device=None,
+                 verbose: bool = True):
+        if gallery_path is None:
+            gallery_path = str(SCRIPT_DIR / "gallery" / "students.npz")
+        self.gallery_path = gallery_path
+        self.aggregation_method = aggregation_method
+        self.students: Dict[str, StudentRecord] = {}
+        self.verbose = verbose
+        self._device = torch.device(device) if device is not None else None
+        self._handle: Optional[_lib.Handle] = None
+        self._version = 0          # bumped by every mutation
+        self._device_version = -1  # version the HBM copy holds
+        self._ids: List[str] = []
+        os.makedirs(os.path.dirname(gallery_path) or ".", exist_ok=True)
+        if os.path.exists(self._arrays_path(gallery_path)):
+            self.load()
+            self._log(f"Loaded gallery with {len(self.students)} students")
+        else:
+            self._log("Initialized empty gallery")
+
+    # -- records -------------------------------------------------------------
+    def add_student(self, student_id: str, name: str, embeddings: np.ndarray, metadata: Optional[Dict] = None,
+                    overwrite: bool = False) -> bool:
+        if student_id in self.students and not overwrite:
+            self._log(f"Student {student_id} already exists. Use overwrite=True to replace.")
+            return False
+        emb = embeddings.reshape(1, -1) if embeddings.ndim == 1 else embeddings
+        now = datetime.now().isoformat()
+        self.students[student_id] = StudentRecord(student_id, name, emb, self._aggregate_embeddings(emb),
+                                                  len(emb), now, now, metadata or {})
+        self._touch()
+        self._log(f"{'Updated' if overwrite else 'Added'} student: {name} ({student_id}) with {len(emb)} embeddings")
+        return True
+
+    def update_embeddings(self, student_id: str, new_embeddings: np.ndarray, mode: str = "append") -> bool:
+        rec = self.students.get(student_id)
+        if rec is None:
+            self._log(f"Student {student_id} not found")
+            return False
+        new = new_embeddings.reshape(1, -1) if new_embeddings.ndim == 1 else new_embeddings
+        if mode == "append":
+            emb = np.vstack([rec.embeddings, new])
+        elif mode == "replace":
+            emb = new
+        elif mode == "merge":
+            emb = self._remove_outliers(np.vstack([rec.embeddings, new]))
+        else:
+            raise ValueError(f"Unknown mode: {mode}")
+        rec.embeddings = emb
+        rec.template_embedding = self._aggregate_embeddings(emb)
+        rec.num_samples = len(emb)
+        rec.last_updated = datetime.now().isoformat()
+        self._touch()
+        return True
+
+    def delete_student(self, student_id: str) -> bool:
+        if student_id not in self.students:
+            self._log(f"Student {student_id} not found")
+            return False
+        del self.students[student_id]
+        self._touch()
+        return True
+
+    def get_student(self, student_id: str) -> Optional[StudentRecord]:
+        return self.students.get(student_id)
+
+    def get_all_students(self) -> Dict[str, StudentRecord]:
+        return self.students
+
+    def get_gallery_embeddings(self) -> Tuple[np.ndarray, List[str]]:
+        if not self.students:
+            return np.array([]), []
+        ids = list(self.students.keys())
+        return np.vstack([self.students[s].template_embedding for s in ids]), ids
+
+    # -- matching (device) ---------------------------------------------------
+    def search(self, query_embedding: np.ndarray, top_k: int = 5) -> List[Tuple[str, str, float]]:
+        if not self.students:
+            return []
+        return self.search_batch(np.asarray(query_embedding).reshape(1, -1), top_k)[0]
+
+    def search_batch(self, queries: np.ndarray, top_k: int = 5) -> List[List[Tuple[str, str, float]]]:
+        """search() for every row of ``queries`` [n, 512], one device round trip."""
+        if not self.students:
+            return [[] for _ in range(len(queries))]
+        k = _slice_len(len(self.students), top_k)
+        if k == 0:
+            return [[] for _ in range(len(queries))]
+        q = torch.from_numpy(np.ascontiguousarray(queries, dtype=np.float32)).to(self.device)
+        idx, score = self.search_device(q, k)
+        idx, score = idx.cpu().numpy(), score.cpu().numpy()
+        return [[(self._ids[i], self.students[self._ids[i]].name, float(s)) for i, s in zip(ri, rs)]
+                for ri, rs in zip(idx, score)]
+
+    def search_device(self, queries: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Device form: float32 [n,512] on the GPU -> (int32 [n,k] gallery rows, float32 [n,k] scores).
+        Row order is ``get_gallery_embeddings()`` order (dict insertion order)."""
+        h = self._sync_device()
+        n = queries.shape[0]
+        idx = torch.empty((n, k), dtype=torch.int32, device=self.device)
+        score = torch.empty((n, k), dtype=torch.float32, device=self.device)
+        h.match(queries.contiguous(), k, idx, score)
+        return idx, score
+
+    @property
+    def device(self) -> torch.device:
+        if self._device is None:
+            self._device = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+        return self._device
+
+    def attach_handle(self, handle: "_lib.Handle") -> None:
+        """Share an existing handle (e.g. a FaceEmbedder's) so embed+match run in one library state."""
+        self._handle = handle
+        self._device = handle.device
+        self._device_version = -1
+
+    def _sync_device(self) -> "_lib.Handle":
+        if self._handle is None:
+            self._handle = _lib.Handle("ir_50", "adaface", self.device, max_batch=1)
+        if self._device_version != self._version:
+            E, ids = self.get_gallery_embeddings()
+            self._ids = ids
+            self._handle.gallery_set(torch.from_numpy(np.ascontiguousarray(E, dtype=np.float32)).to(self.device))
+            self._device_version = self._version
+        return self._handle
+
+    # -- persistence ---------------------------------------------------------
+    @staticmethod
+    def _arrays_path(path: str) -> str:
+        root, _ext = os.path.splitext(path)
+        return root + ".npz"
+
+    def save(self, path: Optional[str] = None) -> None:
+        path = path or self.gallery_path
+        ids = list(self.students.keys())
+        arrays = {}
+        for i, s in enumerate(ids):
+            arrays[f"e{i}"] = np.asarray(self.students[s].embeddings)
+            arrays[f"t{i}"] = np.asarray(self.students[s].template_embedding)
+        np.savez(self._arrays_path(path), **arrays)
+        meta = {"num_students": len(ids), "last_saved": datetime.now().isoformat(), "order": ids,
+                "students": {s: {"student_id": r.student_id, "name": r.name, "num_samples": r.num_samples,
+                                 "enrollment_date": r.enrollment_date, "last_updated": r.last_updated,
+                                 "metadata": r.metadata} for s, r in self.students.items()}}
+        with open(os.path.splitext(path)[0] + ".json", "w") as f:
+            json.dump(meta, f, indent=2)
+
+    def load(self, path: Optional[str] = None) -> None:
+        path = path or self.gallery_path
+        arr_path = self._arrays_path(path)
+        if not os.path.exists(arr_path):
+            self._log(f"Gallery file not found: {arr_path}")
+            return
+        with open(os.path.splitext(path)[0] + ".json") as f:
+            meta = json.load(f)
+        arrays = np.load(arr_path)
+        self.students = {}
+        for i, s in enumerate(meta["order"]):
+            m = meta["students"][s]
+            self.students[s] = StudentRecord(s, m["name"], arrays[f"e{i}"], arrays[f"t{i}"], m["num_samples"],
+                                             m["enrollment_date"], m["last_updated"], m.get("metadata", {}))
+        self._touch()
+
+    def load_backup(self, json_path: str) -> None:
+        """Import a reference ``export_for_backup`` JSON (gallery_manager.py:246-270)."""
+        with open(json_path) as f:
+            data = json.load(f)
+        self.students = {sid: StudentRecord.from_dict(d) for sid, d in data["students"].items()}
+        self._touch()
+
+    def export_for_backup(self, backup_dir: str, backup_name: Optional[str] = None) -> str:
+        os.makedirs(backup_dir, exist_ok=True)
+        stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
+        stem = f"{backup_name}_backup_{stamp}" if backup_name else f"gallery_backup_{stamp}"
+        if os.path.exists(self._arrays_path(self.gallery_path)):
+            shutil.copy2(self._arrays_path(self.gallery_path), os.path.join(backup_dir, stem + ".npz"))
+        out = os.path.join(backup_dir, stem + ".json")
+        with open(out, "w") as f:
+            json.dump({"backup_date": datetime.now().isoformat(), "backup_name": backup_name,
+                       "num_students": len(self.students),
+                       "students": {s: r.to_dict() for s, r in self.students.items()}}, f, indent=2)
+        return out
+
+    def get_statistics(self) -> Dict:
+        n = len(self.students)
+        if n == 0:
+            return {"num_students": 0, "total_embeddings": 0, "avg_embeddings_per_student": 0}
+        total = sum(r.num_samples for r in self.students.values())
+        return {"num_students": n, "total_embeddings": total, "avg_embeddings_per_student": total / n,
+                "students": [{"id": r.student_id, "name": r.name, "num_samples": r.num_samples,
+                              "enrollment_date": r.enrollment_date} for r in self.students.values()]}
+
+    # -- template construction (host; offline, KAT-pinned) -------------------
+    def _filter_quality_embeddings(self, embeddings: np.ndarray, min_similarity: float = 0.70) -> np.ndarray:
+        if len(embeddings) <= 2:
+            return embeddings
+        sim = embeddings @ embeddings.T
+        np.fill_diagonal(sim, 0)
+        mean_sim = sim.mean(axis=1)
+        kept = embeddings[mean_sim >= min_similarity]
+        if len(kept) < 2:
+            kept = embeddings[np.argsort(mean_sim)[-2:]]
+        return kept
+
+    def _aggregate_embeddings(self, embeddings: np.ndarray) -> np.ndarray:
+        if len(embeddings) == 1:
+            return embeddings[0]
+        e = self._filter_quality_embeddings(embeddings)
+        if self.aggregation_method == "median":
+            t = np.median(e, axis=0)
+        elif self.aggregation_method == "weighted_mean":
+            w = (e @ e.T).mean(axis=1)
+            t = (e * (w / w.sum())[:, None]).sum(axis=0)
+        else:  # 'mean' and any unknown method (reference falls back to mean)
+            t = e.mean(axis=0)
+        return t / (np.linalg.norm(t) + 1e-8)
+
+    def _remove_outliers(self, embeddings: np.ndarray, threshold: float = 0.7) -> np.ndarray:
+        if len(embeddings) <= 2:
+            return embeddings
+        avg = (embeddings @ embeddings.T).mean(axis=1)
+        return embeddings[avg >= np.median(avg) * threshold]
+
+    def _touch(self) -> None:
+        self._version += 1
+
+    def _log(self, msg: str) -> None:
+        if self.verbose:
+            print(msg)
+
+
+def build_gallery_matrix(records: Sequence[StudentRecord]) -> np.ndarray:
+    """Stack templates in record order (the matrix ``search`` scores against)."""
+    return np.vstack([r.template_embedding for r in records]).astype(np.float32)

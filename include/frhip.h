@@ -1,0 +1,106 @@
+/*
+ * frhip.h — C ABI of the MI355X (gfx950) face embed + match hot path.
+ *
+ * The reference (tuoasty/FaceRecognitionPipeline) has no FFI: its seams are
+ * Python duck types.  Each entry point below replaces one
+ * of them; the Python host layer (facerecognitionpipeline_amd/face_embedder.py,
+ * gallery_manager.py) binds these symbols with ctypes and keeps the
+ * reference's method names, argument meaning and exception types.
+ *
+ * Conventions
+ *  - Return value: FR_OK (0) or a negative FR_ERR_* code; fr_last_error()
+ *    gives the message.  No call aborts the process.
+ *  - "device" pointers are HIP device allocations on the handle's device;
+ *    "host" pointers are ordinary host memory, borrowed for the call only.
+ *  - `stream` is a hipStream_t (NULL = the null stream).  Device-pointer calls
+ *    are asynchronous on that stream; host-pointer calls synchronise.
+ *  - One mutex per handle: a handle may be shared by threads (the reference
+ *    server shares one FaceEmbedder/GalleryManager across Flask request
+ *    threads, face_recognition_server.py:1102).
+ *  - Embeddings are 512-d float32 rows; images are uint8 RGB HWC 112x112x3,
+ *    C-contiguous (the reference's aligned crops, face_recognition.py:64-74).
+ */
+#ifndef FRHIP_H_
+#define FRHIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FR_OK 0
+#define FR_ERR_INVALID_ARGUMENT (-1) /* Python: ValueError  */
+#define FR_ERR_MISSING_PARAM (-2)    /* Python: RuntimeError (load_state_dict strict) */
+#define FR_ERR_HIP (-3)              /* Python: RuntimeError */
+#define FR_ERR_STATE (-4)            /* Python: RuntimeError (not finalised / no gallery) */
+#define FR_ERR_UNSUPPORTED (-5)      /* Python: NotImplementedError */
+
+#define FR_EMBED_DIM 512
+#define FR_INPUT_SIZE 112
+
+typedef struct fr_handle fr_handle;
+
+/* Build an empty model.  Replaces FaceEmbedder.__init__'s
+ * `net.build_model(architecture)` (face_embedder.py:27-49).
+ * architecture: "ir_50" | "ir_101" (also "ir_18", "ir_34"); model_type: "adaface"
+ * ("arcface" -> FR_ERR_UNSUPPORTED: the ORT path is parity-unpinned).
+ * max_batch: images per internal forward chunk (workspace sizing), 1..2048. */
+int fr_create(const char* architecture, const char* model_type, int device, int max_batch, fr_handle** out);
+int fr_destroy(fr_handle* h);
+
+/* One AdaFace state-dict tensor, key WITHOUT the "model." prefix, float32
+ * host data in PyTorch's layout (conv weights [out][in][kh][kw]).  Replaces
+ * `self.model.load_state_dict(model_statedict)` (face_embedder.py:51-53);
+ * num_batches_tracked keys are accepted and ignored. */
+int fr_set_param(fr_handle* h, const char* name, const float* host_data, int64_t numel);
+/* Fold BatchNorms, repack weights NHWC, upload.  Missing keys -> FR_ERR_MISSING_PARAM
+ * (strict load_state_dict semantics).  Replaces `.to(device).eval()` (face_embedder.py:55-56). */
+int fr_finalize(fr_handle* h);
+
+/* Embed n crops.  Replaces FaceEmbedder.extract_embeddings_batch
+ * (face_embedder.py:137-182) and extract_embedding (:112-135): BGR + LUT
+ * normalise, IR forward, x/||x||, and with normalize!=0 the extra
+ * e/(||e||+1e-8).  rgb: device [n][112][112][3] uint8; out: device [n][512]. */
+int fr_embed(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize,
+             void* stream);
+/* Same with host buffers (H2D, forward, D2H, synchronise). */
+int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize);
+
+/* Replace the gallery matrix (G rows of D=512 float32).  Replaces the per-query
+ * `np.vstack` of GalleryManager.get_gallery_embeddings (gallery_manager.py:177-187):
+ * the handle keeps one device-resident copy until the next fr_gallery_set.
+ * src_is_device: 1 if E is a device pointer.  G == 0 clears the gallery. */
+int fr_gallery_set(fr_handle* h, const float* E, int G, int D, int src_is_device, void* stream);
+int fr_gallery_size(fr_handle* h, int* G);
+
+/* Batched GalleryManager.search (gallery_manager.py:189-205): q/(||q||+1e-8),
+ * S = E.q (fp32), top-k by descending score (ties: lower gallery index first).
+ * Q: device [n][512]; idx: device [n][k] int32 (gallery row, -1 if G<k... never
+ * returned: k is clamped to G by the caller); score: device [n][k]. */
+int fr_match_topk(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float* score, void* stream);
+/* Host-buffer variant (synchronises). */
+int fr_match_topk_host(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float* score);
+
+/* Fused unit of work of FaceMatcher.match_single_face (face_matcher.py:52-58),
+ * batched: embed(normalize=1) then match.  emb_out may be NULL.  Device pointers. */
+int fr_embed_match(fr_handle* h, const uint8_t* rgb, int n, int k, int32_t* idx, float* score, float* emb_out,
+                   void* stream);
+
+/* Per-kernel-class timing with HIP events on the call stream (bench roofline).
+ * enable=1 starts recording; fr_profile_read synchronises and returns, since the
+ * last read: summed milliseconds and algorithmic FLOPs of the conv_mfma launches,
+ * their launch count, and the summed milliseconds of all launches. */
+int fr_profile_enable(fr_handle* h, int enable);
+int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* conv_launches, double* total_ms);
+
+/* Last error message of this handle (or of the last failed fr_create if h is NULL). */
+const char* fr_last_error(fr_handle* h);
+/* Library build/version string. */
+const char* fr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRHIP_H_ */

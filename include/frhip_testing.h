@@ -1,0 +1,40 @@
+/*
+ * frhip_testing.h — kernel-level entry points of libfrhip for parity tests.
+ *
+ * Not part of the drop-in surface (include/frhip.h): these expose single
+ * kernels so tests can compare each against a PyTorch-CPU fp32 op of the same
+ * shape (one Conv2d of net.BasicBlockIR, the stem, the matcher's top-k).
+ * All pointers are device pointers; every call is asynchronous on `stream`.
+ */
+#ifndef FRHIP_TESTING_H_
+#define FRHIP_TESTING_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* y = epi(conv(pre(x))) in NHWC f32, w [cout][kh][kw][cin].
+ * epi: 0 affine, 1 affine+PReLU, 2 affine+residual(res same shape as y),
+ *      3 affine+residual(res[b][2oy][2ox], res spatial res_h x res_w), 4 raw.
+ * pre_scale/pre_shift may be NULL (no pre-affine).  nsplit > 1 only with epi 4:
+ * y then holds nsplit partial slabs of B*Ho*Wo*cout floats.
+ * tile: 0 = 256x64, 1 = 128x128. */
+int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout, int kh, int kw,
+               int stride, int pad, const float* pre_scale, const float* pre_shift, const float* post_scale,
+               const float* post_shift, const float* prelu, const float* res, int res_h, int res_w, int epi,
+               int nsplit, int tile, void* stream);
+
+/* Fused preprocess + input_layer on uint8 RGB [B][112][112][3]; w27x64 is the
+ * repacked [ky][kx][c_rgb][64] weight; lut the 256-entry normalisation table. */
+int frt_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, const float* bn_scale,
+             const float* bn_shift, const float* prelu, float* y, void* stream);
+
+/* Row-wise top-k of a [n][G] score matrix (score desc, index asc). */
+int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRHIP_TESTING_H_ */

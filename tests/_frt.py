@@ -1,0 +1,57 @@
+"""ctypes binding of include/frhip_testing.h (kernel-level test entry points)."""
+import ctypes
+
+import torch
+
+from facerecognitionpipeline_amd import _lib
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+
+
+def lib():
+    L = _lib.load()
+    if not getattr(L, "_frt_ready", False):
+        L.frt_conv2d.restype = _I
+        L.frt_conv2d.argtypes = [_P, _P, _P] + [_I] * 9 + [_P] * 6 + [_I] * 5 + [_P]
+        L.frt_stem.restype = _I
+        L.frt_stem.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P, _P]
+        L.frt_topk.restype = _I
+        L.frt_topk.argtypes = [_P, _I, _I, _I, _P, _P, _P]
+        L._frt_ready = True
+    return L
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def conv2d(x, w, B, H, W, cin, cout, kh, kw, stride, pad, pre=None, post=None, prelu=None, res=None,
+           res_hw=(0, 0), epi=0, nsplit=1, tile=1):
+    """x: NHWC cuda f32, w: [cout][kh][kw][cin] cuda f32.  Returns y (NHWC) or partial slabs."""
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    y = torch.full((nsplit, B, Ho, Wo, cout), float("nan"), device=x.device)
+    ps, ph = (pre if pre is not None else (None, None))
+    qs, qh = (post if post is not None else (None, None))
+    rc = lib().frt_conv2d(_p(x), _p(w), _p(y), B, H, W, cin, cout, kh, kw, stride, pad, _p(ps), _p(ph), _p(qs),
+                          _p(qh), _p(prelu), _p(res), res_hw[0], res_hw[1], epi, nsplit, tile,
+                          torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc)
+    return y if nsplit > 1 else y[0]
+
+
+def stem(img, lut, w27x64, sc, sh, al):
+    B = img.shape[0]
+    y = torch.full((B, 112, 112, 64), float("nan"), device=img.device)
+    _lib.check(lib().frt_stem(_p(img), B, _p(lut), _p(w27x64), _p(sc), _p(sh), _p(al), _p(y),
+                              torch.cuda.current_stream().cuda_stream))
+    return y
+
+
+def topk(scores, k):
+    n, G = scores.shape
+    idx = torch.empty((n, k), dtype=torch.int32, device=scores.device)
+    val = torch.empty((n, k), dtype=torch.float32, device=scores.device)
+    _lib.check(lib().frt_topk(_p(scores), n, G, k, _p(idx), _p(val), torch.cuda.current_stream().cuda_stream))
+    return idx, val

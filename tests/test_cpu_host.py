@@ -1,0 +1,110 @@
+"""CPU-only: the C-ABI library loads and exports its header; host-side logic of the mirrors."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    with open(os.path.join(REPO, "include", header)) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*((?:fr|frt)_[a-z_0-9]+)\s*\(", src, re.M)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from facerecognitionpipeline_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        from facerecognitionpipeline_amd.build import build
+        build(verbose=False)
+    lib = _lib.load()
+    names = _declared("frhip.h") + _declared("frhip_testing.h")
+    assert len(names) >= 18, names
+    for n in names:
+        assert hasattr(lib, n), f"libfrhip.so does not export {n}"
+    assert b"gfx950" in lib.fr_version()
+
+
+def test_capi_reports_errors_without_gpu():
+    import ctypes
+    from facerecognitionpipeline_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.fr_create(b"ir_7", b"adaface", 0, 8, ctypes.byref(h)) == _lib.FR_ERR_INVALID_ARGUMENT
+    assert b"Unknown architecture" in lib.fr_last_error(None)
+    assert lib.fr_create(b"ir_50", b"arcface", 0, 8, ctypes.byref(h)) == _lib.FR_ERR_UNSUPPORTED
+    with pytest.raises(ValueError):
+        _lib.check(_lib.FR_ERR_INVALID_ARGUMENT)
+
+
+def test_product_refuses_cpu_device():
+    import torch
+    from facerecognitionpipeline_amd import _lib
+    with pytest.raises(RuntimeError):
+        _lib.Handle("ir_50", "adaface", torch.device("cpu"))
+
+
+def _gm(tmp_path):
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    return GalleryManager(gallery_path=str(tmp_path / "g" / "students.npz"), verbose=False)
+
+
+def test_gallery_records_and_templates(tmp_path, golden_dir):
+    from oracle.reference_path import aggregate_template
+    f = np.load(os.path.join(golden_dir, "backup_adaface_ir_101.npz"))
+    gm = _gm(tmp_path)
+    for sid, e in zip(f["student_ids"][:5], f["embeddings"][:5]):
+        assert gm.add_student(str(sid), str(sid), e)
+    assert not gm.add_student(str(f["student_ids"][0]), "x", f["embeddings"][0])
+    E, ids = gm.get_gallery_embeddings()
+    assert ids == [str(s) for s in f["student_ids"][:5]]
+    assert np.array_equal(E, f["ref_template"][:5])
+    for method in ("median", "weighted_mean"):
+        gm.aggregation_method = method
+        t = gm._aggregate_embeddings(f["embeddings"][0])
+        assert np.abs(t - aggregate_template(f["embeddings"][0], method)).max() <= 1e-7
+    gm.aggregation_method = "mean"
+    sid = str(f["student_ids"][1])
+    assert gm.update_embeddings(sid, f["embeddings"][6][:2], mode="append")
+    assert gm.get_student(sid).num_samples == 10
+    assert gm.update_embeddings(sid, f["embeddings"][6], mode="replace")
+    assert gm.get_student(sid).num_samples == 8
+    assert gm.update_embeddings(sid, f["embeddings"][7], mode="merge")
+    with pytest.raises(ValueError):
+        gm.update_embeddings(sid, f["embeddings"][7], mode="bogus")
+    assert gm.delete_student(sid) and not gm.delete_student(sid)
+    st = gm.get_statistics()
+    assert st["num_students"] == 4
+    # save/load round trip (JSON + npz, no pickle)
+    gm.save()
+    gm2 = _gm(tmp_path)
+    assert list(gm2.students) == list(gm.students)
+    for s in gm.students:
+        assert np.array_equal(gm2.students[s].template_embedding, gm.students[s].template_embedding)
+    out = gm.export_for_backup(str(tmp_path / "bk"), "t")
+    gm3 = _gm(tmp_path / "x")
+    gm3.load_backup(out)
+    assert np.allclose(gm3.get_gallery_embeddings()[0], gm.get_gallery_embeddings()[0])
+
+
+def test_reference_backup_json_loads(tmp_path, golden_dir):
+    """A reference export_for_backup JSON reproduces the fixture templates."""
+    import json
+    f = np.load(os.path.join(golden_dir, "backup_arcface_ir_50.npz"))
+    data = {"students": {str(s): {"student_id": str(s), "name": str(s), "embeddings": e.tolist(),
+                                  "template_embedding": t.tolist(), "num_samples": 8, "enrollment_date": "",
+                                  "last_updated": "", "metadata": {}}
+                         for s, e, t in zip(f["student_ids"], f["embeddings"], f["stored_template"])}}
+    p = tmp_path / "b.json"
+    p.write_text(json.dumps(data))
+    gm = _gm(tmp_path)
+    gm.load_backup(str(p))
+    E, _ = gm.get_gallery_embeddings()
+    assert np.array_equal(E.astype(np.float32), f["stored_template"])
+
+
+def test_slice_semantics_of_top_k():
+    from facerecognitionpipeline_amd.gallery_manager import _slice_len
+    assert [_slice_len(3, k) for k in (5, 3, 1, 0, -1, -5)] == [3, 3, 1, 0, 2, 0]

@@ -1,0 +1,148 @@
+"""Kernel-level parity: each HIP kernel vs a PyTorch-CPU fp32 op of the same shape.
+
+Tolerance: the conv kernel computes exact f32 products with f32 accumulation
+(MFMA f32 = fmaf chain); only the summation order differs from PyTorch CPU, so
+we allow |d| <= 1e-5 * max|ref| + 1e-6 (K <= 25088 terms).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tests import _frt
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rand(*shape, seed=0, lo=-1.0, hi=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(*shape, generator=g) * (hi - lo) + lo
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def _close(got, ref, rel=1e-5):
+    ref = ref.float()
+    tol = rel * ref.abs().max().item() + 1e-6
+    d = (got.float() - ref).abs().max().item()
+    assert d <= tol, f"max |diff| {d:.3e} > tol {tol:.3e}"
+
+
+def _conv_case(B, H, cin, cout, k, stride, pad, epi, tile, use_pre, seed, nsplit=1):
+    x = _rand(B, cin, H, H, seed=seed)
+    w = _rand(cout, cin, k, k, seed=seed + 1) / (cin * k * k) ** 0.5
+    pre_s, pre_b = _rand(cin, seed=seed + 2, lo=0.5, hi=1.5), _rand(cin, seed=seed + 3, lo=-0.2, hi=0.2)
+    post_s, post_b = _rand(cout, seed=seed + 4, lo=0.5, hi=1.5), _rand(cout, seed=seed + 5, lo=-0.2, hi=0.2)
+    al = _rand(cout, seed=seed + 6, lo=0.1, hi=0.4)
+    xin = x * pre_s.view(1, -1, 1, 1) + pre_b.view(1, -1, 1, 1) if use_pre else x
+    ref = F.conv2d(xin, w, stride=stride, padding=pad)
+    Ho = ref.shape[2]
+    res = None
+    res_hw = (0, 0)
+    if epi != 4:
+        ref = ref * post_s.view(1, -1, 1, 1) + post_b.view(1, -1, 1, 1)
+    if epi == 1:
+        ref = torch.where(ref > 0, ref, ref * al.view(1, -1, 1, 1))
+    if epi == 2:
+        r = _rand(B, cout, Ho, Ho, seed=seed + 7)
+        ref = ref + r
+        res = _nhwc(r).to(DEV)
+    if epi == 3:
+        assert cin == cout and stride == 2
+        ref = ref + x[:, :, ::2, ::2]
+        res = _nhwc(x).to(DEV)
+        res_hw = (H, H)
+    wd = w.permute(0, 2, 3, 1).contiguous().to(DEV)
+    got = _frt.conv2d(_nhwc(x).to(DEV), wd, B, H, H, cin, cout, k, k, stride, pad,
+                      pre=(pre_s.to(DEV), pre_b.to(DEV)) if use_pre else None,
+                      post=(post_s.to(DEV), post_b.to(DEV)) if epi != 4 else None,
+                      prelu=al.to(DEV) if epi == 1 else None, res=res, res_hw=res_hw, epi=epi,
+                      nsplit=nsplit, tile=tile)
+    torch.cuda.synchronize()
+    if nsplit > 1:
+        got = got.sum(0)
+    return got.cpu(), _nhwc(ref)
+
+
+@pytest.mark.parametrize("tile", [0, 1])
+def test_conv1_pre_bn_prelu(tile):
+    # res_layer[0..3]: BN(in) -> conv3x3 s1 p1 -> BN -> PReLU; M = 2*14*14 = 392 (ragged tiles)
+    got, ref = _conv_case(2, 14, 64, 64 if tile == 0 else 128, 3, 1, 1, epi=1, tile=tile, use_pre=True, seed=10)
+    _close(got, ref)
+
+
+def test_conv2_stride2_conv_shortcut_residual():
+    # res_layer[4..5] stride 2 + residual from the conv1x1 shortcut tensor
+    got, ref = _conv_case(3, 14, 128, 256, 3, 2, 1, epi=2, tile=1, use_pre=False, seed=20)
+    _close(got, ref)
+
+
+def test_conv2_stride2_maxpool_shortcut():
+    # stage-1 unit-1: shortcut = MaxPool2d(1,2)(x), i.e. x[:, :, ::2, ::2]
+    got, ref = _conv_case(2, 16, 64, 64, 3, 2, 1, epi=3, tile=0, use_pre=False, seed=30)
+    _close(got, ref)
+
+
+def test_conv2_identity_residual_tile0():
+    got, ref = _conv_case(2, 12, 64, 64, 3, 1, 1, epi=2, tile=0, use_pre=False, seed=35)
+    _close(got, ref)
+
+
+def test_shortcut_conv1x1_stride2():
+    got, ref = _conv_case(2, 14, 64, 128, 1, 2, 0, epi=0, tile=1, use_pre=False, seed=40)
+    _close(got, ref)
+
+
+def test_head_fc_as_7x7_conv_split_k():
+    # output_layer: BN2d pre-affine + Linear(25088,512) == 7x7 valid conv; split-K over the 49 taps
+    got, ref = _conv_case(5, 7, 512, 512, 7, 1, 0, epi=4, tile=1, use_pre=True, seed=50, nsplit=49)
+    _close(got, ref)
+
+
+def test_gemm_ragged_n_for_gallery_scores():
+    # the matcher's S = Qn . E^T as a 1x1 conv over 1x1 images, N = G = 1000 (not a tile multiple)
+    got, ref = _conv_case(7, 1, 512, 1000, 1, 1, 0, epi=4, tile=1, use_pre=False, seed=60)
+    _close(got, ref)
+
+
+def test_stem_matches_preprocess_and_input_layer():
+    from oracle.reference_path import preprocess, preprocess_lut
+    from facerecognitionpipeline_amd.weights import synthetic_crops
+    imgs = synthetic_crops(3, seed=123)
+    w = _rand(64, 3, 3, 3, seed=70) / 27 ** 0.5
+    sc, sh = _rand(64, seed=71, lo=0.5, hi=1.5), _rand(64, seed=72, lo=-0.2, hi=0.2)
+    al = _rand(64, seed=73, lo=0.1, hi=0.4)
+    x = torch.cat([preprocess(i) for i in imgs])
+    ref = F.conv2d(x, w, padding=1) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+    ref = torch.where(ref > 0, ref, ref * al.view(1, -1, 1, 1))
+    w27 = torch.empty(3, 3, 3, 64)
+    for c in range(3):  # tensor channel c (BGR) is RGB channel 2-c
+        w27[:, :, 2 - c, :] = w[:, c].permute(1, 2, 0)
+    got = _frt.stem(torch.from_numpy(imgs).to(DEV), torch.from_numpy(preprocess_lut()).to(DEV),
+                    w27.reshape(27, 64).contiguous().to(DEV), sc.to(DEV), sh.to(DEV), al.to(DEV))
+    torch.cuda.synchronize()
+    _close(got.cpu(), _nhwc(ref))
+
+
+def test_preprocess_lut_is_bit_exact():
+    from oracle.reference_path import preprocess, preprocess_lut
+    img = np.arange(256, dtype=np.uint8).repeat(3 * 112 * 112 // 256 + 1)[: 112 * 112 * 3].reshape(112, 112, 3)
+    t = preprocess(img)[0].numpy()           # reference float64 -> float32 path
+    lut = preprocess_lut()
+    assert np.array_equal(t, lut[img[:, :, ::-1].transpose(2, 0, 1)])
+
+
+@pytest.mark.parametrize("G,k", [(1000, 5), (37, 3), (100_000, 5), (64, 64)])
+def test_topk_matches_policy(G, k):
+    from oracle.reference_path import topk_policy
+    g = torch.Generator().manual_seed(G)
+    s = torch.rand(9, G, generator=g)
+    s[0, :] = 0.5            # all ties: lowest indices first
+    s[1, 3] = s[1, 7] = 2.0  # a tie at the top
+    idx, val = _frt.topk(s.to(DEV), k)
+    ri, rv = topk_policy(s.numpy(), k)
+    assert np.array_equal(idx.cpu().numpy(), ri)
+    assert np.array_equal(val.cpu().numpy(), rv)
