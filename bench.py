@@ -93,12 +93,13 @@ def main():
 
     # gallery: rank 0 embeds G synthetic gallery crops on its GPU, RCCL broadcast to the others
     G = args.gallery
-    gallery = torch.empty((G, 512), dtype=torch.float32, device=dev)
     gal_crops = W.synthetic_crops(G, W.CROP_SEED_GALLERY)
+    gallery = None
     if rank == 0:
-        emb.embed_tensor(torch.from_numpy(gal_crops).to(dev), out=gallery)
+        gallery = emb.embed_tensor(torch.from_numpy(gal_crops).to(dev))
     if world > 1:
-        dist.broadcast(gallery, src=0)
+        from facerecognitionpipeline_amd.distributed import broadcast_gallery
+        gallery = broadcast_gallery(gallery, G, dev, src=0)
     emb.model.gallery_set(gallery)
 
     # probes resident in HBM: noisy copies of gallery crops (rank-dependent)
