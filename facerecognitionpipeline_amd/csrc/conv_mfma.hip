@@ -69,10 +69,18 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
   const int rsub = tid >> 3;    // 0..31
 
   const int H = p.H, W = p.W, Cin = p.Cin;
-  const int cchunks = Cin / BK;
-  const int Ktot = p.KH * p.KW * Cin;
+  const int taps = p.KH * p.KW;
+  const int Ktot = taps * Cin;
 
-  // ---- per-row im2col bases for the A rows this thread stages
+  // Buffer descriptors: an out-of-range offset returns zeros, so padding taps,
+  // rows past M and columns past N need no branches (OOB = 0x80000000).
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.B * H * W * Cin * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.Cout * Ktot * 4, 0x00020000);
+  constexpr int OOB = 0x80000000;
+
+  // ---- per-row im2col bases (bytes) for the A rows this thread stages
   int a_base[A_IT], a_iy[A_IT], a_ix[A_IT];
   const int HoWo = p.Ho * p.Wo;
 #pragma unroll
@@ -85,48 +93,66 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
       const int ox = rem - oy * p.Wo;
       a_iy[i] = oy * p.stride - p.pad;
       a_ix[i] = ox * p.stride - p.pad;
-      a_base[i] = ((b * H + a_iy[i]) * W + a_ix[i]) * Cin + 4 * k4;
+      a_base[i] = (((b * H + a_iy[i]) * W + a_ix[i]) * Cin + 4 * k4) * 4;
     } else {
       a_iy[i] = -(1 << 20);
       a_ix[i] = 0;
       a_base[i] = 0;
     }
   }
-  int b_off[B_IT];
-  bool b_ok[B_IT];
+  int b_base[B_IT];
 #pragma unroll
   for (int j = 0; j < B_IT; ++j) {
     const int n = n0 + rsub + 32 * j;
-    b_ok[j] = n < p.Cout;
-    b_off[j] = (b_ok[j] ? n : 0) * Ktot + 4 * k4;
+    b_base[j] = n < p.Cout ? (n * Ktot + 4 * k4) * 4 : OOB;
   }
+
+  // K-step s = cc * taps + tap: channel chunk outer, tap inner, so the 9 taps of
+  // one 32-channel slice are consecutive steps (the shifted im2col rows re-hit L1/L2).
+  int tap = s_begin % taps;
+  int cc = s_begin / taps;
+  int ky = tap / p.KW;
+  int kx = tap - ky * p.KW;
 
   float4 ra[A_IT], rb[B_IT];
   float4 psc = make_float4(1.f, 1.f, 1.f, 1.f), psh = make_float4(0.f, 0.f, 0.f, 0.f);
-  bool a_ok[A_IT];
+  unsigned a_okm = 0;
 
-  auto load_step = [&](int s) {
-    const int tap = s / cchunks;
-    const int c0 = (s - tap * cchunks) * BK;
-    const int ky = tap / p.KW;
-    const int kx = tap - ky * p.KW;
-    const int tap_off = (ky * W + kx) * Cin + c0;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  auto ld4 = [](__amdgpu_buffer_rsrc_t rs, int off) {
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+  };
+
+  auto load_step = [&](bool live) {
+    const int c0 = cc * BK;
+    const int tap_off = ((ky * W + kx) * Cin + c0) * 4;
+    a_okm = 0;
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
-      a_ok[i] = ((unsigned)iy < (unsigned)H) && ((unsigned)ix < (unsigned)W);
-      ra[i] = a_ok[i] ? *reinterpret_cast<const float4*>(p.x + a_base[i] + tap_off)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      const unsigned ok = (unsigned)live & (unsigned)((unsigned)iy < (unsigned)H) & (unsigned)((unsigned)ix < (unsigned)W);
+      a_okm |= ok << i;
+      ra[i] = ld4(xr, ok ? a_base[i] + tap_off : OOB);
     }
-    const int koff = tap * Cin + c0;
+    const int koff = (tap * Cin + c0) * 4;
 #pragma unroll
-    for (int j = 0; j < B_IT; ++j)
-      rb[j] = b_ok[j] ? *reinterpret_cast<const float4*>(p.w + b_off[j] + koff)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < B_IT; ++j) rb[j] = ld4(wr, (b_base[j] == OOB || !live) ? OOB : b_base[j] + koff);
     if constexpr (PRE) {
       psc = *reinterpret_cast<const float4*>(p.pre_scale + c0 + 4 * k4);
       psh = *reinterpret_cast<const float4*>(p.pre_shift + c0 + 4 * k4);
     }
+  };
+  // Step counters of s+1; frozen on the last step (its loads are OOB no-ops).
+  auto advance = [&](bool live) {
+    const int kx1 = kx + 1 == p.KW ? 0 : kx + 1;
+    const int ky1 = kx + 1 == p.KW ? (ky + 1 == p.KH ? 0 : ky + 1) : ky;
+    const int tap1 = tap + 1 == taps ? 0 : tap + 1;
+    const int cc1 = tap + 1 == taps ? cc + 1 : cc;
+    kx = live ? kx1 : kx;
+    ky = live ? ky1 : ky;
+    tap = live ? tap1 : tap;
+    cc = live ? cc1 : cc;
   };
 
   auto store_step = [&](int buf) {
@@ -137,7 +163,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
       float4 v = ra[i];
       if constexpr (PRE) {
         // BN(x) only where the tap is inside the image: padded zeros stay zero.
-        if (a_ok[i]) {
+        if (a_okm & (1u << i)) {
           v.x = v.x * psc.x + psh.x;
           v.y = v.y * psc.y + psh.y;
           v.z = v.z * psc.z + psh.z;
@@ -163,33 +189,59 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
   const int frag_k = 4 * (lane >> 5);
 
   if (s_begin < s_end) {
-    load_step(s_begin);
+    load_step(true);
     store_step(0);
     __syncthreads();
     int buf = 0;
+    // Branch-free body (one basic block) so the schedule below can interleave the next
+    // step's global loads and LDS writes with this step's MFMAs.
     for (int s = s_begin; s < s_end; ++s) {
-      const bool more = (s + 1) < s_end;
-      if (more) load_step(s + 1);
+      const bool live = (s + 1) < s_end;
+      advance(live);
+      load_step(live);
       const float* Ab = As0 + buf * BUF + (wm * TM * 32 + frag_row) * LDK + frag_k;
       const float* Bb = Bs0 + buf * BUF + (wn * TN * 32 + frag_row) * LDK + frag_k;
+      float4 fa[BK / 8][TM], fb[BK / 8][TN];
 #pragma unroll
       for (int g = 0; g < BK / 8; ++g) {
-        float4 fa[TM], fb[TN];
 #pragma unroll
-        for (int a = 0; a < TM; ++a) fa[a] = *reinterpret_cast<const float4*>(Ab + a * 32 * LDK + g * 8);
+        for (int a = 0; a < TM; ++a) fa[g][a] = *reinterpret_cast<const float4*>(Ab + a * 32 * LDK + g * 8);
 #pragma unroll
-        for (int b = 0; b < TN; ++b) fb[b] = *reinterpret_cast<const float4*>(Bb + b * 32 * LDK + g * 8);
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b) {
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[a].x, fb[b].x, acc[a][b], 0, 0, 0);
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[a].y, fb[b].y, acc[a][b], 0, 0, 0);
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[a].z, fb[b].z, acc[a][b], 0, 0, 0);
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[a].w, fb[b].w, acc[a][b], 0, 0, 0);
-          }
+        for (int b = 0; b < TN; ++b) fb[g][b] = *reinterpret_cast<const float4*>(Bb + b * 32 * LDK + g * 8);
       }
-      if (more) store_step(buf ^ 1);
+#pragma unroll
+      for (int g = 0; g < BK / 8; ++g) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[g][a][e], fb[g][b][e], acc[a][b], 0, 0, 0);
+      }
+      store_step(buf ^ 1);
+      // Schedule (MFMA f32 = 64 pipe cycles; other instructions issue in its shadow):
+      //   fragments of groups 0-1 | 1 MFMA + 1 global load, x loads | fragments of groups 2-3 |
+      //   MFMAs | 2 MFMA + 1 LDS write, x writes (the loads had the whole step to land)
+      constexpr int NMFMA = (BK / 2) * TM * TN;
+      constexpr int NLD = A_IT + B_IT + (PRE ? 2 : 0);
+      constexpr int NDSR = (BK / 8) * (TM + TN);
+      constexpr int NDSW = A_IT + B_IT;
+      constexpr int NMID = NMFMA - NLD - 2 * NDSW;
+      static_assert(NMID >= 0, "tile too small for the interleave");
+      __builtin_amdgcn_sched_group_barrier(0x100, NDSR / 2, 0);
+#pragma unroll
+      for (int i = 0; i < NLD; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, NDSR - NDSR / 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NMID, 0);
+#pragma unroll
+      for (int i = 0; i < NDSW; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      }
       __syncthreads();
       buf ^= 1;
     }
@@ -258,10 +310,18 @@ static hipError_t launch_tile(const ConvParams& p0, bool pre, Epi epi, int nspli
 
 hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s) {
   if (p.Cin % BK != 0 || p.steps_total != p.KH * p.KW * p.Cin / BK || nsplit < 1 ||
-      (long long)p.steps_per_split * nsplit < p.steps_total || p.M <= 0 || p.Cout <= 0)
+      (long long)p.steps_per_split * nsplit < p.steps_total || p.M <= 0 || p.Cout <= 0 ||
+      (long long)p.B * p.H * p.W * p.Cin * 4 >= (1ll << 31) || (long long)p.Cout * p.KH * p.KW * p.Cin * 4 >= (1ll << 31))
     return hipErrorInvalidValue;
-  if (tile == TILE_256x64) return launch_tile<256, 64, 4, 1>(p, pre, epi, nsplit, s);
-  return launch_tile<128, 128, 2, 2>(p, pre, epi, nsplit, s);
+  switch (tile) {
+    case TILE_256x64: return launch_tile<256, 64, 4, 1>(p, pre, epi, nsplit, s);
+    case TILE_128x128: return launch_tile<128, 128, 2, 2>(p, pre, epi, nsplit, s);
+    case TILE_128x64: return launch_tile<128, 64, 4, 1>(p, pre, epi, nsplit, s);
+    case TILE_64x128: return launch_tile<64, 128, 1, 4>(p, pre, epi, nsplit, s);
+    case TILE_256x128: return launch_tile<256, 128, 2, 2>(p, pre, epi, nsplit, s);
+    case TILE_128x256: return launch_tile<128, 256, 2, 2>(p, pre, epi, nsplit, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace frhip

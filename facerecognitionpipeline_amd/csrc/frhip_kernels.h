@@ -38,7 +38,15 @@ struct ConvParams {
 };
 
 // Tile family of a conv launch.
-enum ConvTile : int { TILE_256x64 = 0, TILE_128x128 = 1 };
+enum ConvTile : int {
+  TILE_256x64 = 0,
+  TILE_128x128 = 1,
+  TILE_128x64 = 2,
+  TILE_64x128 = 3,
+  TILE_256x128 = 4,
+  TILE_128x256 = 5,
+  TILE_COUNT = 6
+};
 
 hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s);
 

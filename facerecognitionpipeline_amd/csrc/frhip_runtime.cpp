@@ -328,7 +328,9 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   p.steps_per_split = (p.steps_total + nsplit - 1) / nsplit;
   p.split_stride = split_stride;
   const double flop = 2.0 * p.M * (double)p.Cout * cw.kh * cw.kw * cw.cin;
-  const ConvTile tile = cw.cout <= 64 ? TILE_256x64 : TILE_128x128;
+  // Tile per output width, from tools/conv_sweep.py on MI355X at B=256:
+  // 128x64 for the 64-channel stage, 64x128 for 256 channels, 128x128 otherwise.
+  const ConvTile tile = cw.cout <= 64 ? TILE_128x64 : (cw.cout == 256 ? TILE_64x128 : TILE_128x128);
   ProfScope ps(h, s, flop, true);
   hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
@@ -744,7 +746,7 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
                int stride, int pad, const float* pre_scale, const float* pre_shift, const float* post_scale,
                const float* post_shift, const float* prelu, const float* res, int res_h, int res_w, int epi,
                int nsplit, int tile, void* stream) {
-  if (epi < 0 || epi > 4 || nsplit < 1 || (nsplit > 1 && epi != EPI_RAW) || (tile != 0 && tile != 1) ||
+  if (epi < 0 || epi > 4 || nsplit < 1 || (nsplit > 1 && epi != EPI_RAW) || (tile < 0 || tile >= TILE_COUNT) ||
       stride < 1 || kh < 1 || kw < 1 || B < 1)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d: bad arguments");
   ConvParams p{};

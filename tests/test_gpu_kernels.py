@@ -146,3 +146,12 @@ def test_topk_matches_policy(G, k):
     ri, rv = topk_policy(s.numpy(), k)
     assert np.array_equal(idx.cpu().numpy(), ri)
     assert np.array_equal(val.cpu().numpy(), rv)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
+def test_every_tile_config(tile):
+    # ragged M (2*10*10 = 200) and N = 320 (not a multiple of 64/128/256) through each tile shape
+    got, ref = _conv_case(2, 10, 64, 320, 3, 1, 1, epi=1, tile=tile, use_pre=True, seed=80 + tile)
+    _close(got, ref)
+    got, ref = _conv_case(2, 10, 96, 96, 3, 2, 1, epi=3, tile=tile, use_pre=False, seed=90 + tile)
+    _close(got, ref)

@@ -18,6 +18,7 @@ for s in $STEPS; do
     kernels)  step kernels 900 python -m pytest tests/test_gpu_kernels.py -q -rfE; rc=$? ;;
     pipeline) step pipeline 1200 python -m pytest tests/test_gpu_pipeline.py -q -rfE; rc=$? ;;
     allgpu)   step allgpu 1500 python -m pytest tests -m gpu -q -rfE; rc=$? ;;
+    sweep)    step sweep 900 python tools/conv_sweep.py --json gpurun_out/sweep.json; rc=$? ;;
     smoke)    step smoke 600 python -c "import __graft_entry__ as g; g.smoke()"; rc=$? ;;
     bench)    step bench 900 python bench.py ${BENCH_ARGS:-}; rc=$? ;;
     *) echo "unknown step $s"; exit 2 ;;
