@@ -35,6 +35,14 @@ struct ConvParams {
   int steps_per_split;   // K-steps per blockIdx.y slice
   long long split_stride;// elements between split-K partial slabs
   int mtiles, ntiles;
+  // stream-K schedule (sk_cus > 0): persistent grid of sk_cus x blocks-per-CU blocks.
+  int sk_cus;            // input: CUs to fill (0 = grid mode)
+  int sk_blocks;         // set by the launcher: persistent grid size P
+  int sk_dp_tiles;       // set by the launcher: tiles done whole, round-robin
+  float* sk_ws;          // [P][2][BM*BN] partial-accumulator slabs
+  long long sk_ws_floats;
+  int* sk_cnt;           // per stream-K tile arrival counters, zero at allocation
+  int sk_cnt_cap;
 };
 
 // Tile family of a conv launch.
@@ -49,6 +57,8 @@ enum ConvTile : int {
 };
 
 hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s);
+int conv_tile_bm(ConvTile t);
+int conv_tile_bn(ConvTile t);
 
 // uint8 RGB HWC 112x112 -> (BGR, LUT normalise) -> conv3x3 3->64 -> BN -> PReLU, NHWC f32.
 hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64,

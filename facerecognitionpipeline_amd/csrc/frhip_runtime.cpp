@@ -124,6 +124,14 @@ struct fr_handle {
   void* match_io = nullptr;
   size_t match_io_cap = 0;
 
+  // stream-K workspace shared by every body conv launch (launches are stream-ordered)
+  int cus = 0;
+  float* sk_ws = nullptr;
+  long long sk_ws_floats = 0;
+  int* sk_cnt = nullptr;
+  int sk_cnt_cap = 0;
+  bool stream_k = true;
+
   // profiling
   bool prof = false;
   std::vector<ProfEvent> events;
@@ -145,6 +153,8 @@ struct fr_handle {
     (void)hipFree(qn);
     (void)hipFree(scores);
     (void)hipFree(match_io);
+    (void)hipFree(sk_ws);
+    (void)hipFree(sk_cnt);
   }
 };
 
@@ -263,6 +273,22 @@ int ensure_buf(fr_handle* h, void** p, size_t* cap, size_t bytes) {
   return FR_OK;
 }
 
+// Stream-K slabs for P = CUs x (<=2 blocks/CU) blocks x 2 slots x the largest tile (256x128).
+int ensure_stream_k(int device, int* cus, float** ws, long long* ws_floats, int** cnt, int* cnt_cap) {
+  if (*ws) return FR_OK;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) n = 256;
+  const long long floats = (long long)n * 4 * 2 * 256 * 128;
+  const int cap = 8 * n;
+  if (hipMalloc((void**)ws, floats * sizeof(float)) != hipSuccess) return FR_ERR_HIP;
+  if (hipMalloc((void**)cnt, cap * sizeof(int)) != hipSuccess) return FR_ERR_HIP;
+  if (hipMemset(*cnt, 0, cap * sizeof(int)) != hipSuccess) return FR_ERR_HIP;
+  *cus = n;
+  *ws_floats = floats;
+  *cnt_cap = cap;
+  return FR_OK;
+}
+
 hipEvent_t take_event(fr_handle* h) {
   if (!h->pool.empty()) {
     hipEvent_t e = h->pool.back();
@@ -327,10 +353,17 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   p.steps_total = cw.kh * cw.kw * cw.cin / 32;
   p.steps_per_split = (p.steps_total + nsplit - 1) / nsplit;
   p.split_stride = split_stride;
+  if (h->stream_k && nsplit == 1 && h->sk_ws) {
+    p.sk_cus = h->cus;
+    p.sk_ws = h->sk_ws;
+    p.sk_ws_floats = h->sk_ws_floats;
+    p.sk_cnt = h->sk_cnt;
+    p.sk_cnt_cap = h->sk_cnt_cap;
+  }
   const double flop = 2.0 * p.M * (double)p.Cout * cw.kh * cw.kw * cw.cin;
-  // Tile per output width, from tools/conv_sweep.py on MI355X at B=256:
-  // 128x64 for the 64-channel stage, 64x128 for 256 channels, 128x128 otherwise.
-  const ConvTile tile = cw.cout <= 64 ? TILE_128x64 : (cw.cout == 256 ? TILE_64x128 : TILE_128x128);
+  // Tile per output width, from tools/conv_sweep.py on MI355X at B=256 with the stream-K
+  // schedule: 128x64 for the 64-channel stage, 64x128 otherwise.
+  const ConvTile tile = cw.cout <= 64 ? TILE_128x64 : TILE_64x128;
   ProfScope ps(h, s, flop, true);
   hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
@@ -392,6 +425,8 @@ int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float
   if (n <= 0) return FR_OK;
   int rc = ensure_buf(h, (void**)&h->qn, &h->qn_cap, (size_t)n * 512 * sizeof(float));
   if (rc) return rc;
+  if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
+    return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
   rc = ensure_buf(h, (void**)&h->scores, &h->scores_cap, (size_t)n * h->G * sizeof(float));
   if (rc) return rc;
   {
@@ -585,6 +620,8 @@ int fr_finalize(fr_handle* h) {
     FR_HIP(h, hipMalloc((void**)&h->in_stage, mb * 112 * 112 * 3));
     FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
   }
+  if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
+    return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
   h->finalized = true;
   return FR_OK;
 }
@@ -745,7 +782,11 @@ const char* fr_version(void) { return "frhip 0.1 gfx950 fp32-mfma"; }
 int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout, int kh, int kw,
                int stride, int pad, const float* pre_scale, const float* pre_shift, const float* post_scale,
                const float* post_shift, const float* prelu, const float* res, int res_h, int res_w, int epi,
-               int nsplit, int tile, void* stream) {
+               int nsplit, int tile, int stream_k, void* stream) {
+  static int t_cus = 0, t_cap = 0;
+  static float* t_ws = nullptr;
+  static long long t_wsf = 0;
+  static int* t_cnt = nullptr;
   if (epi < 0 || epi > 4 || nsplit < 1 || (nsplit > 1 && epi != EPI_RAW) || (tile < 0 || tile >= TILE_COUNT) ||
       stride < 1 || kh < 1 || kw < 1 || B < 1)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d: bad arguments");
@@ -776,6 +817,17 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
   p.steps_total = kh * kw * cin / 32;
   p.steps_per_split = (p.steps_total + nsplit - 1) / nsplit;
   p.split_stride = (long long)p.M * cout;
+  if (stream_k) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (ensure_stream_k(dev, &t_cus, &t_ws, &t_wsf, &t_cnt, &t_cap) != FR_OK)
+      return fail(nullptr, FR_ERR_HIP, "frt_conv2d: stream-K workspace allocation failed");
+    p.sk_cus = t_cus;
+    p.sk_ws = t_ws;
+    p.sk_ws_floats = t_wsf;
+    p.sk_cnt = t_cnt;
+    p.sk_cnt_cap = t_cap;
+  }
   hipError_t e = launch_conv(p, (ConvTile)tile, pre_scale != nullptr, (Epi)epi, nsplit, (hipStream_t)stream);
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d: ") + hipGetErrorString(e));
   return FR_OK;

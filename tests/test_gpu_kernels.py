@@ -155,3 +155,33 @@ def test_every_tile_config(tile):
     _close(got, ref)
     got, ref = _conv_case(2, 10, 96, 96, 3, 2, 1, epi=3, tile=tile, use_pre=False, seed=90 + tile)
     _close(got, ref)
+
+
+def _conv_case_sk(B, H, cin, cout, k, stride, pad, epi, tile, use_pre, seed):
+    got1, ref = _conv_case(B, H, cin, cout, k, stride, pad, epi, tile, use_pre, seed)  # grid mode
+    import tests._frt as F_
+    orig = F_.conv2d
+
+    def sk(*a, **kw):
+        kw["stream_k"] = 1
+        return orig(*a, **kw)
+    F_.conv2d = sk
+    try:
+        a, _ = _conv_case(B, H, cin, cout, k, stride, pad, epi, tile, use_pre, seed)
+        b, _ = _conv_case(B, H, cin, cout, k, stride, pad, epi, tile, use_pre, seed)
+    finally:
+        F_.conv2d = orig
+    return got1, a, b, ref
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+def test_stream_k_schedule_matches_and_is_deterministic(tile):
+    # 8*28*28 = 6272 rows: fewer tiles than the persistent grid, so every tile is cut
+    # across blocks and finished by the last arriver (slab sum in block order)
+    grid, a, b, ref = _conv_case_sk(8, 28, 128, 256, 3, 1, 1, epi=1, tile=tile, use_pre=True, seed=100 + tile)
+    _close(a, ref)
+    assert torch.equal(a, b), "stream-K result depends on arrival order"
+    # more tiles than blocks: whole-tile rounds + a stream-K tail; stride-2 residual epilogue
+    grid, a, b, ref = _conv_case_sk(64, 28, 128, 128, 3, 2, 1, epi=2, tile=tile, use_pre=False, seed=110 + tile)
+    _close(a, ref)
+    assert torch.equal(a, b)
