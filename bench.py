@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--topk", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
-    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per conv launch (optional)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per conv launch (tools/prof_summary.py --json); "
+                         "default: the newest profiles/r*/layers_pmc.json")
     return ap.parse_args()
 
 
@@ -139,10 +141,18 @@ def main():
         faces = world * args.batch * args.steps
         conv_tflops = prof["conv_flop"] / (prof["conv_ms"] * 1e-3) / 1e12 if prof["conv_ms"] > 0 else 0.0
         per_launch_flop = prof["conv_flop"] / max(prof["conv_launches"], 1)
-        traffic = None
-        if args.traffic_json and os.path.exists(args.traffic_json):
-            with open(args.traffic_json) as f:
-                traffic = json.load(f).get("hbm_bytes_per_conv_launch")
+        traffic, traffic_src, alg_bytes = None, None, None
+        tj = args.traffic_json
+        if tj is None:
+            import glob
+            cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "layers_pmc.json")))
+            tj = cands[-1] if cands else None
+        if tj and os.path.exists(tj) and args.arch == "ir_101" and args.batch == 256:
+            with open(tj) as f:
+                pj = json.load(f)
+            traffic = pj.get("hbm_bytes_per_conv_launch")
+            alg_bytes = pj.get("alg_bytes_per_conv_launch")
+            traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
         out = {
             "metric": METRIC,
             "value": round(faces / tmax, 2),
@@ -166,6 +176,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "conv_mfma_kernel (all conv/FC launches)",
                          "achieved": round(conv_tflops, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(conv_tflops / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "alg_bytes_per_launch": alg_bytes,
                          "launches": prof["conv_launches"], "flop_per_launch": per_launch_flop,
                          "avg_launch_ms": round(prof["conv_ms"] / max(prof["conv_launches"], 1), 5),
                          "conv_share_of_step": round(prof["conv_ms"] / max(prof["total_ms"], 1e-9), 4)},

@@ -22,19 +22,44 @@ PEAK = 157.3
 
 
 def layers(arch, B):
-    out = [("stem", 2.0 * B * 112 * 112 * 64 * 27)]
+    """(name, algorithmic FLOP, algorithmic HBM bytes) per launch of one B-image forward."""
+    f4 = 4.0
+    out = [("stem", 2.0 * B * 112 * 112 * 64 * 27, B * 112 * 112 * 3 + f4 * B * 112 * 112 * 64)]
     hw = 112
     for i, (cin, d, s) in enumerate(block_specs(arch)):
         st = {64: 1, 128: 2, 256: 3, 512: 4}[d]
-        out.append((f"s{st}.conv1.{cin}->{d}@{hw}", 2.0 * B * hw * hw * d * 9 * cin))
+        x_b = f4 * B * hw * hw * cin
+        out.append((f"s{st}.conv1.{cin}->{d}@{hw}", 2.0 * B * hw * hw * d * 9 * cin,
+                    x_b + f4 * d * 9 * cin + f4 * B * hw * hw * d))
         ho = hw // s
+        y_b = f4 * B * ho * ho * d
         if cin != d:
-            out.append((f"s{st}.shortcut1x1.{cin}->{d}@{ho}", 2.0 * B * ho * ho * d * cin))
-        out.append((f"s{st}.conv2.{d}->{d}@{ho}{'/s2' if s == 2 else ''}", 2.0 * B * ho * ho * d * 9 * d))
+            out.append((f"s{st}.shortcut1x1.{cin}->{d}@{ho}", 2.0 * B * ho * ho * d * cin,
+                        x_b / (s * s) + f4 * d * cin + y_b))
+        # conv2 reads r (B*hw*hw*d), weights, the residual (y-sized) and writes y
+        out.append((f"s{st}.conv2.{d}->{d}@{ho}{'/s2' if s == 2 else ''}", 2.0 * B * ho * ho * d * 9 * d,
+                    f4 * B * hw * hw * d + f4 * d * 9 * d + 2 * y_b))
         hw = ho
-    out.append(("head.fc7x7", 2.0 * B * 512 * 25088))
-    out.append(("head_reduce", 0.0))
+    out.append(("head.fc7x7", 2.0 * B * 512 * 25088, f4 * B * 25088 + f4 * 512 * 25088 + f4 * 49 * B * 512))
+    out.append(("head_reduce", 0.0, f4 * 49 * B * 512 + f4 * B * 512))
     return out
+
+
+def align(rows, L, B):
+    """[(layer name, row)] for every B-image forward found in a sorted kernel-trace."""
+    stem_grid = B * 112 * 256
+    found = []
+    i = 0
+    while i < len(rows):
+        r = rows[i]
+        if "stem_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == stem_grid and i + len(L) <= len(rows):
+            seq = rows[i:i + len(L)]
+            if "head_reduce" in seq[-1]["Kernel_Name"]:
+                found.append([(n[0], d) for n, d in zip(L, seq)])
+                i += len(L)
+                continue
+        i += 1
+    return found
 
 
 def read_csv(path):
@@ -53,81 +78,74 @@ def main():
     rows = read_csv(glob.glob(os.path.join(a.trace_dir, "*kernel_trace.csv"))[0])
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     L = layers(a.arch, a.batch)
-    stem_grid = a.batch * 112 * 256
+    fwds = align(rows, L, a.batch)
     per = collections.defaultdict(list)
-    fwd = 0
-    i = 0
-    while i < len(rows):
-        r = rows[i]
-        if "stem_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == stem_grid and i + len(L) <= len(rows):
-            seq = rows[i:i + len(L)]
-            if "head_reduce" in seq[-1]["Kernel_Name"]:
-                for (name, flop), d in zip(L, seq):
-                    ns = int(d["End_Timestamp"]) - int(d["Start_Timestamp"])
-                    per[name].append((ns, flop, d["Kernel_Name"], int(d.get("Dispatch_Id", 0))))
-                fwd += 1
-                i += len(L)
-                continue
-        i += 1
-    # PMC bytes keyed by dispatch id
-    pmc = {}
+    for fw in fwds:
+        for name, d in fw:
+            per[name].append(int(d["End_Timestamp"]) - int(d["Start_Timestamp"]))
+    # PMC: counters per dispatch of the aligned forwards in each PMC pass
+    pmc = collections.defaultdict(lambda: collections.defaultdict(list))  # counter -> layer -> [values]
     for d in a.pmc:
+        prow = read_csv(glob.glob(os.path.join(d, "*kernel_trace.csv"))[0])
+        prow.sort(key=lambda r: int(r["Start_Timestamp"]))
+        vals = collections.defaultdict(dict)
         for c in read_csv(glob.glob(os.path.join(d, "*counter_collection.csv"))[0]):
-            pmc.setdefault(c["Counter_Name"], {})
-            pmc[c["Counter_Name"]].setdefault((c["Kernel_Name"], int(c["Grid_Size"])), []).append(
-                float(c["Counter_Value"]))
-    # group layer names into classes (strip block index by shape)
-    cls = collections.OrderedDict()
-    for name, _f in L:
-        cls.setdefault(name, [])
+            k = int(c["Dispatch_Id"])
+            vals[k][c["Counter_Name"]] = vals[k].get(c["Counter_Name"], 0.0) + float(c["Counter_Value"])
+        for fw in align(prow, L, a.batch):
+            for name, r in fw:
+                for cn, v in vals.get(int(r["Dispatch_Id"]), {}).items():
+                    pmc[cn][name].append(v)
+    print(f"forwards aligned: {len(fwds)}")
+    hdr = f"{'layer':38s} {'n/fwd':>5s} {'avg us':>9s} {'TF/s':>7s} {'%peak':>6s} {'%time':>6s} {'alg MB':>8s}"
+    if pmc:
+        hdr += f" {'HBM MB':>8s} {'HBM/alg':>7s}"
+    print(hdr)
+    counts = collections.Counter(n for n, _f, _b in L)
+    total_time = sum(counts[n] * sum(v) / len(v) for n, v in per.items()) if per else 1.0
+    summary, seen = [], set()
     tot_ns = tot_flop = conv_ns = conv_flop = 0.0
-    print(f"forwards aligned: {fwd}")
-    print(f"{'layer class':38s} {'n/fwd':>5s} {'avg us':>9s} {'TF/s':>7s} {'%peak':>6s} {'%time':>6s}")
-    agg = collections.OrderedDict()
-    for name, flop in L:
-        v = per[name]
-        if not v:
+    conv_alg = conv_hbm = conv_n = 0.0
+    for name, flop, alg in L:
+        if name in seen or not per[name]:
             continue
-        key = name
-        agg.setdefault(key, [0, 0.0, 0.0])
-        agg[key][0] += 1
-    total_time = sum(sum(x[0] for x in per[n]) for n in per) / max(fwd, 1)
-    summary = []
-    for name in agg:
+        seen.add(name)
         v = per[name]
-        cnt = agg[name][0]
-        avg_ns = sum(x[0] for x in v) / len(v)
-        flop = v[0][1]
+        cnt = counts[name]
+        avg_ns = sum(v) / len(v)
         tf = flop / (avg_ns * 1e-9) / 1e12 if avg_ns else 0.0
         share = avg_ns * cnt / total_time
         tot_ns += avg_ns * cnt
         tot_flop += flop * cnt
-        if "conv" in name or "shortcut" in name or "head.fc" in name:
+        row = {"layer": name, "per_fwd": cnt, "avg_us": avg_ns / 1e3, "tflops": tf, "alg_bytes": alg}
+        line = f"{name:38s} {cnt:5d} {avg_ns / 1e3:9.1f} {tf:7.1f} {100 * tf / PEAK:6.1f} {100 * share:6.1f} {alg / 1e6:8.1f}"
+        is_conv = "conv" in name or "shortcut" in name or "head.fc" in name
+        if is_conv:
             conv_ns += avg_ns * cnt
             conv_flop += flop * cnt
-        summary.append({"layer": name, "per_fwd": cnt, "avg_us": avg_ns / 1e3, "tflops": tf, "kernel": v[0][2]})
-        print(f"{name:38s} {cnt:5d} {avg_ns / 1e3:9.1f} {tf:7.1f} {100 * tf / PEAK:6.1f} {100 * share:6.1f}")
+        if pmc:
+            fe = pmc.get("FETCH_SIZE", {}).get(name, [])
+            wr = pmc.get("WRITE_SIZE", {}).get(name, [])
+            if fe and wr:
+                hbm = 2 * 1024 * sum(fe) / len(fe) + 1024 * sum(wr) / len(wr)
+                row["hbm_bytes"] = hbm
+                line += f" {hbm / 1e6:8.1f} {hbm / alg:7.2f}"
+                if is_conv:
+                    conv_alg += alg * cnt
+                    conv_hbm += hbm * cnt
+                    conv_n += cnt
+        summary.append(row)
+        print(line)
     print(f"forward: {tot_ns / 1e6:.3f} ms, {tot_flop / 1e12:.3f} TFLOP -> {tot_flop / tot_ns / 1e3:.1f} TF/s; "
           f"conv family {conv_flop / conv_ns / 1e3:.1f} TF/s = {100 * conv_flop / conv_ns / 1e3 / PEAK:.1f}% of peak")
-    res = {"forwards": fwd, "forward_ms": tot_ns / 1e6, "conv_tflops": conv_flop / conv_ns / 1e3, "layers": summary}
-    if pmc:
-        # per-launch HBM bytes of the conv family: FETCH_SIZE (KB, x2 on gfx950 wide streams) + WRITE_SIZE (KB)
-        f_tot = w_tot = n_l = 0.0
-        for (kname, grid), vals in pmc.get("FETCH_SIZE", {}).items():
-            if "conv_mfma" in kname:
-                f_tot += sum(vals)
-                n_l += len(vals)
-        for (kname, grid), vals in pmc.get("WRITE_SIZE", {}).items():
-            if "conv_mfma" in kname:
-                w_tot += sum(vals)
-        if n_l:
-            fetch_b = 2 * f_tot * 1024 / n_l
-            write_b = w_tot * 1024 / n_l
-            res["hbm_bytes_per_conv_launch"] = fetch_b + write_b
-            res["fetch_bytes_per_conv_launch_x2"] = fetch_b
-            res["write_bytes_per_conv_launch"] = write_b
-            print(f"PMC conv family: {n_l:.0f} launches, FETCH x2 {fetch_b / 1e6:.1f} MB + WRITE {write_b / 1e6:.1f} MB "
-                  f"per launch")
+    res = {"forwards": len(fwds), "forward_ms": tot_ns / 1e6, "conv_tflops": conv_flop / conv_ns / 1e3,
+           "conv_launches_per_forward": sum(counts[n] for n in counts if "conv" in n or "shortcut" in n or "head.fc" in n),
+           "layers": summary}
+    if conv_n:
+        res["hbm_bytes_per_conv_launch"] = conv_hbm / conv_n
+        res["alg_bytes_per_conv_launch"] = conv_alg / conv_n
+        print(f"PMC conv family per launch: HBM {conv_hbm / conv_n / 1e6:.1f} MB (FETCH x2 + WRITE) vs algorithmic "
+              f"{conv_alg / conv_n / 1e6:.1f} MB -> {conv_hbm / conv_alg:.2f}x")
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)
