@@ -41,9 +41,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--arch", default="ir_101")
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c3",
+                    help="BASELINE.json config: c2 IR-50 embed-only B=256; c3 IR-101 embed+match B=256 G=1k "
+                         "(default, the headline metric); c5 IR-101 embed+match B=256/GPU G=100k")
+    ap.add_argument("--arch", default=None)
     ap.add_argument("--batch", type=int, default=256, help="crops per GPU per step")
-    ap.add_argument("--gallery", type=int, default=1000)
+    ap.add_argument("--gallery", type=int, default=None, help="gallery rows (0 = embed only)")
     ap.add_argument("--topk", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
@@ -67,6 +70,8 @@ def cpu_baseline(arch, sd, gallery_np, crops, budget_s):
     while done < len(crops):
         e = rp.extract_embeddings_batch(model, list(crops[done:done + 32]), batch_size=32)
         for q in e:
+            if gallery_np.shape[0] == 0:
+                break
             gal = np.vstack([gallery_np[i] for i in range(gallery_np.shape[0])])  # per-query vstack, as the reference
             rp.search(gal, ids, names, q, top_k=5)
         done += len(e)
@@ -74,12 +79,19 @@ def cpu_baseline(arch, sd, gallery_np, crops, budget_s):
             break
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 3), "unit": "faces/s", "cores": threads, "kind": "port",
-            "sample": f"{done} crops of the bench workload ({arch}, batch 32, G={gallery_np.shape[0]} per-probe "
-                      f"vstack+sgemv+argsort search), {dt:.1f} s on {threads} host threads"}
+            "sample": f"{done} crops of the bench workload ({arch}, batch 32"
+                      + (f", G={gallery_np.shape[0]} per-probe vstack+sgemv+argsort search" if gallery_np.shape[0] else
+                         ", embed only") + f"), {dt:.1f} s on {threads} host threads"}
+
+
+PRESETS = {"c2": ("ir_50", 0), "c3": ("ir_101", 1000), "c5": ("ir_101", 100_000)}
 
 
 def main():
     args = parse()
+    arch0, gal0 = PRESETS[args.config]
+    args.arch = args.arch or arch0
+    args.gallery = gal0 if args.gallery is None else args.gallery
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -93,16 +105,21 @@ def main():
     sd = W.synthetic_state_dict(args.arch)
     emb = FaceEmbedder(architecture=args.arch, state_dict=sd, device=dev, max_batch=args.batch)
 
-    # gallery: rank 0 embeds G synthetic gallery crops on its GPU, RCCL broadcast to the others
+    # gallery: rank 0 embeds min(G, 1000) synthetic gallery crops on its GPU and grows them to G
+    # rows as normalize(e + 0.0214 z); RCCL broadcast to the other ranks
     G = args.gallery
-    gal_crops = W.synthetic_crops(G, W.CROP_SEED_GALLERY)
+    G0 = min(max(G, 1), 1000)
+    gal_crops = W.synthetic_crops(G0, W.CROP_SEED_GALLERY)
     gallery = None
-    if rank == 0:
+    if rank == 0 and G > 0:
         gallery = emb.embed_tensor(torch.from_numpy(gal_crops).to(dev))
-    if world > 1:
+        if G > G0:
+            gallery = torch.from_numpy(W.expand_gallery(gallery.cpu().numpy(), G)).to(dev)
+    if world > 1 and G > 0:
         from facerecognitionpipeline_amd.distributed import broadcast_gallery
         gallery = broadcast_gallery(gallery, G, dev, src=0)
-    emb.model.gallery_set(gallery)
+    if G > 0:
+        emb.model.gallery_set(gallery)
 
     # probes resident in HBM: noisy copies of gallery crops (rank-dependent)
     probes_np = W.probe_crops(gal_crops, args.batch, seed=W.CROP_SEED_PROBE + rank)
@@ -112,8 +129,14 @@ def main():
     score = torch.empty((args.batch, k), dtype=torch.float32, device=dev)
     e_out = torch.empty((args.batch, 512), dtype=torch.float32, device=dev)
 
+    def step():
+        if G > 0:
+            emb.model.embed_match(rgb, k, idx, score, e_out)
+        else:
+            emb.model.embed(rgb, e_out, True)
+
     for _ in range(args.warmup):
-        emb.model.embed_match(rgb, k, idx, score, e_out)
+        step()
     torch.cuda.synchronize()
     emb.model.profile_enable(True)
     emb.model.profile_read()
@@ -122,7 +145,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        emb.model.embed_match(rgb, k, idx, score, e_out)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -135,7 +158,7 @@ def main():
     tmax = t.item()
 
     # sanity: probes are noisy copies of gallery rows i % G
-    top1_ok = float((idx[:, 0].cpu().numpy() == np.arange(args.batch) % G).mean())
+    top1_ok = float((idx[:, 0].cpu().numpy() == np.arange(args.batch) % G0).mean()) if G > 0 else None
 
     if rank == 0:
         faces = world * args.batch * args.steps
@@ -147,14 +170,16 @@ def main():
             import glob
             cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "layers_pmc.json")))
             tj = cands[-1] if cands else None
-        if tj and os.path.exists(tj) and args.arch == "ir_101" and args.batch == 256:
+        if tj and os.path.exists(tj) and args.arch == "ir_101" and args.batch == 256 and G == 1000:
             with open(tj) as f:
                 pj = json.load(f)
             traffic = pj.get("hbm_bytes_per_conv_launch")
             alg_bytes = pj.get("alg_bytes_per_conv_launch")
             traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
         out = {
-            "metric": METRIC,
+            "metric": METRIC if args.config == "c3" else (
+                f"faces/sec embed-only ({args.arch.upper().replace('_', '-')}, 112×112)" if G == 0 else
+                f"faces/sec embed+match ({args.arch.upper().replace('_', '-')}, 112×112, gallery={G})"),
             "value": round(faces / tmax, 2),
             "unit": "faces/s",
             "n_gpus": world,
@@ -166,12 +191,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded uint8 crops; seeded random-init AdaFace weights)",
-            "config": {"workload": f"C3: {args.arch.upper().replace('_', '-')} AdaFace embed + cosine top-{k} match "
-                                   f"vs {G}-row gallery, batch {args.batch}/GPU, 112x112 uint8 RGB",
+            "config": {"workload": (f"{args.config.upper()}: {args.arch.upper().replace('_', '-')} AdaFace embed"
+                                    + (f" + cosine top-{k} match vs {G}-row gallery" if G > 0 else " only")
+                                    + f", batch {args.batch}/GPU, 112x112 uint8 RGB"),
                        "arch": args.arch, "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "gallery": G, "top_k": k, "parallelism": f"dp{world}",
                        "gallery_exchange": "rccl broadcast" if world > 1 else "none"},
             "flop_per_face": flop_per_face(args.arch, G),
+            "path_tflops": round(faces / tmax * flop_per_face(args.arch, G) / 1e12, 2),
             "top1_self_match": top1_ok,
             "roofline": {"bound": "mfma", "kernel": "conv_mfma_kernel (all conv/FC launches)",
                          "achieved": round(conv_tflops, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -183,7 +210,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             sample = W.probe_crops(gal_crops, 256, seed=W.CROP_SEED_PROBE)
-            out["cpu_baseline"] = cpu_baseline(args.arch, sd, gallery.cpu().numpy(), sample, args.cpu_seconds)
+            gnp = gallery.cpu().numpy() if G > 0 else np.zeros((0, 512), np.float32)
+            out["cpu_baseline"] = cpu_baseline(args.arch, sd, gnp, sample, args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -198,9 +198,101 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sco
   }
 }
 
+// Single-pass form for k <= KMAX: one 256-thread block per row.  Each thread keeps its
+// best KMAX (score, index) pairs of a strided slice in registers (unrolled insertion, no
+// runtime-indexed arrays), then k block-wide arg-max rounds pop the global best in order.
+template <int KMAX>
+__global__ __launch_bounds__(256) void topk_small_kernel(const float* __restrict__ scores, int G, int k,
+                                                         int32_t* __restrict__ idx, float* __restrict__ val) {
+  __shared__ float s_s[4];
+  __shared__ int s_i[4];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* r = scores + (long long)row * G;
+  float ls[KMAX];
+  int li[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    ls[j] = -INFINITY;
+    li[j] = 0x7fffffff;
+  }
+  auto push = [&](float sv, int iv) {
+    if (sv != sv || !ranks_before(sv, iv, ls[KMAX - 1], li[KMAX - 1])) return;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {  // bubble the new pair into the sorted list
+      if (ranks_before(sv, iv, ls[j], li[j])) {
+        const float ts = ls[j];
+        const int ti = li[j];
+        ls[j] = sv;
+        li[j] = iv;
+        sv = ts;
+        iv = ti;
+      }
+    }
+  };
+  const bool vec = (G & 3) == 0 && (((unsigned long long)r) & 15) == 0;
+  if (vec) {
+    const float4* r4 = reinterpret_cast<const float4*>(r);
+    for (int g = tid; g < G / 4; g += 256) {
+      const float4 v = r4[g];
+      push(v.x, 4 * g);
+      push(v.y, 4 * g + 1);
+      push(v.z, 4 * g + 2);
+      push(v.w, 4 * g + 3);
+    }
+  } else {
+    for (int g = tid; g < G; g += 256) push(r[g], g);
+  }
+  // k rounds of block arg-max over the list heads; the owning thread pops its head
+  for (int t = 0; t < k; ++t) {
+    float bs = ls[0];
+    int bi = li[0];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float os = __shfl_xor(bs, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ranks_before(os, oi, bs, bi)) {
+        bs = os;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      s_s[wid] = bs;
+      s_i[wid] = bi;
+    }
+    __syncthreads();
+    bs = s_s[0];
+    bi = s_i[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w)
+      if (ranks_before(s_s[w], s_i[w], bs, bi)) {
+        bs = s_s[w];
+        bi = s_i[w];
+      }
+    __syncthreads();
+    if (tid == 0) {
+      idx[(long long)row * k + t] = bi == 0x7fffffff ? -1 : bi;
+      val[(long long)row * k + t] = bs;
+    }
+    if (li[0] == bi && bi != 0x7fffffff) {  // indices are unique: exactly one owner pops
+#pragma unroll
+      for (int j = 0; j < KMAX - 1; ++j) {
+        ls[j] = ls[j + 1];
+        li[j] = li[j + 1];
+      }
+      ls[KMAX - 1] = -INFINITY;
+      li[KMAX - 1] = 0x7fffffff;
+    }
+  }
+}
+
 hipError_t launch_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, hipStream_t s) {
   if (n <= 0 || k <= 0) return hipSuccess;
-  hipLaunchKernelGGL(topk_kernel, dim3((n + 3) / 4), dim3(256), 0, s, scores, n, G, k, idx, val);
+  if (k <= 8) {
+    hipLaunchKernelGGL(topk_small_kernel<8>, dim3(n), dim3(256), 0, s, scores, G, k, idx, val);
+  } else {
+    hipLaunchKernelGGL(topk_kernel, dim3((n + 3) / 4), dim3(256), 0, s, scores, n, G, k, idx, val);
+  }
   return hipGetLastError();
 }
 
