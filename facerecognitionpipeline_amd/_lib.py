@@ -38,6 +38,9 @@ _SIGNATURES = {
     "fr_match_topk": (_I, [_P, _P, _I, _I, _P, _P, _P]),
     "fr_match_topk_host": (_I, [_P, _P, _I, _I, _P, _P]),
     "fr_embed_match": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
+    "fr_align_faces": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P, _P]),
+    "fr_warp_affine": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P]),
+    "fr_blur_scores": (_I, [_P, _P, _I, _I, _P]),
     "fr_profile_enable": (_I, [_P, _I]),
     "fr_profile_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
@@ -150,6 +153,30 @@ class Handle:
                     emb: Optional[torch.Tensor] = None) -> None:
         check(self._lib.fr_embed_match(self.h, ptr(rgb), rgb.shape[0], int(k), ptr(idx), ptr(score), ptr(emb),
                                        stream_of(self.device)), self.h)
+
+    # -- alignment / quality ----------------------------------------------
+    def align_faces(self, frame: torch.Tensor, landmarks, out_size: int, out: torch.Tensor):
+        """frame: uint8 [H,W,3] on device; landmarks: host float32 [n,5,2] -> out [n,S,S,3]; returns tforms."""
+        import numpy as np
+        lm = np.ascontiguousarray(landmarks, dtype=np.float32)
+        n = lm.shape[0]
+        tf = np.empty((n, 2, 3), dtype=np.float64)
+        check(self._lib.fr_align_faces(self.h, ptr(frame), frame.shape[0], frame.shape[1], lm.ctypes.data, n,
+                                       int(out_size), ptr(out), tf.ctypes.data, stream_of(self.device)), self.h)
+        return tf
+
+    def warp_affine(self, frame: torch.Tensor, tforms, out_size: int, out: torch.Tensor) -> None:
+        import numpy as np
+        tf = np.ascontiguousarray(tforms, dtype=np.float64)
+        check(self._lib.fr_warp_affine(self.h, ptr(frame), frame.shape[0], frame.shape[1], tf.ctypes.data,
+                                       tf.shape[0], int(out_size), ptr(out), stream_of(self.device)), self.h)
+
+    def blur_scores(self, crops: torch.Tensor):
+        import numpy as np
+        n = crops.shape[0]
+        out = np.empty(n, dtype=np.float64)
+        check(self._lib.fr_blur_scores(self.h, ptr(crops), n, crops.shape[1], out.ctypes.data), self.h)
+        return out
 
     # -- profiling ---------------------------------------------------------
     def profile_enable(self, on: bool = True) -> None:

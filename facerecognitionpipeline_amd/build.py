@@ -22,7 +22,7 @@ LIB = os.path.join(PKG, "libfrhip.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = "gfx950"
-SOURCES = ["conv_mfma.hip", "embed_misc.hip", "frhip_runtime.cpp"]
+SOURCES = ["conv_mfma.hip", "embed_misc.hip", "align.hip", "frhip_runtime.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
 LDFLAGS = ["-shared", f"--offload-arch={ARCH}", f"-Wl,-rpath,{ROCM}/lib", "-Wl,--no-undefined"]

@@ -76,4 +76,12 @@ hipError_t launch_l2norm_rows(const float* q, float* out, int n, int d, hipStrea
 // Per row of a [n][G] score matrix: top-k by (score desc, index asc).
 hipError_t launch_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, hipStream_t s);
 
+// warpAffine INTER_LINEAR / BORDER_CONSTANT 0 of n crops from one uint8 RGB frame;
+// minv: device [n][6] inverse maps (double), out: [n][S][S][3].
+hipError_t launch_warp_affine(const uint8_t* frame, int H, int W, const double* minv, int n, int S, uint8_t* out,
+                              hipStream_t s);
+
+// Laplacian variance of the gray image of n uint8 RGB crops [n][S][S][3] -> var[n] (double).
+hipError_t launch_blur(const uint8_t* crops, int n, int S, double* var, hipStream_t s);
+
 }  // namespace frhip

@@ -124,6 +124,12 @@ struct fr_handle {
   void* match_io = nullptr;
   size_t match_io_cap = 0;
 
+  // alignment / quality workspace
+  void* align_m = nullptr;  // [n][6] inverse affine maps (double)
+  size_t align_m_cap = 0;
+  void* blur_out = nullptr;  // [n] double
+  size_t blur_out_cap = 0;
+
   // stream-K workspace shared by every body conv launch (launches are stream-ordered)
   int cus = 0;
   float* sk_ws = nullptr;
@@ -155,6 +161,8 @@ struct fr_handle {
     (void)hipFree(match_io);
     (void)hipFree(sk_ws);
     (void)hipFree(sk_cnt);
+    (void)hipFree(align_m);
+    (void)hipFree(blur_out);
   }
 };
 
@@ -449,6 +457,112 @@ int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float
   return FR_OK;
 }
 
+// ---- FaceAligner (face_recognition.py:50-75) host side: cv2.estimateAffinePartial2D
+// semantics for 5 landmarks, and warpAffine's inverse.  Same IEEE operation order as
+// oracle/align_ref.py so both produce identical doubles.
+#pragma clang fp contract(off)
+void ls_similarity(const double* src, const double* dst, const int* idx, int n, double M[6]) {
+  double sx = 0, sy = 0, dx = 0, dy = 0;
+  for (int k = 0; k < n; ++k) {
+    const int i = idx[k];
+    sx += src[2 * i];
+    sy += src[2 * i + 1];
+    dx += dst[2 * i];
+    dy += dst[2 * i + 1];
+  }
+  sx /= n;
+  sy /= n;
+  dx /= n;
+  dy /= n;
+  double num_a = 0, num_b = 0, den = 0;
+  for (int k = 0; k < n; ++k) {
+    const int i = idx[k];
+    const double px = src[2 * i] - sx, py = src[2 * i + 1] - sy;
+    const double qx = dst[2 * i] - dx, qy = dst[2 * i + 1] - dy;
+    num_a += px * qx + py * qy;
+    num_b += px * qy - py * qx;
+    den += px * px + py * py;
+  }
+  const double a = den != 0 ? num_a / den : 0.0, b = den != 0 ? num_b / den : 0.0;
+  M[0] = a;
+  M[1] = -b;
+  M[2] = dx - (a * sx - b * sy);
+  M[3] = b;
+  M[4] = a;
+  M[5] = dy - (b * sx + a * sy);
+}
+
+int count_inliers(const double M[6], const double* src, const double* dst, int n, double thr, bool* in) {
+  int c = 0;
+  for (int i = 0; i < n; ++i) {
+    const double px = M[0] * src[2 * i] + M[1] * src[2 * i + 1] + M[2];
+    const double py = M[3] * src[2 * i] + M[4] * src[2 * i + 1] + M[5];
+    const double ex = px - dst[2 * i], ey = py - dst[2 * i + 1];
+    in[i] = std::sqrt(ex * ex + ey * ey) < thr;
+    c += in[i];
+  }
+  return c;
+}
+
+void fit_similarity(const float* src_f, const float* dst_f, int n, double M[6]) {
+  double src[16], dst[16];
+  int all[8];
+  bool in[8];
+  for (int i = 0; i < n; ++i) {
+    src[2 * i] = src_f[2 * i];
+    src[2 * i + 1] = src_f[2 * i + 1];
+    dst[2 * i] = dst_f[2 * i];
+    dst[2 * i + 1] = dst_f[2 * i + 1];
+    all[i] = i;
+  }
+  ls_similarity(src, dst, all, n, M);
+  if (count_inliers(M, src, dst, n, 3.0, in) == n) return;
+  double best[6];
+  int best_n = -1;
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      const int pair[2] = {i, j};
+      double Mi[6];
+      ls_similarity(src, dst, pair, 2, Mi);
+      const int c = count_inliers(Mi, src, dst, n, 3.0, in);
+      if (c > best_n) {
+        best_n = c;
+        memcpy(best, Mi, sizeof(best));
+      }
+    }
+  int sel[8], ns = 0;
+  count_inliers(best, src, dst, n, 3.0, in);
+  for (int i = 0; i < n; ++i)
+    if (in[i]) sel[ns++] = i;
+  if (ns >= 2)
+    ls_similarity(src, dst, sel, ns, M);
+  else
+    memcpy(M, best, sizeof(best));
+}
+
+void invert_affine(const double Mf[6], double Mi[6]) {
+  double m[6];
+  memcpy(m, Mf, sizeof(m));
+  double D = m[0] * m[4] - m[1] * m[3];
+  D = D != 0 ? 1. / D : 0;
+  const double A11 = m[4] * D, A22 = m[0] * D;
+  m[0] = A11;
+  m[1] *= -D;
+  m[3] *= -D;
+  m[4] = A22;
+  const double b1 = -m[0] * m[2] - m[1] * m[5];
+  const double b2 = -m[3] * m[2] - m[4] * m[5];
+  m[2] = b1;
+  m[5] = b2;
+  memcpy(Mi, m, sizeof(m));
+}
+#pragma clang fp contract(on)
+
+void reference_template(int S, float t[10]) {
+  const double r[10] = {0.34, 0.46, 0.66, 0.46, 0.50, 0.61, 0.37, 0.74, 0.63, 0.74};
+  for (int i = 0; i < 10; ++i) t[i] = (float)(r[i] * S);
+}
+
 const std::vector<float>* getp(fr_handle* h, const std::string& k) {
   auto it = h->params.find(k);
   return it == h->params.end() ? nullptr : &it->second;
@@ -472,8 +586,8 @@ int fr_create(const char* architecture, const char* model_type, int device, int 
     return fail(nullptr, FR_ERR_UNSUPPORTED, "model_type 'arcface' (ONNX/onnxruntime path) is not implemented");
   if (mt != "adaface")
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "Unknown model_type: " + mt + ". Must be 'adaface' or 'arcface'");
-  if (max_batch < 1 || max_batch > 2048)
-    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "max_batch must be in [1, 2048]");
+  if (max_batch < 1 || max_batch > 512)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "max_batch must be in [1, 512]");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(nullptr, FR_ERR_HIP, "no HIP device available");
@@ -741,6 +855,73 @@ int fr_embed_match(fr_handle* h, const uint8_t* rgb, int n, int k, int32_t* idx,
   return match_device(h, emb, n, k, idx, score, s);
 }
 
+int fr_align_faces(fr_handle* h, const uint8_t* frame, int height, int width, const float* landmarks, int n,
+                   int out_size, uint8_t* out, double* tforms, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < 0 || height <= 0 || width <= 0 || out_size <= 0 || out_size > 1024 ||
+      (n > 0 && (!frame || !landmarks || !out)))
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "bad alignment arguments");
+  if (n == 0) return FR_OK;
+  DeviceGuard dg(h->device);
+  float tmpl[10];
+  reference_template(out_size, tmpl);
+  std::vector<double> minv((size_t)n * 6);
+  for (int f = 0; f < n; ++f) {
+    double Mf[6];
+    fit_similarity(landmarks + (size_t)f * 10, tmpl, 5, Mf);
+    if (tforms) memcpy(tforms + (size_t)f * 6, Mf, sizeof(Mf));
+    invert_affine(Mf, &minv[(size_t)f * 6]);
+  }
+  int rc = ensure_buf(h, &h->align_m, &h->align_m_cap, minv.size() * sizeof(double));
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  FR_HIP(h, hipMemcpyAsync(h->align_m, minv.data(), minv.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  hipError_t e = launch_warp_affine(frame, height, width, (const double*)h->align_m, n, out_size, out, s);
+  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("warp launch: ") + hipGetErrorString(e));
+  // the host copy of the maps must outlive the async H2D copy
+  FR_HIP(h, hipStreamSynchronize(s));
+  return FR_OK;
+}
+
+int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, const double* tforms, int n,
+                   int out_size, uint8_t* out, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < 0 || height <= 0 || width <= 0 || out_size <= 0 || out_size > 1024 ||
+      (n > 0 && (!frame || !tforms || !out)))
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "bad warp arguments");
+  if (n == 0) return FR_OK;
+  DeviceGuard dg(h->device);
+  std::vector<double> minv((size_t)n * 6);
+  for (int f = 0; f < n; ++f) invert_affine(tforms + (size_t)f * 6, &minv[(size_t)f * 6]);
+  int rc = ensure_buf(h, &h->align_m, &h->align_m_cap, minv.size() * sizeof(double));
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  FR_HIP(h, hipMemcpyAsync(h->align_m, minv.data(), minv.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  hipError_t e = launch_warp_affine(frame, height, width, (const double*)h->align_m, n, out_size, out, s);
+  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("warp launch: ") + hipGetErrorString(e));
+  FR_HIP(h, hipStreamSynchronize(s));
+  return FR_OK;
+}
+
+int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* scores) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < 0 || size < 3 || size > 256 || (n > 0 && (!crops || !scores)))
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "bad blur arguments (size in [3, 256])");
+  if (n == 0) return FR_OK;
+  DeviceGuard dg(h->device);
+  int rc = ensure_buf(h, &h->blur_out, &h->blur_out_cap, (size_t)n * sizeof(double));
+  if (rc) return rc;
+  hipStream_t s = nullptr;
+  hipError_t e = launch_blur(crops, n, size, (double*)h->blur_out, s);
+  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("blur launch: ") + hipGetErrorString(e));
+  FR_HIP(h, hipMemcpyAsync(scores, h->blur_out, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s));
+  FR_HIP(h, hipStreamSynchronize(s));
+  return FR_OK;
+}
+
 int fr_profile_enable(fr_handle* h, int enable) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -837,6 +1018,12 @@ int frt_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, c
              const float* bn_shift, const float* prelu, float* y, void* stream) {
   hipError_t e = launch_stem(img, B, lut, w27x64, bn_scale, bn_shift, prelu, y, (hipStream_t)stream);
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_stem: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+int frt_fit_similarity(const float* src, const float* dst, int n, double* M) {
+  if (n < 2 || n > 8) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "n in [2, 8]");
+  fit_similarity(src, dst, n, M);
   return FR_OK;
 }
 

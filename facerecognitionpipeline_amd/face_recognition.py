@@ -1,0 +1,169 @@
+"""Drop-in ``FaceAligner`` / ``FaceQualityFilter`` / ``FaceProcessor`` (face_recognition.py:50-216).
+
+Alignment (cv2.estimateAffinePartial2D + cv2.warpAffine, face_recognition.py:64-74)
+and the blur score (cv2.Laplacian variance, :94-99) run on the GPU through
+``fr_align_faces`` / ``fr_warp_affine`` / ``fr_blur_scores``, so a frame uploaded
+once yields crops that stay in HBM for ``FaceEmbedder.embed_tensor``.  Pose
+angles and the threshold logic are scalar host code, as in the reference.
+
+The detector (insightface ``FaceAnalysis('buffalo_l')`` SCRFD, :19-48) is not
+rebuilt yet (no weights or insightface offline):
+``FaceProcessor`` takes any detector object with the reference's
+``detect(image_rgb) -> [{'bbox','landmarks','det_score',...}]`` contract.
+
+Parity of the OpenCV arithmetic is UNPINNED (cv2 absent); the kernels are
+pinned bit-exactly to the restatement in ``oracle/align_ref.py``.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def reference_template(output_size: int) -> np.ndarray:
+    S = output_size
+    return np.array([[0.34 * S, 0.46 * S], [0.66 * S, 0.46 * S], [0.50 * S, 0.61 * S],
+                     [0.37 * S, 0.74 * S], [0.63 * S, 0.74 * S]], dtype=np.float32)
+
+
+class _DeviceOps:
+    """One lightweight handle for the alignment / quality kernels (no model weights)."""
+
+    def __init__(self, device=None):
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+        self._h: Optional[_lib.Handle] = None
+
+    @property
+    def handle(self) -> "_lib.Handle":
+        if self._h is None:
+            self._h = _lib.Handle("ir_50", "adaface", self.device, max_batch=1)
+        return self._h
+
+
+class FaceAligner:
+    def __init__(self, output_size: int = 112, device=None):
+        self.output_size = output_size
+        self.template = reference_template(output_size)
+        self._ops = _DeviceOps(device)
+
+    def align(self, image: np.ndarray, landmarks: np.ndarray, method: str = "similarity") -> np.ndarray:
+        """Host image in, host crop out (reference signature)."""
+        frame = torch.from_numpy(np.ascontiguousarray(image, dtype=np.uint8)).to(self._ops.device)
+        return self.align_batch(frame, np.asarray(landmarks, np.float32)[None], method)[0].cpu().numpy()
+
+    def align_batch(self, frame: torch.Tensor, landmarks: np.ndarray, method: str = "similarity") -> torch.Tensor:
+        """Device form: uint8 [H,W,3] frame on the GPU, float32 [n,5,2] landmarks -> uint8 [n,S,S,3] on the GPU."""
+        if frame.dtype != torch.uint8 or frame.dim() != 3 or frame.shape[2] != 3:
+            raise ValueError("expected a uint8 [H,W,3] RGB frame tensor")
+        lm = np.ascontiguousarray(landmarks, dtype=np.float32).reshape(-1, 5, 2)
+        S = self.output_size
+        out = torch.empty((lm.shape[0], S, S, 3), dtype=torch.uint8, device=self._ops.device)
+        frame = frame.to(self._ops.device).contiguous()
+        if method == "similarity":
+            self._ops.handle.align_faces(frame, lm, S, out)
+        else:
+            tf = np.stack([affine_from_3_points(x[:3], self.template[:3]) for x in lm])
+            self._ops.handle.warp_affine(frame, tf, S, out)
+        return out
+
+
+def affine_from_3_points(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
+    """cv2.getAffineTransform(src[:3], dst[:3]) (exact 3-point solve, float64)."""
+    s = np.asarray(src, np.float32).astype(np.float64)
+    d = np.asarray(dst, np.float32).astype(np.float64)
+    A = np.zeros((6, 6))
+    b = np.zeros(6)
+    for i in range(3):
+        A[2 * i, :3] = [s[i, 0], s[i, 1], 1.0]
+        A[2 * i + 1, 3:] = [s[i, 0], s[i, 1], 1.0]
+        b[2 * i], b[2 * i + 1] = d[i, 0], d[i, 1]
+    return np.linalg.solve(A, b).reshape(2, 3)
+
+
+class FaceQualityFilter:
+    def __init__(self, min_det_score=0.6, min_face_size=60, max_yaw=45, max_pitch=30, max_roll=30,
+                 check_blur=True, blur_threshold=100, device=None):
+        self.min_det_score = min_det_score
+        self.min_face_size = min_face_size
+        self.max_yaw = max_yaw
+        self.max_pitch = max_pitch
+        self.max_roll = max_roll
+        self.check_blur = check_blur
+        self.blur_threshold = blur_threshold
+        self._ops = _DeviceOps(device)
+
+    def compute_blur_score(self, face_image) -> float:
+        return float(self.compute_blur_scores(face_image[None] if isinstance(face_image, np.ndarray)
+                                              else face_image.unsqueeze(0))[0])
+
+    def compute_blur_scores(self, crops) -> np.ndarray:
+        """uint8 [n,S,S,3] RGB crops (host array or device tensor) -> float64 [n]."""
+        t = crops if isinstance(crops, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(crops, np.uint8))
+        if t.dim() != 4 or t.shape[3] != 3 or t.shape[1] != t.shape[2]:
+            raise ValueError("expected uint8 [n,S,S,3] RGB crops")
+        return self._ops.handle.blur_scores(t.to(self._ops.device).contiguous())
+
+    def compute_pose_angles(self, landmarks: np.ndarray) -> Dict[str, float]:
+        le, re, nose, lm, rm = [np.asarray(p) for p in landmarks]
+        eye_c = (le + re) / 2
+        d = re - le
+        roll = np.degrees(np.arctan2(d[1], d[0]))
+        yaw = np.degrees(np.arcsin(np.clip((nose[0] - eye_c[0]) / np.linalg.norm(d), -1, 1))) * 2
+        mouth_c = (lm + rm) / 2
+        pitch = ((nose[1] - eye_c[1]) / (mouth_c[1] - eye_c[1]) - 0.5) * 60
+        return {"yaw": yaw, "pitch": pitch, "roll": roll}
+
+    def is_valid(self, face_dict: Dict, face_image=None, blur_score: Optional[float] = None) -> Tuple[bool, Dict]:
+        m: Dict = {"det_score": face_dict["det_score"]}
+        if m["det_score"] < self.min_det_score:
+            return False, m
+        x0, y0, x1, y1 = face_dict["bbox"][:4]
+        m["face_size"] = min(x1 - x0, y1 - y0)
+        if m["face_size"] < self.min_face_size:
+            return False, m
+        pose = self.compute_pose_angles(face_dict["landmarks"])
+        m.update(pose)
+        if abs(pose["yaw"]) > self.max_yaw or abs(pose["pitch"]) > self.max_pitch or abs(pose["roll"]) > self.max_roll:
+            return False, m
+        if self.check_blur and (face_image is not None or blur_score is not None):
+            m["blur_score"] = blur_score if blur_score is not None else self.compute_blur_score(face_image)
+            if m["blur_score"] < self.blur_threshold:
+                return False, m
+        return True, m
+
+
+class FaceProcessor:
+    """detect -> align -> quality (face_recognition.py:160-216) with device alignment and blur."""
+
+    def __init__(self, output_size=224, det_size=(640, 640), det_thresh=0.5,
+                 quality_filter_config: Optional[Dict] = None, providers=None, detector=None, device=None):
+        if detector is None:
+            raise NotImplementedError("the SCRFD detector is not rebuilt yet: pass detector=<object with "
+                                      "detect(image_rgb) -> list of {'bbox','landmarks','det_score'}>")
+        self.detector = detector
+        self.aligner = FaceAligner(output_size=output_size, device=device)
+        self.quality_filter = FaceQualityFilter(**(quality_filter_config or {}), device=device)
+
+    def process_numpy(self, image_rgb: np.ndarray, return_all: bool = False) -> List[Dict]:
+        faces = self.detector.detect(image_rgb)
+        if len(faces) == 0:
+            return []
+        frame = torch.from_numpy(np.ascontiguousarray(image_rgb, np.uint8)).to(self.aligner._ops.device)
+        crops = self.aligner.align_batch(frame, np.stack([f["landmarks"] for f in faces]))
+        blur = self.quality_filter.compute_blur_scores(crops) if self.quality_filter.check_blur else None
+        host = crops.cpu().numpy()
+        results = []
+        for i, face in enumerate(faces):
+            ok, q = self.quality_filter.is_valid(face, None, None if blur is None else float(blur[i]))
+            if ok or return_all:
+                results.append({"aligned_face": host[i], "bbox": face["bbox"], "landmarks": face["landmarks"],
+                                "det_score": face["det_score"], "quality_metrics": q, "is_valid": ok})
+        results.sort(key=lambda x: x["det_score"] * x["quality_metrics"].get("blur_score", 1000), reverse=True)
+        if not return_all and results:
+            return [results[0]]
+        return results

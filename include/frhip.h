@@ -46,7 +46,7 @@ typedef struct fr_handle fr_handle;
  * `net.build_model(architecture)` (face_embedder.py:27-49).
  * architecture: "ir_50" | "ir_101" (also "ir_18", "ir_34"); model_type: "adaface"
  * ("arcface" -> FR_ERR_UNSUPPORTED: the ORT path is parity-unpinned).
- * max_batch: images per internal forward chunk (workspace sizing), 1..2048. */
+ * max_batch: images per internal forward chunk (workspace sizing), 1..512. */
 int fr_create(const char* architecture, const char* model_type, int device, int max_batch, fr_handle** out);
 int fr_destroy(fr_handle* h);
 
@@ -87,6 +87,24 @@ int fr_match_topk_host(fr_handle* h, const float* Q, int n, int k, int32_t* idx,
  * batched: embed(normalize=1) then match.  emb_out may be NULL.  Device pointers. */
 int fr_embed_match(fr_handle* h, const uint8_t* rgb, int n, int k, int32_t* idx, float* score, float* emb_out,
                    void* stream);
+
+/* FaceAligner.align for n faces of one frame (face_recognition.py:50-75): similarity fit of
+ * each face's 5 landmarks to the reference template (cv2.estimateAffinePartial2D semantics,
+ * host, double) then warpAffine INTER_LINEAR / BORDER_CONSTANT 0 on the device, so the crops
+ * stay in HBM for fr_embed.  frame: device uint8 [height][width][3] RGB; landmarks: host float
+ * [n][5][2]; out: device uint8 [n][out_size][out_size][3]; tforms: host double [n][2][3] forward
+ * maps as cv2 returns them, or NULL.  Synchronises (the maps are staged from the host). */
+int fr_align_faces(fr_handle* h, const uint8_t* frame, int height, int width, const float* landmarks, int n,
+                   int out_size, uint8_t* out, double* tforms, void* stream);
+/* cv2.warpAffine(frame, M, (out_size, out_size), INTER_LINEAR, BORDER_CONSTANT, 0) for n
+ * caller-supplied FORWARD maps (host double [n][2][3], e.g. cv2.getAffineTransform's for
+ * FaceAligner.align(method != 'similarity'), face_recognition.py:66-67).  Synchronises. */
+int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, const double* tforms, int n,
+                   int out_size, uint8_t* out, void* stream);
+/* FaceQualityFilter.compute_blur_score for n crops (face_recognition.py:94-99):
+ * cv2.Laplacian(cvtColor(RGB2GRAY), CV_64F).var().  crops: device uint8 [n][size][size][3];
+ * scores: host double [n].  Synchronises. */
+int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* scores);
 
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).
  * enable=1 starts recording; fr_profile_read synchronises and returns, since the

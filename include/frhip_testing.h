@@ -32,6 +32,9 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
 int frt_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, const float* bn_scale,
              const float* bn_shift, const float* prelu, float* y, void* stream);
 
+/* The host similarity fit of fr_align_faces: src/dst float [n][2] -> M double [2][3]. */
+int frt_fit_similarity(const float* src, const float* dst, int n, double* M);
+
 /* Row-wise top-k of a [n][G] score matrix (score desc, index asc). */
 int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, void* stream);
 

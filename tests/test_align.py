@@ -1,0 +1,166 @@
+"""Alignment (K7) + blur quality (K8): FaceAligner.align / FaceQualityFilter (face_recognition.py:50-158).
+
+PARITY UNPINNED against OpenCV (absent here; the reference has no aligned-crop
+fixtures).  The HIP kernels are pinned bit for bit to oracle/align_ref.py, the
+restatement of OpenCV's uint8 fixed-point arithmetic; CPU tests check the
+restatement's own invariants (identity / integer shifts copy pixels exactly,
+half-pixel shifts round half up, the fit is the least-squares similarity).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import align_ref as A
+
+
+def _faces(rng, n, H, W, S=112, jitter=2.0, scale=(1.0, 3.0)):
+    """n landmark sets: the reference template scaled/rotated/translated into the frame + noise."""
+    t = A.reference_template(S).astype(np.float64)
+    out = []
+    for _ in range(n):
+        s = rng.uniform(*scale)
+        th = rng.uniform(-0.4, 0.4)
+        R = s * np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+        c = np.array([rng.uniform(-50, W + 50), rng.uniform(-50, H + 50)])  # some faces cross the border
+        p = (t - S / 2) @ R.T + c + rng.normal(0, jitter, t.shape)
+        out.append(p)
+    return np.array(out, dtype=np.float32)
+
+
+# ---------------------------------------------------------------- CPU: the restatement
+def test_warp_identity_and_integer_shift_copy_pixels():
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, (40, 50, 3), dtype=np.uint8)
+    I = np.array([[1.0, 0, 0], [0, 1.0, 0]])
+    assert np.array_equal(A.warp_affine_linear(img, I, 32), img[:32, :32])
+    T = np.array([[1.0, 0, -3], [0, 1.0, -5]])  # dst(x,y) = src(x+3, y+5)
+    assert np.array_equal(A.warp_affine_linear(img, T, 30), img[5:35, 3:33])
+    out = A.warp_affine_linear(img, np.array([[1.0, 0, 10], [0, 1.0, 10]]), 20)
+    assert (out[:10] == 0).all() and (out[:, :10] == 0).all()  # BORDER_CONSTANT 0
+
+
+def test_warp_half_pixel_rounds_half_up():
+    img = np.zeros((4, 8, 1), np.uint8)
+    img[0, :, 0] = [10, 11, 20, 30, 40, 50, 60, 70]
+    M = np.array([[1.0, 0, -0.5], [0, 1.0, 0]])  # dst(x) = src(x + 0.5)
+    out = A.warp_affine_linear(img, M, 4)[0, :, 0]
+    assert out.tolist() == [11, 16, 25, 35]  # (10+11+1)//2, (11+20+1)//2, ...
+
+
+def test_similarity_fit_recovers_exact_similarity():
+    t = A.reference_template(112)
+    M = np.array([[0.8, -0.3, 12.5], [0.3, 0.8, -7.25]])
+    src = ((t.astype(np.float64) - M[:, 2]) @ np.linalg.inv(M[:, :2]).T).astype(np.float32)
+    got = A.fit_similarity(src, t)
+    assert np.abs(got - M).max() < 1e-4
+
+
+def test_fit_outlier_is_excluded():
+    t = A.reference_template(112).astype(np.float64)
+    src = t * 2.0 + 10
+    src[2] += 40.0  # nose far off: RANSAC drops it
+    M = A.fit_similarity(src.astype(np.float32), t.astype(np.float32))
+    assert np.abs(M - np.array([[0.5, 0, -5], [0, 0.5, -5]])).max() < 1e-9
+
+
+def test_host_fit_matches_restatement_bitwise():
+    """The C++ fit behind fr_align_faces performs the oracle's IEEE operation sequence (no GPU needed)."""
+    from facerecognitionpipeline_amd import _lib
+    lib = _lib.load()
+    lib.frt_fit_similarity.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int, ctypes.c_void_p]
+    rng = np.random.default_rng(1)
+    t = A.reference_template(112)
+    for lm in _faces(rng, 50, 1080, 1920, jitter=3.0):
+        M = np.zeros(6)
+        assert lib.frt_fit_similarity(lm.ctypes.data, t.ctypes.data, 5, M.ctypes.data) == 0
+        assert np.array_equal(M.reshape(2, 3), A.fit_similarity(lm, t))
+
+
+def test_laplacian_var_matches_direct_definition():
+    rng = np.random.default_rng(2)
+    g = rng.integers(0, 256, (112, 112), dtype=np.uint8)
+    gi = g.astype(np.int64)
+    P = np.pad(gi, 1, mode="reflect")
+    L = P[:-2, 1:-1] + P[2:, 1:-1] + P[1:-1, :-2] + P[1:-1, 2:] - 4 * gi
+    n = L.size
+    exact = (n * (L * L).sum() - L.sum() ** 2) / n ** 2
+    assert abs(A.laplacian_var(g) - exact) <= 1e-12 * exact
+
+
+def test_pose_angles_of_frontal_template():
+    p = A.pose_angles(A.reference_template(112).astype(np.float64))
+    assert abs(p["roll"]) < 1e-4 and abs(p["yaw"]) < 1e-4  # float32 template coordinates
+    assert abs(p["pitch"] - ((0.61 - 0.46) / (0.74 - 0.46) - 0.5) * 60) < 1e-4
+
+
+# ---------------------------------------------------------------- GPU: kernels vs restatement
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [112, 224])
+def test_align_kernel_bit_exact(S):
+    from facerecognitionpipeline_amd.face_recognition import FaceAligner
+    rng = np.random.default_rng(10 + S)
+    H, W = 1080, 1920
+    frame = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    lms = _faces(rng, 24, H, W, S=S)
+    al = FaceAligner(output_size=S, device="cuda:0")
+    got = al.align_batch(torch.from_numpy(frame).cuda(), lms).cpu().numpy()
+    t = A.reference_template(S)
+    for i, lm in enumerate(lms):
+        ref = A.warp_affine_linear(frame, A.fit_similarity(lm, t), S)
+        assert np.array_equal(got[i], ref), f"face {i}: {np.count_nonzero(got[i] != ref)} px differ"
+    one = al.align(frame, lms[0])                      # reference host signature
+    assert one.dtype == np.uint8 and np.array_equal(one, got[0])
+    aff = al.align_batch(torch.from_numpy(frame).cuda(), lms[:3], method="affine").cpu().numpy()
+    from facerecognitionpipeline_amd.face_recognition import affine_from_3_points
+    for i in range(3):
+        assert np.array_equal(aff[i], A.warp_affine_linear(frame, affine_from_3_points(lms[i][:3], t[:3]), S))
+
+
+@pytest.mark.gpu
+def test_blur_kernel_matches_restatement():
+    from facerecognitionpipeline_amd.face_recognition import FaceQualityFilter
+    rng = np.random.default_rng(20)
+    crops = rng.integers(0, 256, (9, 112, 112, 3), dtype=np.uint8)
+    crops[1] = 128                                    # flat crop: variance 0
+    crops[2] = crops[2] // 16 * 16
+    qf = FaceQualityFilter()
+    got = qf.compute_blur_scores(crops)
+    ref = np.array([A.blur_score(c) for c in crops])
+    assert np.allclose(got, ref, rtol=1e-12, atol=0)
+    assert got[1] == 0.0
+    big = rng.integers(0, 256, (2, 224, 224, 3), dtype=np.uint8)
+    assert np.allclose(qf.compute_blur_scores(big), [A.blur_score(c) for c in big], rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_processor_align_embed_match_stays_on_device():
+    """frame -> device align -> embed == host-aligned crops -> embed; FaceProcessor filter/sort semantics."""
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    from facerecognitionpipeline_amd.face_recognition import FaceAligner, FaceProcessor
+    rng = np.random.default_rng(30)
+    H, W = 720, 1280
+    frame = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    lms = _faces(rng, 6, H, W, S=112, scale=(1.5, 2.5))
+    emb = FaceEmbedder(architecture="ir_50", model_path="synthetic", max_batch=16)
+    al = FaceAligner(112)
+    crops_dev = al.align_batch(torch.from_numpy(frame).cuda(), lms)
+    e_dev = emb.embed_tensor(crops_dev).cpu().numpy()
+    t = A.reference_template(112)
+    host = [A.warp_affine_linear(frame, A.fit_similarity(lm, t), 112) for lm in lms]
+    assert np.array_equal(e_dev, emb.extract_embeddings_batch(host))
+
+    class FakeDetector:
+        def detect(self, image):
+            return [{"bbox": np.array([0, 0, 200, 200], np.int32), "landmarks": lm, "det_score": 0.9 - 0.01 * i}
+                    for i, lm in enumerate(lms)]
+
+    fp = FaceProcessor(output_size=112, detector=FakeDetector(),
+                       quality_filter_config={"max_yaw": 90, "max_pitch": 90, "max_roll": 90, "blur_threshold": 0})
+    out = fp.process_numpy(frame, return_all=True)
+    assert len(out) == 6
+    keys = [r["det_score"] * r["quality_metrics"]["blur_score"] for r in out]
+    assert keys == sorted(keys, reverse=True)
+    best = fp.process_numpy(frame)
+    assert len(best) == 1 and np.array_equal(best[0]["aligned_face"], out[0]["aligned_face"])
