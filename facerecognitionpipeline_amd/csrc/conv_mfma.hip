@@ -45,7 +45,6 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;
 constexpr int LDK = BK + 4;
-constexpr int NTHREADS = 256;
 
 // XCD-aware bijection: blocks b, b+8, ... share an XCD; give each XCD a contiguous run
 // of work items so neighbouring M-tiles and one weight panel share its L2.
@@ -56,13 +55,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
 }
 
 template <int BM, int BN, int WM, int WN, bool PRE, int EPI>
-__global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
-  static_assert(WM * WN == 4, "4 waves per block");
+__global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p) {
+  constexpr int NTHREADS = 64 * WM * WN;  // one wave per (wm, wn) sub-tile
+  constexpr int RPP = NTHREADS / 8;       // staged rows per pass (8 float4 per 32-channel row)
+  static_assert(BM % RPP == 0 && BN % RPP == 0, "tile rows must be a multiple of the staging pass");
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
-  constexpr int A_IT = BM / 32;  // A rows staged per thread (8 float4 per row, 32 rows per pass)
-  constexpr int B_IT = BN / 32;
+  constexpr int A_IT = BM / RPP;  // A rows staged per thread
+  constexpr int B_IT = BN / RPP;
   constexpr int ACC = TM * TN * 16;  // accumulator floats per lane
 
   __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
   const int wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int k4 = tid & 7;       // which float4 of the 32-channel K-step
-  const int rsub = tid >> 3;    // 0..31
+  const int rsub = tid >> 3;    // 0..RPP-1
 
   const int H = p.H, W = p.W, Cin = p.Cin;
   const int taps = p.KH * p.KW;
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
     int a_base[A_IT], a_iy[A_IT], a_ix[A_IT];
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
-      const int m = m0 + rsub + 32 * i;
+      const int m = m0 + rsub + RPP * i;
       if (m < p.M) {
         const int b = m / HoWo;
         const int rem = m - b * HoWo;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
     int b_base[B_IT];
 #pragma unroll
     for (int j = 0; j < B_IT; ++j) {
-      const int n = n0 + rsub + 32 * j;
+      const int n = n0 + rsub + RPP * j;
       b_base[j] = n < p.Cout ? (n * Ktot + 4 * k4) * 4 : OOB;
     }
 
@@ -190,10 +191,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
             v.w = v.w * psc.w + psh.w;
           }
         }
-        *reinterpret_cast<float4*>(As + (rsub + 32 * i) * LDK + 4 * k4) = v;
+        *reinterpret_cast<float4*>(As + (rsub + RPP * i) * LDK + 4 * k4) = v;
       }
 #pragma unroll
-      for (int j = 0; j < B_IT; ++j) *reinterpret_cast<float4*>(Bs + (rsub + 32 * j) * LDK + 4 * k4) = rb[j];
+      for (int j = 0; j < B_IT; ++j) *reinterpret_cast<float4*>(Bs + (rsub + RPP * j) * LDK + 4 * k4) = rb[j];
     };
 
     load_step(true);
@@ -390,6 +391,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_mfma_kernel(ConvParams p) {
 
 template <int BM, int BN, int WM, int WN>
 static hipError_t launch_tile(const ConvParams& p0, bool pre, Epi epi, int nsplit, hipStream_t s) {
+  constexpr int NTHREADS = 64 * WM * WN;
   ConvParams p = p0;
   p.mtiles = (p.M + BM - 1) / BM;
   p.ntiles = (p.Cout + BN - 1) / BN;
@@ -459,22 +461,26 @@ hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, in
     case TILE_64x128: return launch_tile<64, 128, 1, 4>(p, pre, epi, nsplit, s);
     case TILE_256x128: return launch_tile<256, 128, 2, 2>(p, pre, epi, nsplit, s);
     case TILE_128x256: return launch_tile<128, 256, 2, 2>(p, pre, epi, nsplit, s);
+    case TILE_128x128_W8: return launch_tile<128, 128, 2, 4>(p, pre, epi, nsplit, s);
+    case TILE_256x128_W8: return launch_tile<256, 128, 4, 2>(p, pre, epi, nsplit, s);
+    case TILE_128x64_W8: return launch_tile<128, 64, 4, 2>(p, pre, epi, nsplit, s);
+    case TILE_64x256_W8: return launch_tile<64, 256, 2, 4>(p, pre, epi, nsplit, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 int conv_tile_bm(ConvTile t) {
   switch (t) {
-    case TILE_256x64: case TILE_256x128: return 256;
-    case TILE_64x128: return 64;
+    case TILE_256x64: case TILE_256x128: case TILE_256x128_W8: return 256;
+    case TILE_64x128: case TILE_64x256_W8: return 64;
     default: return 128;
   }
 }
 
 int conv_tile_bn(ConvTile t) {
   switch (t) {
-    case TILE_256x64: case TILE_128x64: return 64;
-    case TILE_128x256: return 256;
+    case TILE_256x64: case TILE_128x64: case TILE_128x64_W8: return 64;
+    case TILE_128x256: case TILE_64x256_W8: return 256;
     default: return 128;
   }
 }

@@ -53,7 +53,11 @@ enum ConvTile : int {
   TILE_64x128 = 3,
   TILE_256x128 = 4,
   TILE_128x256 = 5,
-  TILE_COUNT = 6
+  TILE_128x128_W8 = 6,  // 8 waves (512 threads)
+  TILE_256x128_W8 = 7,
+  TILE_128x64_W8 = 8,
+  TILE_64x256_W8 = 9,
+  TILE_COUNT = 10
 };
 
 hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s);

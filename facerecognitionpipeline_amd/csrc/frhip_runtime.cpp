@@ -369,9 +369,17 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     p.sk_cnt_cap = h->sk_cnt_cap;
   }
   const double flop = 2.0 * p.M * (double)p.Cout * cw.kh * cw.kw * cw.cin;
-  // Tile per output width, from tools/conv_sweep.py on MI355X at B=256 with the stream-K
-  // schedule: 128x64 for the 64-channel stage, 64x128 otherwise.
-  const ConvTile tile = cw.cout <= 64 ? TILE_128x64 : TILE_64x128;
+  // Tile per layer shape, from tools/conv_sweep.py on MI355X at B=256 with the stream-K
+  // schedule (profiles/r01/sweep.txt): 8-wave 128x64 for the 64-channel
+  // stage and the 128-channel residual convs, 8-wave 128x128 for the 1x1 shortcuts,
+  // 8-wave 256x128 for every other 3x3 conv and the FC.
+  ConvTile tile = TILE_256x128_W8;
+  if (cw.cout <= 64 || (cw.cout == 128 && epi == EPI_AFFINE_RES && cw.kh == 3))
+    tile = TILE_128x64_W8;
+  else if (cw.kh == 1 && cw.kw == 1 && p.H > 1)
+    tile = TILE_128x128_W8;
+  else if (p.H == 1)
+    tile = TILE_64x128;  // gallery scores (1x1 GEMM)
   ProfScope ps(h, s, flop, true);
   hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));

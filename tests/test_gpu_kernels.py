@@ -148,7 +148,7 @@ def test_topk_matches_policy(G, k):
     assert np.array_equal(val.cpu().numpy(), rv)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("tile", list(range(10)))
 def test_every_tile_config(tile):
     # ragged M (2*10*10 = 200) and N = 320 (not a multiple of 64/128/256) through each tile shape
     got, ref = _conv_case(2, 10, 64, 320, 3, 1, 1, epi=1, tile=tile, use_pre=True, seed=80 + tile)
@@ -174,7 +174,7 @@ def _conv_case_sk(B, H, cin, cout, k, stride, pad, epi, tile, use_pre, seed):
     return got1, a, b, ref
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 6, 7, 8, 9])
 def test_stream_k_schedule_matches_and_is_deterministic(tile):
     # 8*28*28 = 6272 rows: fewer tiles than the persistent grid, so every tile is cut
     # across blocks and finished by the last arriver (slab sum in block order)
