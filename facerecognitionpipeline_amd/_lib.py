@@ -41,6 +41,7 @@ _SIGNATURES = {
     "fr_align_faces": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P, _P]),
     "fr_warp_affine": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P]),
     "fr_blur_scores": (_I, [_P, _P, _I, _I, _P]),
+    "fr_set_precision": (_I, [_P, _I]),
     "fr_profile_enable": (_I, [_P, _I]),
     "fr_profile_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
@@ -177,6 +178,12 @@ class Handle:
         out = np.empty(n, dtype=np.float64)
         check(self._lib.fr_blur_scores(self.h, ptr(crops), n, crops.shape[1], out.ctypes.data), self.h)
         return out
+
+    def set_precision(self, mode: str) -> None:
+        modes = {"fp32": 0, "f32": 0, "bf16x3": 1}
+        if mode not in modes:
+            raise ValueError(f"precision must be one of {sorted(modes)}")
+        check(self._lib.fr_set_precision(self.h, modes[mode]), self.h)
 
     # -- profiling ---------------------------------------------------------
     def profile_enable(self, on: bool = True) -> None:

@@ -60,7 +60,12 @@ enum ConvTile : int {
   TILE_COUNT = 10
 };
 
-hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s);
+// Arithmetic of the conv GEMM: exact-f32 MFMA (default, the parity path) or the opt-in
+// split-bf16 "bf16x3" (x = hi + lo, x.y ~= hi.hi + hi.lo + lo.hi, f32 accumulation).
+enum Precision : int { PREC_F32 = 0, PREC_BF16X3 = 1 };
+
+hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s,
+                       Precision prec = PREC_F32);
 int conv_tile_bm(ConvTile t);
 int conv_tile_bn(ConvTile t);
 

@@ -137,6 +137,7 @@ struct fr_handle {
   int* sk_cnt = nullptr;
   int sk_cnt_cap = 0;
   bool stream_k = true;
+  Precision prec = PREC_F32;
 
   // profiling
   bool prof = false;
@@ -381,7 +382,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   else if (p.H == 1)
     tile = TILE_64x128;  // gallery scores (1x1 GEMM)
   ProfScope ps(h, s, flop, true);
-  hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s);
+  hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s, h->prec);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
   return FR_OK;
 }
@@ -930,6 +931,15 @@ int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* 
   return FR_OK;
 }
 
+int fr_set_precision(fr_handle* h, int mode) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (mode != FR_PRECISION_F32 && mode != FR_PRECISION_BF16X3)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "precision must be FR_PRECISION_F32 or FR_PRECISION_BF16X3");
+  h->prec = mode == FR_PRECISION_BF16X3 ? PREC_BF16X3 : PREC_F32;
+  return FR_OK;
+}
+
 int fr_profile_enable(fr_handle* h, int enable) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -971,7 +981,7 @@ const char* fr_version(void) { return "frhip 0.1 gfx950 fp32-mfma"; }
 int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout, int kh, int kw,
                int stride, int pad, const float* pre_scale, const float* pre_shift, const float* post_scale,
                const float* post_shift, const float* prelu, const float* res, int res_h, int res_w, int epi,
-               int nsplit, int tile, int stream_k, void* stream) {
+               int nsplit, int tile, int stream_k, int precision, void* stream) {
   static int t_cus = 0, t_cap = 0;
   static float* t_ws = nullptr;
   static long long t_wsf = 0;
@@ -1017,7 +1027,8 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
     p.sk_cnt = t_cnt;
     p.sk_cnt_cap = t_cap;
   }
-  hipError_t e = launch_conv(p, (ConvTile)tile, pre_scale != nullptr, (Epi)epi, nsplit, (hipStream_t)stream);
+  hipError_t e = launch_conv(p, (ConvTile)tile, pre_scale != nullptr, (Epi)epi, nsplit, (hipStream_t)stream,
+                             precision == 1 ? PREC_BF16X3 : PREC_F32);
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d: ") + hipGetErrorString(e));
   return FR_OK;
 }

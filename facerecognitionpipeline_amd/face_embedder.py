@@ -49,7 +49,7 @@ def _as_device(device) -> torch.device:
 class FaceEmbedder:
     def __init__(self, architecture: str = "ir_101", model_path: Optional[str] = None,
                  model_type: str = "adaface", device=None, max_batch: int = 256,
-                 state_dict=None, weight_seed: Optional[int] = None):
+                 state_dict=None, weight_seed: Optional[int] = None, precision: str = "fp32"):
         self.device = _as_device(device)
         self.model_type = model_type
         self.architecture = architecture
@@ -70,6 +70,8 @@ class FaceEmbedder:
             block_specs(architecture)
             self.model = _lib.Handle(architecture, model_type, self.device, max_batch)
             self.model.load_state_dict(state_dict)
+            self.precision = precision
+            self.model.set_precision(precision)
             self.input_size = INPUT_SIZE
             self.mean = 0.5
             self.std = 0.5

@@ -106,6 +106,14 @@ int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, co
  * scores: host double [n].  Synchronises. */
 int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* scores);
 
+/* Conv arithmetic of this handle.  FR_PRECISION_F32 (default): exact f32 products and f32
+ * accumulation on fp32 MFMA -- the parity path.  FR_PRECISION_BF16X3 (opt-in fast mode):
+ * each f32 operand split into bf16 hi + lo, x.y ~= hi.hi + hi.lo + lo.hi on bf16 MFMA with f32
+ * accumulation (per-product relative error ~2^-16; measured score drift in DESIGN.md). */
+#define FR_PRECISION_F32 0
+#define FR_PRECISION_BF16X3 1
+int fr_set_precision(fr_handle* h, int mode);
+
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).
  * enable=1 starts recording; fr_profile_read synchronises and returns, since the
  * last read: summed milliseconds and algorithmic FLOPs of the conv_mfma launches,

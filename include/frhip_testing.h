@@ -21,11 +21,12 @@ extern "C" {
  * pre_scale/pre_shift may be NULL (no pre-affine).  nsplit > 1 only with epi 4:
  * y then holds nsplit partial slabs of B*Ho*Wo*cout floats.
  * tile: 0 = 256x64, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 256x128, 5 = 128x256.
- * stream_k: 1 = persistent stream-K schedule (nsplit must be 1), 0 = one block per tile. */
+ * stream_k: 1 = persistent stream-K schedule (nsplit must be 1), 0 = one block per tile.
+ * precision: 0 = f32 MFMA, 1 = bf16x3 split (tiles 1, 3, 4, 6, 7, 8 only). */
 int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout, int kh, int kw,
                int stride, int pad, const float* pre_scale, const float* pre_shift, const float* post_scale,
                const float* post_shift, const float* prelu, const float* res, int res_h, int res_w, int epi,
-               int nsplit, int tile, int stream_k, void* stream);
+               int nsplit, int tile, int stream_k, int precision, void* stream);
 
 /* Fused preprocess + input_layer on uint8 RGB [B][112][112][3]; w27x64 is the
  * repacked [ky][kx][c_rgb][64] weight; lut the 256-entry normalisation table. */

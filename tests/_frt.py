@@ -13,7 +13,7 @@ def lib():
     L = _lib.load()
     if not getattr(L, "_frt_ready", False):
         L.frt_conv2d.restype = _I
-        L.frt_conv2d.argtypes = [_P, _P, _P] + [_I] * 9 + [_P] * 6 + [_I] * 6 + [_P]
+        L.frt_conv2d.argtypes = [_P, _P, _P] + [_I] * 9 + [_P] * 6 + [_I] * 7 + [_P]
         L.frt_stem.restype = _I
         L.frt_stem.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P, _P]
         L.frt_topk.restype = _I
@@ -27,7 +27,7 @@ def _p(t):
 
 
 def conv2d(x, w, B, H, W, cin, cout, kh, kw, stride, pad, pre=None, post=None, prelu=None, res=None,
-           res_hw=(0, 0), epi=0, nsplit=1, tile=1, stream_k=0):
+           res_hw=(0, 0), epi=0, nsplit=1, tile=1, stream_k=0, precision=0):
     """x: NHWC cuda f32, w: [cout][kh][kw][cin] cuda f32.  Returns y (NHWC) or partial slabs."""
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
@@ -35,7 +35,7 @@ def conv2d(x, w, B, H, W, cin, cout, kh, kw, stride, pad, pre=None, post=None, p
     ps, ph = (pre if pre is not None else (None, None))
     qs, qh = (post if post is not None else (None, None))
     rc = lib().frt_conv2d(_p(x), _p(w), _p(y), B, H, W, cin, cout, kh, kw, stride, pad, _p(ps), _p(ph), _p(qs),
-                          _p(qh), _p(prelu), _p(res), res_hw[0], res_hw[1], epi, nsplit, tile, stream_k,
+                          _p(qh), _p(prelu), _p(res), res_hw[0], res_hw[1], epi, nsplit, tile, stream_k, precision,
                           torch.cuda.current_stream().cuda_stream)
     _lib.check(rc)
     return y if nsplit > 1 else y[0]

@@ -164,3 +164,32 @@ def test_processor_align_embed_match_stays_on_device():
     assert keys == sorted(keys, reverse=True)
     best = fp.process_numpy(frame)
     assert len(best) == 1 and np.array_equal(best[0]["aligned_face"], out[0]["aligned_face"])
+
+
+@pytest.mark.gpu
+def test_recognition_pipeline_frame_to_matches(tmp_path):
+    """frame + detections -> device align -> blur/quality gate -> batched embed+match (serving path)."""
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    from facerecognitionpipeline_amd.pipeline import RecognitionPipeline
+    rng = np.random.default_rng(40)
+    H, W = 1080, 1920
+    frame = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    lms = _faces(rng, 8, H - 200, W - 200, S=112, scale=(1.5, 2.0)) + 100  # inside the frame
+    emb = FaceEmbedder(architecture="ir_50", model_path="synthetic", max_batch=16)
+    t = A.reference_template(112)
+    crops = np.stack([A.warp_affine_linear(frame, A.fit_similarity(lm, t), 112) for lm in lms])
+    gm = GalleryManager(gallery_path=str(tmp_path / "g" / "s.npz"), device=emb.device, verbose=False)
+    for i, e in enumerate(emb.extract_embeddings_batch(list(crops))):
+        gm.add_student(f"S{i}", f"N{i}", e)
+    dets = [{"bbox": np.array([0, 0, 150, 150], np.int32), "landmarks": lm, "det_score": 0.9} for lm in lms]
+    dets[3]["det_score"] = 0.1                                       # fails the det-score gate
+    pipe = RecognitionPipeline(emb, gm, {"max_yaw": 90, "max_pitch": 90, "max_roll": 90, "blur_threshold": 0})
+    res = pipe.recognize(frame, dets, top_k=3)
+    assert [r["is_valid"] for r in res] == [i != 3 for i in range(8)]
+    for i, r in enumerate(res):
+        if i == 3:
+            assert r["matches"] == []
+            continue
+        assert r["matches"][0][0] == f"S{i}" and abs(r["matches"][0][2] - 1.0) < 1e-5 and r["recognized"]
+        assert abs(r["quality_metrics"]["blur_score"] - A.blur_score(crops[i])) <= 1e-9 * r["quality_metrics"]["blur_score"]

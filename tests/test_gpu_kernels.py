@@ -185,3 +185,27 @@ def test_stream_k_schedule_matches_and_is_deterministic(tile):
     grid, a, b, ref = _conv_case_sk(64, 28, 128, 128, 3, 2, 1, epi=2, tile=tile, use_pre=False, seed=110 + tile)
     _close(a, ref)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("tile", [1, 3, 4, 6, 7, 8])
+@pytest.mark.parametrize("sk", [0, 1])
+def test_bf16x3_split_precision(tile, sk):
+    """Opt-in bf16x3 mode: x = hi + lo in bf16, three bf16 MFMAs per product, f32 accumulation.
+    Per-product relative error <= ~2^-16, so the bar is 5e-5 * max|ref| (vs 1e-5 for f32)."""
+    import tests._frt as F_
+    orig = F_.conv2d
+
+    def split(*a, **kw):
+        kw["precision"] = 1
+        kw["stream_k"] = sk
+        return orig(*a, **kw)
+    F_.conv2d = split
+    try:
+        got, ref = _conv_case(2, 14, 128, 256, 3, 1, 1, epi=1, tile=tile, use_pre=True, seed=200 + tile)
+        _close(got, ref, rel=5e-5)
+        got, ref = _conv_case(3, 14, 64, 64, 3, 2, 1, epi=3, tile=tile, use_pre=False, seed=210 + tile)
+        _close(got, ref, rel=5e-5)
+        got, ref = _conv_case(5, 7, 512, 512, 7, 1, 0, epi=4, tile=tile, use_pre=True, seed=220 + tile)
+        _close(got, ref, rel=5e-5)
+    finally:
+        F_.conv2d = orig

@@ -174,3 +174,21 @@ def test_edge_cases(arch_embedder, tmp_path):
     # all-black and all-white crops stay finite
     ext = emb.extract_embeddings_batch([np.zeros((112, 112, 3), np.uint8), np.full((112, 112, 3), 255, np.uint8)])
     assert np.isfinite(ext).all()
+
+
+@pytest.mark.parametrize("arch", ["ir_50", "ir_101"])
+def test_bf16x3_mode_drift_vs_golden(arch, golden_dir):
+    """Opt-in bf16x3 conv arithmetic: same top-5 ids as the reference, scores within 1e-4."""
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    g = _golden(golden_dir, arch)
+    emb = FaceEmbedder(architecture=arch, model_path="synthetic", precision="bf16x3", max_batch=64)
+    base = W.synthetic_crops(8, int(g["gallery_seed"]))
+    probes = W.probe_crops(base, 8)
+    ge = emb.extract_embeddings_batch(list(base))
+    pe = emb.extract_embeddings_batch(list(probes))
+    S = pe @ ge.T
+    S_ref = g["probe_emb"] @ g["gallery_emb"].T
+    assert np.abs(S - S_ref).max() <= SCORE_TOL
+    assert np.array_equal(np.argsort(-S, axis=1)[:, :5], g["search_idx"])
+    with pytest.raises(ValueError):
+        FaceEmbedder(architecture=arch, model_path="synthetic", precision="fp8")

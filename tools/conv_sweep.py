@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--filter", default=None, help="substring of the layer label to run")
     ap.add_argument("--sk", type=int, default=1, help="1 = persistent stream-K schedule, 0 = one block per tile")
+    ap.add_argument("--precision", type=int, default=0, help="0 = f32 MFMA, 1 = bf16x3 split")
     a = ap.parse_args()
     B = a.batch
     dev = torch.device("cuda", 0)
@@ -74,7 +75,7 @@ def main():
         row = {"layer": label, "count": count, "flop": flop, "tiles": {}}
         for t in tiles:
             try:
-                _frt.conv2d(x, w, B, hw, hw, cin, cout, k, k, stride, pad, tile=t, stream_k=a.sk, **kw)
+                _frt.conv2d(x, w, B, hw, hw, cin, cout, k, k, stride, pad, tile=t, stream_k=a.sk, precision=a.precision, **kw)
             except Exception as e:  # noqa: BLE001
                 row["tiles"][TILES[t]] = str(e)
                 continue
@@ -82,7 +83,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
-                _frt.conv2d(x, w, B, hw, hw, cin, cout, k, k, stride, pad, tile=t, stream_k=a.sk, **kw)
+                _frt.conv2d(x, w, B, hw, hw, cin, cout, k, k, stride, pad, tile=t, stream_k=a.sk, precision=a.precision, **kw)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / a.reps
