@@ -42,9 +42,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c3",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c3",
                     help="BASELINE.json config: c2 IR-50 embed-only B=256; c3 IR-101 embed+match B=256 G=1k "
-                         "(default, the headline metric); c5 IR-101 embed+match B=256/GPU G=100k")
+                         "(default, the headline metric); c4 1080p frames -> align + blur/quality gate + "
+                         "embed + match (detector excluded: not rebuilt); c5 IR-101 embed+match B=256/GPU G=100k")
+    ap.add_argument("--faces-per-frame", type=int, default=8, help="c4: faces per 1080p frame")
     ap.add_argument("--arch", default=None)
     ap.add_argument("--batch", type=int, default=256, help="crops per GPU per step")
     ap.add_argument("--gallery", type=int, default=None, help="gallery rows (0 = embed only)")
@@ -87,7 +89,27 @@ def cpu_baseline(arch, sd, gallery_np, crops, budget_s):
                          ", embed only") + f"), {dt:.1f} s on {threads} host threads"}
 
 
-PRESETS = {"c2": ("ir_50", 0), "c3": ("ir_101", 1000), "c5": ("ir_101", 100_000)}
+PRESETS = {"c2": ("ir_50", 0), "c3": ("ir_101", 1000), "c4": ("ir_101", 1000), "c5": ("ir_101", 100_000)}
+
+
+def c4_inputs(n_faces, per_frame, dev, seed=7):
+    """Synthetic 1080p frames (resident in HBM) with per_frame face landmark sets each."""
+    from facerecognitionpipeline_amd.face_recognition import reference_template
+    rng = np.random.default_rng(seed)
+    n_frames = (n_faces + per_frame - 1) // per_frame
+    frames = torch.randint(0, 256, (n_frames, 1080, 1920, 3), dtype=torch.uint8, device=dev)
+    t = reference_template(112).astype(np.float64)
+    lms = []
+    for f in range(n_frames):
+        cur = []
+        for j in range(per_frame):
+            s = rng.uniform(1.2, 2.5)
+            th = rng.uniform(-0.3, 0.3)
+            R = s * np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+            c = np.array([rng.uniform(200, 1720), rng.uniform(200, 880)])
+            cur.append((t - 56) @ R.T + c)
+        lms.append(np.array(cur, dtype=np.float32))
+    return frames, lms
 
 
 def main():
@@ -133,8 +155,23 @@ def main():
     score = torch.empty((args.batch, k), dtype=torch.float32, device=dev)
     e_out = torch.empty((args.batch, 512), dtype=torch.float32, device=dev)
 
+    if args.config == "c4":
+        frames, lms = c4_inputs(args.batch, args.faces_per_frame, dev)
+        crops = torch.empty((args.batch, 112, 112, 3), dtype=torch.uint8, device=dev)
+
     def step():
-        if G > 0:
+        if args.config == "c4":
+            # per frame: device alignment of its faces; then blur + gate on all crops; one embed+match
+            o = 0
+            for f in range(frames.shape[0]):
+                nf = min(args.faces_per_frame, args.batch - o)
+                emb.model.align_faces(frames[f], lms[f][:nf], 112, crops[o:o + nf])
+                o += nf
+            blur = emb.model.blur_scores(crops)
+            if not (blur >= 0).all():
+                raise RuntimeError("bad blur scores")
+            emb.model.embed_match(crops, k, idx, score, e_out)
+        elif G > 0:
             emb.model.embed_match(rgb, k, idx, score, e_out)
         else:
             emb.model.embed(rgb, e_out, True)
@@ -162,7 +199,8 @@ def main():
     tmax = t.item()
 
     # sanity: probes are noisy copies of gallery rows i % G
-    top1_ok = float((idx[:, 0].cpu().numpy() == np.arange(args.batch) % G0).mean()) if G > 0 else None
+    top1_ok = (float((idx[:, 0].cpu().numpy() == np.arange(args.batch) % G0).mean())
+               if G > 0 and args.config != "c4" else None)
 
     if rank == 0:
         faces = world * args.batch * args.steps
@@ -177,8 +215,8 @@ def main():
             import glob
             cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "layers_pmc.json")))
             tj = cands[-1] if cands else None
-        if (tj and os.path.exists(tj) and args.arch == "ir_101" and args.batch == 256 and G == 1000
-                and args.precision == "fp32"):
+        if (tj and os.path.exists(tj) and args.config == "c3" and args.arch == "ir_101" and args.batch == 256
+                and G == 1000 and args.precision == "fp32"):
             with open(tj) as f:
                 pj = json.load(f)
             traffic = pj.get("hbm_bytes_per_conv_launch")
@@ -186,6 +224,8 @@ def main():
             traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
         out = {
             "metric": METRIC if args.config == "c3" else (
+                f"faces/sec align+quality+embed+match from 1080p frames (IR-101, gallery={G}; detector excluded)"
+                if args.config == "c4" else
                 f"faces/sec embed-only ({args.arch.upper().replace('_', '-')}, 112×112)" if G == 0 else
                 f"faces/sec embed+match ({args.arch.upper().replace('_', '-')}, 112×112, gallery={G})"),
             "value": round(faces / tmax, 2),
@@ -198,10 +238,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32" if args.precision == "fp32" else "bf16x3 (f32 operands split hi+lo, f32 accumulate)",
-            "data": "synthetic (seeded uint8 crops; seeded random-init AdaFace weights)",
-            "config": {"workload": (f"{args.config.upper()}: {args.arch.upper().replace('_', '-')} AdaFace embed"
+            "data": ("synthetic (seeded random 1080p uint8 frames + seeded 5-point landmarks; seeded random-init "
+                     "AdaFace weights)" if args.config == "c4" else
+                     "synthetic (seeded uint8 crops; seeded random-init AdaFace weights)"),
+            "config": {"workload": (f"{args.config.upper()}: "
+                                    + (f"1080p frames ({args.faces_per_frame} faces each) -> device align + blur/"
+                                       "quality gate + " if args.config == "c4" else "")
+                                    + f"{args.arch.upper().replace('_', '-')} AdaFace embed"
                                     + (f" + cosine top-{k} match vs {G}-row gallery" if G > 0 else " only")
-                                    + f", batch {args.batch}/GPU, 112x112 uint8 RGB"),
+                                    + f", batch {args.batch}/GPU, 112x112 uint8 RGB"
+                                    + (" (detector excluded: SCRFD not rebuilt)" if args.config == "c4" else "")),
                        "arch": args.arch, "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "gallery": G, "top_k": k, "parallelism": f"dp{world}",
                        "gallery_exchange": "rccl broadcast" if world > 1 else "none"},
