@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32",
                     help="conv arithmetic: exact f32 MFMA (default, parity path) or opt-in split bf16x3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per conv launch (tools/prof_summary.py --json); "
                          "default: the newest profiles/r*/layers_pmc.json")
@@ -83,7 +83,13 @@ def cpu_baseline(arch, sd, gallery_np, crops, budget_s):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(done / dt, 3), "unit": "faces/s", "cores": threads, "kind": "port",
+    cpu = "unknown CPU"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return {"value": round(done / dt, 3), "unit": "faces/s", "cores": threads, "kind": "port", "cpu": cpu,
             "sample": f"{done} crops of the bench workload ({arch}, batch 32"
                       + (f", G={gallery_np.shape[0]} per-probe vstack+sgemv+argsort search" if gallery_np.shape[0] else
                          ", embed only") + f"), {dt:.1f} s on {threads} host threads"}
@@ -263,7 +269,7 @@ def main():
                          "conv_share_of_step": round(prof["conv_ms"] / max(prof["total_ms"], 1e-9), 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
-            sample = W.probe_crops(gal_crops, 256, seed=W.CROP_SEED_PROBE)
+            sample = W.probe_crops(gal_crops, 1024, seed=W.CROP_SEED_PROBE)
             gnp = gallery.cpu().numpy() if G > 0 else np.zeros((0, 512), np.float32)
             out["cpu_baseline"] = cpu_baseline(args.arch, sd, gnp, sample, args.cpu_seconds)
         else:
