@@ -46,6 +46,8 @@ def parse():
                     help="BASELINE.json config: c2 IR-50 embed-only B=256; c3 IR-101 embed+match B=256 G=1k "
                          "(default, the headline metric); c4 1080p frames -> align + blur/quality gate + "
                          "embed + match (detector excluded: not rebuilt); c5 IR-101 embed+match B=256/GPU G=100k")
+    ap.add_argument("--model-type", choices=["adaface", "arcface"], default="adaface",
+                    help="embedding family (arcface = insightface IResNet weights, face_embedder.py:64-88)")
     ap.add_argument("--faces-per-frame", type=int, default=8, help="c4: faces per 1080p frame")
     ap.add_argument("--arch", default=None)
     ap.add_argument("--batch", type=int, default=256, help="crops per GPU per step")
@@ -133,8 +135,8 @@ def main():
     torch.cuda.set_device(dev)
 
     from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
-    sd = W.synthetic_state_dict(args.arch)
-    emb = FaceEmbedder(architecture=args.arch, state_dict=sd, device=dev, max_batch=args.batch,
+    sd = W.synthetic_state_dict(args.arch, model_type=args.model_type)
+    emb = FaceEmbedder(architecture=args.arch, model_type=args.model_type, state_dict=sd, device=dev, max_batch=args.batch,
                        precision=args.precision)
 
     # gallery: rank 0 embeds min(G, 1000) synthetic gallery crops on its GPU and grows them to G
@@ -221,7 +223,7 @@ def main():
             import glob
             cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "layers_pmc.json")))
             tj = cands[-1] if cands else None
-        if (tj and os.path.exists(tj) and args.config == "c3" and args.arch == "ir_101" and args.batch == 256
+        if (tj and os.path.exists(tj) and args.config == "c3" and args.model_type == "adaface" and args.arch == "ir_101" and args.batch == 256
                 and G == 1000 and args.precision == "fp32"):
             with open(tj) as f:
                 pj = json.load(f)
@@ -229,7 +231,7 @@ def main():
             alg_bytes = pj.get("alg_bytes_per_conv_launch")
             traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
         out = {
-            "metric": METRIC if args.config == "c3" else (
+            "metric": METRIC if args.config == "c3" and args.model_type == "adaface" else (
                 f"faces/sec align+quality+embed+match from 1080p frames (IR-101, gallery={G}; detector excluded)"
                 if args.config == "c4" else
                 f"faces/sec embed-only ({args.arch.upper().replace('_', '-')}, 112×112)" if G == 0 else
@@ -250,15 +252,16 @@ def main():
             "config": {"workload": (f"{args.config.upper()}: "
                                     + (f"1080p frames ({args.faces_per_frame} faces each) -> device align + blur/"
                                        "quality gate + " if args.config == "c4" else "")
-                                    + f"{args.arch.upper().replace('_', '-')} AdaFace embed"
+                                    + f"{args.arch.upper().replace('_', '-')} "
+                                    + ("AdaFace" if args.model_type == "adaface" else "ArcFace (IResNet)") + " embed"
                                     + (f" + cosine top-{k} match vs {G}-row gallery" if G > 0 else " only")
                                     + f", batch {args.batch}/GPU, 112x112 uint8 RGB"
                                     + (" (detector excluded: SCRFD not rebuilt)" if args.config == "c4" else "")),
                        "arch": args.arch, "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "gallery": G, "top_k": k, "parallelism": f"dp{world}",
                        "gallery_exchange": "rccl broadcast" if world > 1 else "none"},
-            "flop_per_face": flop_per_face(args.arch, G),
-            "path_tflops": round(faces / tmax * flop_per_face(args.arch, G) / 1e12, 2),
+            "flop_per_face": flop_per_face(args.arch, G, args.model_type),
+            "path_tflops": round(faces / tmax * flop_per_face(args.arch, G, args.model_type) / 1e12, 2),
             "top1_self_match": top1_ok,
             "roofline": {"bound": "mfma", "kernel": "conv_mfma_kernel (all conv/FC launches)",
                          "achieved": round(conv_tflops, 3), "peak": peak, "unit": "TFLOP/s",
@@ -268,7 +271,7 @@ def main():
                          "avg_launch_ms": round(prof["conv_ms"] / max(prof["conv_launches"], 1), 5),
                          "conv_share_of_step": round(prof["conv_ms"] / max(prof["total_ms"], 1e-9), 4)},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.model_type == "adaface":
             sample = W.probe_crops(gal_crops, 1024, seed=W.CROP_SEED_PROBE)
             gnp = gallery.cpu().numpy() if G > 0 else np.zeros((0, 512), np.float32)
             out["cpu_baseline"] = cpu_baseline(args.arch, sd, gnp, sample, args.cpu_seconds)

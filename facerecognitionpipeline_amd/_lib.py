@@ -35,6 +35,10 @@ _SIGNATURES = {
     "fr_embed_host": (_I, [_P, _P, _I, _I, _I, _P, _I]),
     "fr_gallery_set": (_I, [_P, _P, _I, _I, _I, _P]),
     "fr_gallery_size": (_I, [_P, ctypes.POINTER(_I)]),
+    "fr_gallery_write_rows": (_I, [_P, _I, _I, _P, _I, _P]),
+    "fr_gallery_delete_rows": (_I, [_P, _I, _I, _P]),
+    "fr_gallery_read": (_I, [_P, _I, _I, _P, _I, _P]),
+    "fr_build_templates": (_I, [_P, _P, _P, _I, _I, ctypes.c_float, _P, _P, _P]),
     "fr_match_topk": (_I, [_P, _P, _I, _I, _P, _P, _P]),
     "fr_match_topk_host": (_I, [_P, _P, _I, _I, _P, _P]),
     "fr_embed_match": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
@@ -112,6 +116,7 @@ class Handle:
         h = _P()
         idx = device.index if device.index is not None else torch.cuda.current_device()
         self.device = torch.device("cuda", idx)
+        self.gallery_tag = None  # (owner, version) of the rows in HBM; see GalleryManager._sync_device
         check(self._lib.fr_create(architecture.encode(), model_type.encode(), idx, int(max_batch), ctypes.byref(h)))
         self.h = h
 
@@ -141,10 +146,46 @@ class Handle:
                                  stream_of(self.device)), self.h)
 
     # -- gallery -----------------------------------------------------------
-    def gallery_set(self, E: torch.Tensor) -> None:
+    def gallery_set(self, E: torch.Tensor, tag=None) -> None:
         G = E.shape[0] if E.numel() else 0
         D = E.shape[1] if E.dim() == 2 else 512
         check(self._lib.fr_gallery_set(self.h, ptr(E) if G else None, G, D, 1, stream_of(self.device)), self.h)
+        self.gallery_tag = tag
+
+    def gallery_size(self) -> int:
+        g = ctypes.c_int()
+        check(self._lib.fr_gallery_size(self.h, ctypes.byref(g)), self.h)
+        return g.value
+
+    def gallery_write_rows(self, row0: int, E: torch.Tensor) -> None:
+        """Rows [row0, row0 + len(E)) := E (device f32 [n,512]); may extend the gallery."""
+        E = E.to(device=self.device, dtype=torch.float32).contiguous()
+        check(self._lib.fr_gallery_write_rows(self.h, int(row0), E.shape[0], ptr(E), 1, stream_of(self.device)),
+              self.h)
+
+    def gallery_delete_rows(self, row0: int, n: int = 1) -> None:
+        check(self._lib.fr_gallery_delete_rows(self.h, int(row0), int(n), stream_of(self.device)), self.h)
+
+    def gallery_read(self) -> torch.Tensor:
+        G = self.gallery_size()
+        out = torch.empty((G, 512), dtype=torch.float32, device=self.device)
+        check(self._lib.fr_gallery_read(self.h, 0, G, ptr(out) if G else None, 1, stream_of(self.device)), self.h)
+        return out
+
+    def build_templates(self, emb: torch.Tensor, offsets, method: str = "mean", min_similarity: float = 0.70):
+        """Templates of len(offsets)-1 students whose samples are CSR rows of ``emb`` [total,512]
+        -> (templates f32 [S,512], kept int32 [S]) on the device."""
+        import numpy as np
+        methods = {"mean": 0, "median": 1, "weighted_mean": 2}
+        m = methods.get(method, 0)  # the reference falls back to mean for unknown methods
+        off = np.ascontiguousarray(offsets, dtype=np.int32)
+        S = off.shape[0] - 1
+        emb = emb.to(device=self.device, dtype=torch.float32).contiguous()
+        tpl = torch.empty((max(S, 0), 512), dtype=torch.float32, device=self.device)
+        kept = torch.empty((max(S, 0),), dtype=torch.int32, device=self.device)
+        check(self._lib.fr_build_templates(self.h, ptr(emb), off.ctypes.data, S, m, float(min_similarity), ptr(tpl),
+                                           ptr(kept), stream_of(self.device)), self.h)
+        return tpl, kept
 
     def match(self, Q: torch.Tensor, k: int, idx: torch.Tensor, score: torch.Tensor) -> None:
         check(self._lib.fr_match_topk(self.h, ptr(Q), Q.shape[0], int(k), ptr(idx), ptr(score),

@@ -67,15 +67,53 @@ def state_dict_schema(architecture: str) -> "OrderedDict[str, tuple]":
     return OrderedDict(s)
 
 
-def conv_macs_per_face(architecture: str, match_gallery: int = 0) -> Dict[str, int]:
-    """Multiply-accumulates per 112x112 face (forward-hook count of SURVEY.md §2)."""
+def arcface_state_dict_schema(architecture: str) -> "OrderedDict[str, tuple]":
+    """Every insightface ``arcface_torch`` IResNet key -> shape (ArcFace branch,
+    ``face_embedder.py:64-88``; the ONNX exports come from this module).  Same unit
+    counts as AdaFace; every stage's first unit has a conv1x1+BN ``downsample``."""
+    s: List[Tuple[str, tuple]] = [("conv1.weight", (64, 3, 3, 3))]
+    s += _bn("bn1", 64)
+    s += [("prelu.weight", (64,))]
+    specs = block_specs(architecture)
+    stage, unit = 0, 0
+    for i, (cin, d, stride) in enumerate(specs):
+        if stride == 2 and i > 0:
+            stage, unit = stage + 1, 0
+        p = f"layer{stage + 1}.{unit}."
+        s += _bn(p + "bn1", cin)
+        s += [(p + "conv1.weight", (d, cin, 3, 3))]
+        s += _bn(p + "bn2", d)
+        s += [(p + "prelu.weight", (d,))]
+        s += [(p + "conv2.weight", (d, d, 3, 3))]
+        s += _bn(p + "bn3", d)
+        if stride == 2:
+            s += [(p + "downsample.0.weight", (d, cin, 1, 1))]
+            s += _bn(p + "downsample.1", d)
+        unit += 1
+    s += _bn("bn2", 512)
+    s += [("fc.weight", (EMBED_DIM, 512 * 7 * 7)), ("fc.bias", (EMBED_DIM,))]
+    s += _bn("features", EMBED_DIM)
+    return OrderedDict(s)
+
+
+def schema_for(architecture: str, model_type: str = "adaface") -> "OrderedDict[str, tuple]":
+    if model_type == "adaface":
+        return state_dict_schema(architecture)
+    if model_type == "arcface":
+        return arcface_state_dict_schema(architecture)
+    raise ValueError(f"Unknown model_type: {model_type}. Must be 'adaface' or 'arcface'")
+
+
+def conv_macs_per_face(architecture: str, match_gallery: int = 0, model_type: str = "adaface") -> Dict[str, int]:
+    """Multiply-accumulates per 112x112 face (forward-hook count of SURVEY.md §2).
+    ArcFace adds the stage-1 conv1x1 downsample (AdaFace uses MaxPool2d(1,2) there)."""
     macs3 = 64 * 3 * 9 * 112 * 112  # stem
     macs1, hw = 0, 112
     for cin, d, stride in block_specs(architecture):
         macs3 += d * cin * 9 * hw * hw          # conv1 at input resolution
         ho = hw // stride
         macs3 += d * d * 9 * ho * ho            # conv2 carries the stride
-        if cin != d:
+        if cin != d or (model_type == "arcface" and stride == 2):
             macs1 += d * cin * ho * ho
         hw = ho
     fc = 512 * 49 * EMBED_DIM
@@ -84,5 +122,5 @@ def conv_macs_per_face(architecture: str, match_gallery: int = 0) -> Dict[str, i
             "total": macs3 + macs1 + fc + match_gallery * EMBED_DIM}
 
 
-def flop_per_face(architecture: str, match_gallery: int = 0) -> float:
-    return 2.0 * conv_macs_per_face(architecture, match_gallery)["total"]
+def flop_per_face(architecture: str, match_gallery: int = 0, model_type: str = "adaface") -> float:
+    return 2.0 * conv_macs_per_face(architecture, match_gallery, model_type)["total"]

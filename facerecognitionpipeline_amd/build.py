@@ -23,7 +23,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = "gfx950"
 SOURCES = ["conv_f32_w4.hip", "conv_f32_w8.hip", "conv_bf16x3.hip", "conv_mfma.hip", "embed_misc.hip",
-           "align.hip", "frhip_runtime.cpp"]
+           "align.hip", "gallery.hip", "frhip_runtime.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
 LDFLAGS = ["-shared", f"--offload-arch={ARCH}", f"-Wl,-rpath,{ROCM}/lib", "-Wl,--no-undefined"]

@@ -4,8 +4,8 @@
 //                      (x/255-0.5)/0.5 in f64 -> f32) fused with net input_layer
 //                      (Conv3x3 3->64 + BN2d + PReLU).  uint8 in, NHWC f32 out.
 //   head_reduce_kernel split-K sum of the Linear(25088,512) partials + bias ->
-//                      BN1d(affine=False) -> x/||x|| (net forward tail) -> optional
-//                      e/(||e||+1e-8) (face_embedder.py:133-134, 177-180).
+//                      BN1d -> x/||x|| (AdaFace net forward tail; ArcFace has none)
+//                      -> optional e/(||e||+1e-8) (face_embedder.py:133-134, 177-180).
 //   l2norm_rows_kernel q/(||q||+1e-8) (gallery_manager.py:195).
 //   topk_kernel        argsort(S)[::-1][:k] (gallery_manager.py:197) with the
 //                      documented tie policy: score desc, then index asc.
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
                                                           long long split_stride, const float* __restrict__ fc_bias,
                                                           const float* __restrict__ bn_scale,
                                                           const float* __restrict__ bn_shift, float* __restrict__ emb,
-                                                          int normalize) {
+                                                          int normalize, int model_l2) {
   __shared__ float red[4];
   const int row = blockIdx.x;
   const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
@@ -116,9 +116,11 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
   v1 += fc_bias[c1];
   v0 = v0 * bn_scale[c0] + bn_shift[c0];
   v1 = v1 * bn_scale[c1] + bn_shift[c1];
-  const float norm = sqrtf(block_sum_256(v0 * v0 + v1 * v1, red));
-  v0 = v0 / norm;
-  v1 = v1 / norm;
+  if (model_l2) {  // AdaFace forward tail x / ||x|| (ArcFace's model has none)
+    const float norm = sqrtf(block_sum_256(v0 * v0 + v1 * v1, red));
+    v0 = v0 / norm;
+    v1 = v1 / norm;
+  }
   if (normalize) {
     const float n2 = sqrtf(block_sum_256(v0 * v0 + v1 * v1, red)) + 1e-8f;
     v0 = v0 / n2;
@@ -130,10 +132,10 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
 
 hipError_t launch_head_reduce(const float* partial, int nsplit, long long split_stride, const float* fc_bias,
                               const float* bn_scale, const float* bn_shift, float* emb, int n, int normalize,
-                              hipStream_t s) {
+                              int model_l2, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(head_reduce_kernel, dim3(n), dim3(256), 0, s, partial, nsplit, split_stride, fc_bias, bn_scale,
-                     bn_shift, emb, normalize);
+                     bn_shift, emb, normalize, model_l2);
   return hipGetLastError();
 }
 

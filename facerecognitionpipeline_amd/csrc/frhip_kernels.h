@@ -77,7 +77,7 @@ hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float*
 // Sum split-K partials + FC bias -> BN1d(affine=False) -> x/||x|| -> optional e/(||e||+1e-8).
 hipError_t launch_head_reduce(const float* partial, int nsplit, long long split_stride,
                               const float* fc_bias, const float* bn_scale, const float* bn_shift,
-                              float* emb, int n, int normalize, hipStream_t s);
+                              float* emb, int n, int normalize, int model_l2, hipStream_t s);
 
 // q / (||q|| + 1e-8) row-wise over D=512 rows.
 hipError_t launch_l2norm_rows(const float* q, float* out, int n, int d, hipStream_t s);
@@ -92,5 +92,12 @@ hipError_t launch_warp_affine(const uint8_t* frame, int H, int W, const double* 
 
 // Laplacian variance of the gray image of n uint8 RGB crops [n][S][S][3] -> var[n] (double).
 hipError_t launch_blur(const uint8_t* crops, int n, int S, double* var, hipStream_t s);
+
+// Gallery templates (GalleryManager._aggregate_embeddings) for n_students CSR slices of
+// emb [total][512]; offsets: device [n_students + 1]; out: [n_students][512]; kept: [n] or NULL.
+constexpr int TEMPLATE_MAX_SAMPLES = 1024;
+enum TemplateMethod : int { TEMPLATE_MEAN = 0, TEMPLATE_MEDIAN = 1, TEMPLATE_WEIGHTED_MEAN = 2 };
+hipError_t launch_templates(const float* emb, const int* offsets, int n_students, int method, float min_sim,
+                            float* out, int* kept, hipStream_t s);
 
 }  // namespace frhip

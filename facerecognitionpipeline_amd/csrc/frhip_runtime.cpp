@@ -9,6 +9,7 @@
 //   GalleryManager.search                   gallery_manager.py:189-205 (A11)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -90,6 +91,7 @@ struct ProfEvent {
 struct fr_handle {
   std::mutex mu;
   std::string arch, model_type, err;
+  bool arcface = false;  // insightface IResNet keys/semantics (face_embedder.py:64-88)
   int device = 0;
   int max_batch = 256;
   bool finalized = false;
@@ -123,6 +125,10 @@ struct fr_handle {
   size_t scores_cap = 0;
   void* match_io = nullptr;
   size_t match_io_cap = 0;
+  void* gallery_tmp = nullptr;  // tail staging for row deletes
+  size_t gallery_tmp_cap = 0;
+  void* tpl_offsets = nullptr;  // CSR offsets of fr_build_templates
+  size_t tpl_offsets_cap = 0;
 
   // alignment / quality workspace
   void* align_m = nullptr;  // [n][6] inverse affine maps (double)
@@ -160,6 +166,8 @@ struct fr_handle {
     (void)hipFree(qn);
     (void)hipFree(scores);
     (void)hipFree(match_io);
+    (void)hipFree(gallery_tmp);
+    (void)hipFree(tpl_offsets);
     (void)hipFree(sk_ws);
     (void)hipFree(sk_cnt);
     (void)hipFree(align_m);
@@ -231,6 +239,66 @@ std::map<std::string, size_t> schema(const std::vector<BlockSpec>& specs) {
     add_bn(m, p + "res_layer.5", s.depth);
   }
   return m;
+}
+
+// insightface arcface_torch IResNet keys (the network behind the reference's ArcFace ONNX
+// files, face_embedder.py:64-88): every stage's first unit has a conv1x1+BN downsample,
+// BN1d `features` is affine, and the model output is not L2-normalised.
+std::map<std::string, size_t> schema_arcface(const std::vector<BlockSpec>& specs) {
+  std::map<std::string, size_t> m;
+  m["conv1.weight"] = 64 * 3 * 9;
+  add_bn(m, "bn1", 64);
+  m["prelu.weight"] = 64;
+  add_bn(m, "bn2", 512);
+  m["fc.weight"] = (size_t)512 * 512 * 49;
+  m["fc.bias"] = 512;
+  add_bn(m, "features", 512);
+  int stage = 0, unit = 0;
+  for (size_t i = 0; i < specs.size(); ++i) {
+    const auto& s = specs[i];
+    if (s.stride == 2 && i > 0) {
+      ++stage;
+      unit = 0;
+    }
+    const std::string p = "layer" + std::to_string(stage + 1) + "." + std::to_string(unit) + ".";
+    add_bn(m, p + "bn1", s.cin);
+    m[p + "conv1.weight"] = (size_t)s.depth * s.cin * 9;
+    add_bn(m, p + "bn2", s.depth);
+    m[p + "prelu.weight"] = s.depth;
+    m[p + "conv2.weight"] = (size_t)s.depth * s.depth * 9;
+    add_bn(m, p + "bn3", s.depth);
+    if (s.stride == 2) {
+      m[p + "downsample.0.weight"] = (size_t)s.depth * s.cin;
+      add_bn(m, p + "downsample.1", s.depth);
+    }
+    ++unit;
+  }
+  return m;
+}
+
+// State-dict key names of one residual unit / the stem / the head, per model family.
+struct UnitKeys {
+  std::string pre_bn, conv1, mid_bn, prelu, conv2, out_bn, sc_conv, sc_bn;
+};
+
+UnitKeys unit_keys(bool arcface, const std::vector<BlockSpec>& specs, size_t i) {
+  if (!arcface) {
+    const std::string p = "body." + std::to_string(i) + ".";
+    return {p + "res_layer.0", p + "res_layer.1.weight", p + "res_layer.2", p + "res_layer.3.weight",
+            p + "res_layer.4.weight", p + "res_layer.5", p + "shortcut_layer.0.weight", p + "shortcut_layer.1"};
+  }
+  int stage = 0, unit = 0;
+  for (size_t j = 1; j <= i; ++j) {
+    if (specs[j].stride == 2) {
+      ++stage;
+      unit = 0;
+    } else {
+      ++unit;
+    }
+  }
+  const std::string p = "layer" + std::to_string(stage + 1) + "." + std::to_string(unit) + ".";
+  return {p + "bn1", p + "conv1.weight", p + "bn2", p + "prelu.weight", p + "conv2.weight", p + "bn3",
+          p + "downsample.0.weight", p + "downsample.1"};
 }
 
 // Host staging of every folded tensor before one upload into the arena.
@@ -422,7 +490,7 @@ int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int norma
   if (rc) return rc;
   ProfScope ps(h, s, 0.0, false);
   hipError_t e = launch_head_reduce(h->partial, h->head_split, split_stride, h->fc_bias, h->bn1d_scale,
-                                    h->bn1d_shift, out, n, normalize, s);
+                                    h->bn1d_shift, out, n, normalize, !h->arcface, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("head launch: ") + hipGetErrorString(e));
   return FR_OK;
 }
@@ -591,9 +659,7 @@ int fr_create(const char* architecture, const char* model_type, int device, int 
   if (!ok)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT,
                 "Unknown architecture: " + arch + ". Available: ['ir_50', 'ir_101']");
-  if (mt == "arcface")
-    return fail(nullptr, FR_ERR_UNSUPPORTED, "model_type 'arcface' (ONNX/onnxruntime path) is not implemented");
-  if (mt != "adaface")
+  if (mt != "adaface" && mt != "arcface")
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "Unknown model_type: " + mt + ". Must be 'adaface' or 'arcface'");
   if (max_batch < 1 || max_batch > 512)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "max_batch must be in [1, 512]");
@@ -604,10 +670,11 @@ int fr_create(const char* architecture, const char* model_type, int device, int 
   auto h = std::make_unique<fr_handle>();
   h->arch = arch;
   h->model_type = mt;
+  h->arcface = mt == "arcface";
   h->device = device;
   h->max_batch = max_batch;
   h->specs = specs;
-  h->expected = schema(specs);
+  h->expected = h->arcface ? schema_arcface(specs) : schema(specs);
   *out = h.release();
   return FR_OK;
 }
@@ -659,72 +726,76 @@ int fr_finalize(fr_handle* h) {
     pk.put(dsh, sh);
   };
 
-  // preprocessing LUT: float32((v/255.0 - 0.5)/0.5) in float64 (face_embedder.py:99-101)
+  // preprocessing LUT in float64 then float32: AdaFace (v/255.0 - 0.5)/0.5 (face_embedder.py:99-101),
+  // ArcFace (v - 127.5)/127.5 (face_embedder.py:105-110)
   std::vector<float> lut(256);
-  for (int v = 0; v < 256; ++v) lut[v] = (float)((v / 255.0 - 0.5) / 0.5);
+  for (int v = 0; v < 256; ++v) lut[v] = h->arcface ? (float)((v - 127.5) / 127.5) : (float)((v / 255.0 - 0.5) / 0.5);
   pk.put(&h->lut, lut);
+  const bool af = h->arcface;
   // stem: [64][3][3][3] (BGR channel order) -> [ky][kx][c_rgb][64]
   {
-    const auto& w = P("input_layer.0.weight");
+    const auto& w = P(af ? "conv1.weight" : "input_layer.0.weight");
     std::vector<float> r(27 * 64);
     for (int o = 0; o < 64; ++o)
       for (int c = 0; c < 3; ++c)
         for (int y = 0; y < 3; ++y)
           for (int x = 0; x < 3; ++x) r[((y * 3 + x) * 3 + (2 - c)) * 64 + o] = w[((o * 3 + c) * 3 + y) * 3 + x];
     pk.put(&h->stem_w, r);
-    bn("input_layer.1", &h->stem_scale, &h->stem_shift);
-    pk.put(&h->stem_prelu, P("input_layer.2.weight"));
+    bn(af ? "bn1" : "input_layer.1", &h->stem_scale, &h->stem_shift);
+    pk.put(&h->stem_prelu, P(af ? "prelu.weight" : "input_layer.2.weight"));
   }
   h->blocks.assign(h->specs.size(), BlockW{});
   for (size_t i = 0; i < h->specs.size(); ++i) {
     const auto& s = h->specs[i];
     BlockW& b = h->blocks[i];
     b.spec = s;
-    const std::string p = "body." + std::to_string(i) + ".";
+    const UnitKeys k = unit_keys(af, h->specs, i);
     b.conv1.cin = s.cin;
     b.conv1.cout = s.depth;
     b.conv1.kh = b.conv1.kw = 3;
     b.conv1.stride = 1;
     b.conv1.pad = 1;
-    pk.put(&b.conv1.w, repack_oihw(P(p + "res_layer.1.weight"), s.depth, s.cin, 3, 3));
-    bn(p + "res_layer.0", &b.conv1.pre_scale, &b.conv1.pre_shift);
-    bn(p + "res_layer.2", &b.conv1.post_scale, &b.conv1.post_shift);
-    pk.put(&b.conv1.prelu, P(p + "res_layer.3.weight"));
+    pk.put(&b.conv1.w, repack_oihw(P(k.conv1), s.depth, s.cin, 3, 3));
+    bn(k.pre_bn, &b.conv1.pre_scale, &b.conv1.pre_shift);
+    bn(k.mid_bn, &b.conv1.post_scale, &b.conv1.post_shift);
+    pk.put(&b.conv1.prelu, P(k.prelu));
     b.conv2.cin = s.depth;
     b.conv2.cout = s.depth;
     b.conv2.kh = b.conv2.kw = 3;
     b.conv2.stride = s.stride;
     b.conv2.pad = 1;
-    pk.put(&b.conv2.w, repack_oihw(P(p + "res_layer.4.weight"), s.depth, s.depth, 3, 3));
-    bn(p + "res_layer.5", &b.conv2.post_scale, &b.conv2.post_shift);
-    if (s.cin != s.depth) {
+    pk.put(&b.conv2.w, repack_oihw(P(k.conv2), s.depth, s.depth, 3, 3));
+    bn(k.out_bn, &b.conv2.post_scale, &b.conv2.post_shift);
+    // AdaFace: conv shortcut only where the width changes (MaxPool2d(1,2) in stage 1);
+    // ArcFace: a conv1x1 downsample on every strided unit
+    if (af ? s.stride == 2 : s.cin != s.depth) {
       b.has_sc_conv = true;
       b.sc.cin = s.cin;
       b.sc.cout = s.depth;
       b.sc.kh = b.sc.kw = 1;
       b.sc.stride = s.stride;
       b.sc.pad = 0;
-      pk.put(&b.sc.w, P(p + "shortcut_layer.0.weight"));  // [O][I][1][1] == [O][1][1][I]
-      bn(p + "shortcut_layer.1", &b.sc.post_scale, &b.sc.post_shift);
+      pk.put(&b.sc.w, P(k.sc_conv));  // [O][I][1][1] == [O][1][1][I]
+      bn(k.sc_bn, &b.sc.post_scale, &b.sc.post_shift);
     }
   }
   // head: BN2d(512) as pre-affine; Linear(25088,512) with NCHW-flatten columns
-  // (c*49 + y*7 + x) permuted to NHWC taps ((y*7 + x)*512 + c).
+  // (c*49 + y*7 + x) permuted to NHWC taps ((y*7 + x)*512 + c); BN1d (affine for ArcFace).
   {
     h->head.cin = 512;
     h->head.cout = 512;
     h->head.kh = h->head.kw = 7;
     h->head.stride = 1;
     h->head.pad = 0;
-    const auto& w = P("output_layer.3.weight");
+    const auto& w = P(af ? "fc.weight" : "output_layer.3.weight");
     std::vector<float> r((size_t)512 * 25088);
     for (int o = 0; o < 512; ++o)
       for (int c = 0; c < 512; ++c)
         for (int t = 0; t < 49; ++t) r[(size_t)o * 25088 + (size_t)t * 512 + c] = w[(size_t)o * 25088 + (size_t)c * 49 + t];
     pk.put(&h->head.w, r);
-    bn("output_layer.0", &h->head.pre_scale, &h->head.pre_shift);
-    pk.put(&h->fc_bias, P("output_layer.3.bias"));
-    bn("output_layer.4", &h->bn1d_scale, &h->bn1d_shift, false);
+    bn(af ? "bn2" : "output_layer.0", &h->head.pre_scale, &h->head.pre_shift);
+    pk.put(&h->fc_bias, P(af ? "fc.bias" : "output_layer.3.bias"));
+    bn(af ? "features" : "output_layer.4", &h->bn1d_scale, &h->bn1d_shift, af);
   }
 
   if (h->arena) FR_HIP(h, hipFree(h->arena));
@@ -738,7 +809,8 @@ int fr_finalize(fr_handle* h) {
   const size_t mb = h->max_batch;
   if (!h->act[0]) {
     for (auto& a : h->act) FR_HIP(h, hipMalloc((void**)&a, mb * 112 * 112 * 64 * sizeof(float)));
-    FR_HIP(h, hipMalloc((void**)&h->sc_buf, mb * 28 * 28 * 128 * sizeof(float)));
+    // shortcut output: 28x28x128 per image (AdaFace; stage 1 has no conv shortcut), 56x56x64 (ArcFace)
+    FR_HIP(h, hipMalloc((void**)&h->sc_buf, mb * 56 * 56 * 64 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->partial, (size_t)h->head_split * mb * 512 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->in_stage, mb * 112 * 112 * 3));
     FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
@@ -802,6 +874,102 @@ int fr_gallery_set(fr_handle* h, const float* E, int G, int D, int src_is_device
                            src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
   if (!src_is_device) FR_HIP(h, hipStreamSynchronize(s));
   h->G = G;
+  return FR_OK;
+}
+
+// Grow the gallery allocation to hold `rows` rows, keeping the first G rows (stream-ordered).
+int gallery_reserve(fr_handle* h, int rows, hipStream_t s) {
+  const size_t need = (size_t)rows * 512 * sizeof(float);
+  if (h->gallery_cap >= need) return FR_OK;
+  const size_t want = std::max(need, std::min((size_t)h->gallery_cap * 2, need + ((size_t)256 << 20)));
+  float* p = nullptr;
+  FR_HIP(h, hipMalloc((void**)&p, want));
+  if (h->G > 0) FR_HIP(h, hipMemcpyAsync(p, h->gallery, (size_t)h->G * 512 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  FR_HIP(h, hipStreamSynchronize(s));
+  FR_HIP(h, hipFree(h->gallery));
+  h->gallery = p;
+  h->gallery_cap = want;
+  return FR_OK;
+}
+
+int fr_gallery_write_rows(fr_handle* h, int row0, int n, const float* E, int src_is_device, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < 0 || row0 < 0 || row0 > h->G || (n > 0 && !E))
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "rows must satisfy 0 <= row0 <= G, n >= 0");
+  if (n == 0) return FR_OK;
+  DeviceGuard dg(h->device);
+  hipStream_t s = (hipStream_t)stream;
+  const int G2 = std::max(h->G, row0 + n);
+  int rc = gallery_reserve(h, G2, s);
+  if (rc) return rc;
+  FR_HIP(h, hipMemcpyAsync(h->gallery + (size_t)row0 * 512, E, (size_t)n * 512 * sizeof(float),
+                           src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  if (!src_is_device) FR_HIP(h, hipStreamSynchronize(s));
+  h->G = G2;
+  return FR_OK;
+}
+
+int fr_gallery_delete_rows(fr_handle* h, int row0, int n, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < 0 || row0 < 0 || row0 + n > h->G) return fail(h, FR_ERR_INVALID_ARGUMENT, "rows out of range");
+  if (n == 0) return FR_OK;
+  DeviceGuard dg(h->device);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t tail = (size_t)(h->G - row0 - n) * 512 * sizeof(float);
+  if (tail > 0) {
+    int rc = ensure_buf(h, &h->gallery_tmp, &h->gallery_tmp_cap, tail);
+    if (rc) return rc;
+    float* src = h->gallery + (size_t)(row0 + n) * 512;
+    FR_HIP(h, hipMemcpyAsync(h->gallery_tmp, src, tail, hipMemcpyDeviceToDevice, s));
+    FR_HIP(h, hipMemcpyAsync(h->gallery + (size_t)row0 * 512, h->gallery_tmp, tail, hipMemcpyDeviceToDevice, s));
+  }
+  h->G -= n;
+  return FR_OK;
+}
+
+int fr_gallery_read(fr_handle* h, int row0, int n, float* out, int dst_is_device, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < 0 || row0 < 0 || row0 + n > h->G || (n > 0 && !out))
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "rows out of range");
+  if (n == 0) return FR_OK;
+  DeviceGuard dg(h->device);
+  hipStream_t s = (hipStream_t)stream;
+  FR_HIP(h, hipMemcpyAsync(out, h->gallery + (size_t)row0 * 512, (size_t)n * 512 * sizeof(float),
+                           dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+  if (!dst_is_device) FR_HIP(h, hipStreamSynchronize(s));
+  return FR_OK;
+}
+
+int fr_build_templates(fr_handle* h, const float* emb, const int32_t* offsets, int n_students, int method,
+                       float min_similarity, float* templates, int32_t* kept, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n_students < 0 || (n_students > 0 && (!emb || !offsets || !templates)))
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n_students or NULL buffer");
+  if (method < FR_TEMPLATE_MEAN || method > FR_TEMPLATE_WEIGHTED_MEAN)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "method must be FR_TEMPLATE_MEAN, _MEDIAN or _WEIGHTED_MEAN");
+  if (n_students == 0) return FR_OK;
+  if (offsets[0] != 0) return fail(h, FR_ERR_INVALID_ARGUMENT, "offsets[0] must be 0");
+  for (int i = 0; i < n_students; ++i) {
+    const int n = offsets[i + 1] - offsets[i];
+    if (n < 1 || n > TEMPLATE_MAX_SAMPLES)
+      return fail(h, FR_ERR_INVALID_ARGUMENT,
+                  "every student needs 1.." + std::to_string(TEMPLATE_MAX_SAMPLES) + " samples (student " +
+                      std::to_string(i) + " has " + std::to_string(n) + ")");
+  }
+  DeviceGuard dg(h->device);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t ob = (size_t)(n_students + 1) * sizeof(int32_t);
+  int rc = ensure_buf(h, &h->tpl_offsets, &h->tpl_offsets_cap, ob);
+  if (rc) return rc;
+  FR_HIP(h, hipMemcpyAsync(h->tpl_offsets, offsets, ob, hipMemcpyHostToDevice, s));
+  hipError_t e = launch_templates(emb, (const int*)h->tpl_offsets, n_students, method, min_similarity, templates,
+                                  kept, s);
+  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("template launch: ") + hipGetErrorString(e));
+  FR_HIP(h, hipStreamSynchronize(s));  // the offsets were staged from pageable host memory
   return FR_OK;
 }
 

@@ -94,3 +94,77 @@ def device_embed_match(embedder, k: int) -> Callable[[torch.Tensor], Tuple[torch
         return idx, score
 
     return fn
+
+
+SYNC_NONE, SYNC_DELTA, SYNC_FULL = 0, 1, 2
+
+
+def broadcast_gallery_update(gm, device: torch.device, src: int = 0, group=None):
+    """Ship rank ``src``'s gallery changes to every rank with one small exchange.
+
+    On ``src`` pass the GalleryManager (others pass None).  When every rank holds the
+    previous version, only the row delta travels (ops [n,2] int32 + changed rows [m,512]
+    f32: an enrollment of one student is 2 KB, not the whole G x 512 matrix); otherwise
+    the full matrix is broadcast.  Returns ``(mode, payload)`` where payload is
+    (ops, rows) for SYNC_DELTA, the [G,512] matrix for SYNC_FULL, None for SYNC_NONE;
+    apply it with ``apply_gallery_update``.  Lockstep contract: every rank applies every
+    update it receives, in order.
+    """
+    rank = dist.get_rank(group)
+    hdr = torch.zeros(3, dtype=torch.int64, device=device)
+    ops = rows = E = None
+    if rank == src:
+        if gm._device_version == gm._version and gm._device_current():
+            mode = SYNC_NONE
+        else:
+            delta = gm.pending_delta()
+            if delta is None:
+                mode = SYNC_FULL
+                E_np, _ids = gm.get_gallery_embeddings()
+                E = torch.as_tensor(E_np.reshape(-1, 512), dtype=torch.float32)
+                hdr[:] = torch.tensor([mode, E.shape[0], 0])
+            else:
+                mode = SYNC_DELTA
+                ops, rows, _ids = delta
+                hdr[:] = torch.tensor([mode, ops.shape[0], rows.shape[0]])
+        hdr[0] = mode
+    dist.broadcast(hdr, src=src, group=group)
+    mode, a, b = (int(x) for x in hdr.tolist())
+    if mode == SYNC_NONE:
+        return mode, None
+    if mode == SYNC_FULL:
+        return mode, broadcast_gallery(E, a, device, src=src, group=group)
+    ops_b = (ops.to(device) if rank == src else torch.empty((a, 2), dtype=torch.int32, device=device)).contiguous()
+    rows_b = (rows.to(device) if rank == src else torch.empty((b, 512), dtype=torch.float32, device=device)).contiguous()
+    dist.broadcast(ops_b, src=src, group=group)
+    if b:
+        dist.broadcast(rows_b, src=src, group=group)
+    return mode, (ops_b, rows_b)
+
+
+def apply_gallery_update(mode: int, payload, handle=None, matrix: Optional[torch.Tensor] = None):
+    """Apply what ``broadcast_gallery_update`` returned to a libfrhip handle (GPU ranks) or
+    to a plain [G,512] tensor (returns the new tensor; the CPU/gloo form)."""
+    from .gallery_manager import apply_gallery_delta, apply_gallery_delta_matrix
+    if mode == SYNC_NONE:
+        return matrix
+    if mode == SYNC_FULL:
+        if handle is not None:
+            handle.gallery_set(payload)
+        return payload
+    ops, rows = payload
+    if handle is not None:
+        apply_gallery_delta(handle, ops, rows)
+        return None
+    return apply_gallery_delta_matrix(matrix, ops, rows)
+
+
+def sync_gallery(gm, handle, device: torch.device, src: int = 0, group=None,
+                 matrix: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Every rank: bring ``handle`` (this rank's libfrhip handle; on ``src`` the one the
+    GalleryManager is attached to) or ``matrix`` up to ``src``'s gallery.  ``gm`` on src only."""
+    mode, payload = broadcast_gallery_update(gm, device, src=src, group=group)
+    out = apply_gallery_update(mode, payload, handle=handle, matrix=matrix)
+    if dist.get_rank(group) == src and mode != SYNC_NONE:
+        gm._mark_synced(list(gm.students.keys()))
+    return out

@@ -9,8 +9,10 @@ L2-normalised the way the reference's ``normalize=True`` path leaves it.
 
 Differences (documented in DESIGN.md): inputs must already be 112x112 (the
 reference would ``cv2.resize`` them, face_embedder.py:94-96; cv2 is absent
-here), ``model_type='arcface'`` (onnxruntime) raises NotImplementedError, and
-``device`` must be a HIP device — there is no CPU fallback.
+here), ``model_type='arcface'`` runs the same kernels with the insightface
+IResNet weights of an ``arcface_torch`` state dict (the ONNX files the reference
+loads need onnxruntime, which is absent), and ``device`` must be a HIP device —
+there is no CPU fallback.
 """
 from __future__ import annotations
 
@@ -23,7 +25,7 @@ import torch
 
 from . import _lib
 from .arch import INPUT_SIZE, block_specs
-from .weights import load_checkpoint_state_dict, synthetic_state_dict
+from .weights import load_arcface_state_dict, load_checkpoint_state_dict, synthetic_state_dict
 
 SCRIPT_DIR = Path(__file__).resolve().parent
 
@@ -53,41 +55,44 @@ class FaceEmbedder:
         self.device = _as_device(device)
         self.model_type = model_type
         self.architecture = architecture
-        if model_type == "adaface":
-            if architecture not in ADAFACE_MODELS:
-                raise ValueError(f"Unknown architecture: {architecture}. "
-                                 f"Available: {list(ADAFACE_MODELS.keys())}")
-            if state_dict is None:
-                if model_path == SYNTHETIC or weight_seed is not None:
-                    state_dict = (synthetic_state_dict(architecture) if weight_seed is None
-                                  else synthetic_state_dict(architecture, weight_seed))
-                else:
-                    if model_path is None:
-                        model_path = ADAFACE_MODELS[architecture]
-                    if not os.path.exists(model_path):
-                        raise FileNotFoundError(f"AdaFace checkpoint not found at: {model_path}")
-                    state_dict = load_checkpoint_state_dict(model_path)
-            block_specs(architecture)
-            self.model = _lib.Handle(architecture, model_type, self.device, max_batch)
-            self.model.load_state_dict(state_dict)
-            self.precision = precision
-            self.model.set_precision(precision)
-            self.input_size = INPUT_SIZE
-            self.mean = 0.5
-            self.std = 0.5
-            self.is_onnx = False
-        elif model_type == "arcface":
-            raise NotImplementedError("ArcFace (onnxruntime) path is not part of the MI355X hot path yet; "
-                                      "its parity is unpinned (no onnxruntime, no .onnx files)")
-        else:
+        if model_type not in ("adaface", "arcface"):
             raise ValueError(f"Unknown model_type: {model_type}. Must be 'adaface' or 'arcface'")
+        registry = ADAFACE_MODELS if model_type == "adaface" else ARCFACE_MODELS
+        if architecture not in registry:
+            raise ValueError(f"Unknown architecture: {architecture}. "
+                             f"Available: {list(registry.keys())}")
+        if state_dict is None:
+            if model_path == SYNTHETIC or weight_seed is not None:
+                kw = {} if weight_seed is None else {"seed": weight_seed}
+                state_dict = synthetic_state_dict(architecture, model_type=model_type, **kw)
+            else:
+                if model_path is None:
+                    model_path = registry[architecture]
+                if not os.path.exists(model_path):
+                    raise FileNotFoundError(f"{'AdaFace checkpoint' if model_type == 'adaface' else 'ONNX model'} "
+                                            f"not found at: {model_path}")
+                state_dict = (load_checkpoint_state_dict(model_path) if model_type == "adaface"
+                              else load_arcface_state_dict(model_path))
+        block_specs(architecture)
+        self.model = _lib.Handle(architecture, model_type, self.device, max_batch)
+        self.model.load_state_dict(state_dict)
+        self.precision = precision
+        self.model.set_precision(precision)
+        self.input_size = INPUT_SIZE
+        # face_embedder.py:60-61 (AdaFace) and :86-87 (ArcFace)
+        self.mean, self.std = (0.5, 0.5) if model_type == "adaface" else (127.5, 127.5)
+        self.is_onnx = False
 
     # -- reference API -------------------------------------------------------
-    def preprocess(self, face_image: np.ndarray) -> torch.Tensor:
-        """Host tensor exactly as face_embedder.py:93-104 builds it (for API parity;
-        the GPU path does the same arithmetic inside the stem kernel)."""
+    def preprocess(self, face_image: np.ndarray):
+        """Host input exactly as face_embedder.py:93-110 builds it (for API parity; the
+        GPU path does the same arithmetic inside the stem kernel): a float32 torch tensor
+        for AdaFace, a float32 numpy array for ArcFace."""
         self._check_shape(face_image)
         bgr = face_image[:, :, ::-1]
+        if self.model_type == "arcface":
+            bgr = (bgr - self.mean) / self.std
+            return np.expand_dims(bgr.transpose(2, 0, 1), axis=0).astype(np.float32)
         bgr = (bgr / 255.0 - self.mean) / self.std
         return torch.from_numpy(bgr.transpose(2, 0, 1).copy()).float().unsqueeze(0)
 

@@ -9,6 +9,14 @@ G scores (``:197``); here the template matrix lives in HBM (uploaded once per
 gallery version) and one kernel sequence does renormalise -> fp32 GEMM ->
 top-k.  ``search_batch`` exposes the batched form used by the throughput path.
 
+Gallery lifecycle on the device: every mutation is
+logged, and the next search brings the HBM copy up to date with row writes /
+deletes (``fr_gallery_write_rows`` / ``fr_gallery_delete_rows``) instead of a
+full re-upload; ``pending_delta`` gives the same delta to ship to other GPUs
+(``distributed.sync_gallery``).  ``add_students_batch`` builds many templates at
+once on the GPU (``fr_build_templates``: quality filter + mean / median /
+weighted_mean + L2, ``:104-122``, ``:297-317``).
+
 Persistence uses JSON + ``.npz`` (no pickle); ``load_backup`` reads the
 reference's ``export_for_backup`` JSON (``:246-270``).
 """
@@ -17,6 +25,7 @@ from __future__ import annotations
 import json
 import os
 import shutil
+import uuid
 from dataclasses import dataclass, field
 from datetime import datetime
 from pathlib import Path
@@ -61,6 +70,47 @@ def _slice_len(n: int, top_k: int) -> int:
     return len(range(n)[:top_k])
 
 
+MAX_PENDING_OPS = 256  # beyond this a full upload is cheaper than replaying row ops
+OP_PUT, OP_DELETE = 0, 1
+
+
+def apply_gallery_delta(handle: "_lib.Handle", ops: torch.Tensor, rows: torch.Tensor) -> None:
+    """Replay a compiled delta on a handle's HBM gallery.  ``ops`` int32 [n,2] of
+    (OP_PUT, row) / (OP_DELETE, row); PUTs consume ``rows`` [m,512] in order.  Runs of
+    PUTs to consecutive rows become one write."""
+    ops = ops.cpu().tolist()
+    rows = rows.to(handle.device, torch.float32)
+    i, r = 0, 0
+    while i < len(ops):
+        kind, row = ops[i]
+        if kind == OP_DELETE:
+            handle.gallery_delete_rows(row, 1)
+            i += 1
+            continue
+        j = i + 1
+        while j < len(ops) and ops[j][0] == OP_PUT and ops[j][1] == row + (j - i):
+            j += 1
+        handle.gallery_write_rows(row, rows[r:r + (j - i)])
+        r += j - i
+        i = j
+
+
+def apply_gallery_delta_matrix(E: torch.Tensor, ops: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    """Same delta on a plain [G,512] tensor (the semantics of apply_gallery_delta)."""
+    E = E.clone()
+    r = 0
+    for kind, row in ops.cpu().tolist():
+        if kind == OP_DELETE:
+            E = torch.cat([E[:row], E[row + 1:]])
+        elif row == E.shape[0]:
+            E = torch.cat([E, rows[r:r + 1].to(E)])
+            r += 1
+        else:
+            E[row] = rows[r].to(E)
+            r += 1
+    return E
+
+
 class GalleryManager:
     def __init__(self, gallery_path: Optional[str] = None, aggregation_method: str = "mean", device=None,
                  verbose: bool = True):
@@ -74,7 +124,9 @@ class GalleryManager:
         self._handle: Optional[_lib.Handle] = None
         self._version = 0          # bumped by every mutation
         self._device_version = -1  # version the HBM copy holds
-        self._ids: List[str] = []
+        self._ids: List[str] = []  # row order of the HBM copy
+        self._uid = uuid.uuid4().hex
+        self._pending: Optional[List[Tuple[int, str]]] = None  # row ops since the HBM copy; None = full
         os.makedirs(os.path.dirname(gallery_path) or ".", exist_ok=True)
         if os.path.exists(self._arrays_path(gallery_path)):
             self.load()
@@ -92,7 +144,7 @@ class GalleryManager:
         now = datetime.now().isoformat()
         self.students[student_id] = StudentRecord(student_id, name, emb, self._aggregate_embeddings(emb),
                                                   len(emb), now, now, metadata or {})
-        self._touch()
+        self._touch((OP_PUT, student_id))
         self._log(f"{'Updated' if overwrite else 'Added'} student: {name} ({student_id}) with {len(emb)} embeddings")
         return True
 
@@ -114,7 +166,7 @@ class GalleryManager:
         rec.template_embedding = self._aggregate_embeddings(emb)
         rec.num_samples = len(emb)
         rec.last_updated = datetime.now().isoformat()
-        self._touch()
+        self._touch((OP_PUT, student_id))
         return True
 
     def delete_student(self, student_id: str) -> bool:
@@ -122,8 +174,30 @@ class GalleryManager:
             self._log(f"Student {student_id} not found")
             return False
         del self.students[student_id]
-        self._touch()
+        self._touch((OP_DELETE, student_id))
         return True
+
+    def add_students_batch(self, entries: Sequence[Tuple[str, str, np.ndarray]], overwrite: bool = False,
+                           min_similarity: float = 0.70) -> int:
+        """``add_student`` for many students, templates built in one GPU launch
+        (``fr_build_templates``).  ``entries``: (student_id, name, embeddings [n_i,512]).
+        Returns how many were added (existing ids are skipped unless ``overwrite``)."""
+        todo = [(sid, name, np.asarray(e, np.float32).reshape(-1, 512)) for sid, name, e in entries
+                if overwrite or sid not in self.students]
+        if not todo:
+            return 0
+        h = self._get_handle()
+        offsets = np.zeros(len(todo) + 1, np.int64)
+        offsets[1:] = np.cumsum([len(e) for _s, _n, e in todo])
+        allemb = torch.from_numpy(np.ascontiguousarray(np.concatenate([e for _s, _n, e in todo]))).to(self.device)
+        tpl, _kept = h.build_templates(allemb, offsets, self.aggregation_method, min_similarity)
+        tpl = tpl.cpu().numpy()
+        now = datetime.now().isoformat()
+        for i, (sid, name, e) in enumerate(todo):
+            self.students[sid] = StudentRecord(sid, name, e, tpl[i], len(e), now, now, {})
+            self._touch((OP_PUT, sid))
+        self._log(f"Added {len(todo)} students (templates built on {self.device})")
+        return len(todo)
 
     def get_student(self, student_id: str) -> Optional[StudentRecord]:
         return self.students.get(student_id)
@@ -177,16 +251,69 @@ class GalleryManager:
         self._handle = handle
         self._device = handle.device
         self._device_version = -1
+        self._pending = None
 
-    def _sync_device(self) -> "_lib.Handle":
+    def _get_handle(self) -> "_lib.Handle":
         if self._handle is None:
             self._handle = _lib.Handle("ir_50", "adaface", self.device, max_batch=1)
-        if self._device_version != self._version:
-            E, ids = self.get_gallery_embeddings()
-            self._ids = ids
-            self._handle.gallery_set(torch.from_numpy(np.ascontiguousarray(E, dtype=np.float32)).to(self.device))
-            self._device_version = self._version
         return self._handle
+
+    def _device_current(self) -> bool:
+        """The handle holds exactly this manager's rows at ``_device_version``."""
+        return self._handle is not None and self._handle.gallery_tag == (self._uid, self._device_version)
+
+    def pending_delta(self) -> Optional[Tuple[torch.Tensor, torch.Tensor, List[str]]]:
+        """Row ops that turn the HBM copy (version ``_device_version``) into the current
+        gallery: (ops int32 [n,2], rows f32 [m,512], new row order), or None when only a
+        full upload will do (no copy yet, bulk load, too many ops)."""
+        if self._pending is None or not self._device_current():
+            return None
+        ids = list(self._ids)
+        pos = {s: i for i, s in enumerate(ids)}
+        ops, rows = [], []
+        for kind, sid in self._pending:
+            if kind == OP_DELETE:
+                row = pos.get(sid)
+                if row is None:
+                    return None
+                ops.append((OP_DELETE, row))
+                ids.pop(row)
+                pos = {s: i for i, s in enumerate(ids)}
+            else:
+                row = pos.get(sid)
+                if row is None:
+                    row = len(ids)
+                    ids.append(sid)
+                    pos[sid] = row
+                rec = self.students.get(sid)
+                rows.append(np.zeros(512, np.float32) if rec is None
+                            else np.asarray(rec.template_embedding, np.float32).reshape(512))
+                ops.append((OP_PUT, row))
+        if ids != list(self.students.keys()):
+            return None
+        ops_t = torch.tensor(ops, dtype=torch.int32).reshape(-1, 2)
+        rows_t = torch.from_numpy(np.stack(rows)) if rows else torch.zeros((0, 512), dtype=torch.float32)
+        return ops_t, rows_t, ids
+
+    def _mark_synced(self, ids: List[str]) -> None:
+        self._ids = ids
+        self._device_version = self._version
+        self._pending = []
+        self._handle.gallery_tag = (self._uid, self._version)
+
+    def _sync_device(self) -> "_lib.Handle":
+        h = self._get_handle()
+        if self._device_version == self._version and self._device_current():
+            return h
+        delta = self.pending_delta()
+        if delta is None:
+            E, ids = self.get_gallery_embeddings()
+            h.gallery_set(torch.from_numpy(np.ascontiguousarray(E, dtype=np.float32)).to(self.device))
+        else:
+            ops, rows, ids = delta
+            apply_gallery_delta(h, ops, rows)
+        self._mark_synced(ids)
+        return h
 
     # -- persistence ---------------------------------------------------------
     @staticmethod
@@ -285,8 +412,15 @@ class GalleryManager:
         avg = (embeddings @ embeddings.T).mean(axis=1)
         return embeddings[avg >= np.median(avg) * threshold]
 
-    def _touch(self) -> None:
+    def _touch(self, op: Optional[Tuple[int, str]] = None) -> None:
+        """Bump the version; ``op`` = the row op a device delta replays (None: full upload)."""
         self._version += 1
+        if op is None or self._pending is None:
+            self._pending = None
+        else:
+            self._pending.append(op)
+            if len(self._pending) > MAX_PENDING_OPS:
+                self._pending = None
 
     def _log(self, msg: str) -> None:
         if self.verbose:

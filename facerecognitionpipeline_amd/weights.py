@@ -17,7 +17,7 @@ from typing import Dict
 
 import numpy as np
 
-from .arch import state_dict_schema
+from .arch import schema_for
 
 DEFAULT_WEIGHT_SEED = 20251226
 CROP_SEED_GALLERY = 0xFACE0001
@@ -29,24 +29,26 @@ def _rng(seed: int, key: str) -> np.random.Generator:
     return np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, zlib.crc32(key.encode())])))
 
 
-def synthetic_state_dict(architecture: str, seed: int = DEFAULT_WEIGHT_SEED) -> "OrderedDict[str, np.ndarray]":
-    """AdaFace-keyed state dict (no ``model.`` prefix) of numpy arrays.
+def synthetic_state_dict(architecture: str, seed: int = DEFAULT_WEIGHT_SEED,
+                         model_type: str = "adaface") -> "OrderedDict[str, np.ndarray]":
+    """AdaFace-keyed (or, with model_type='arcface', IResNet-keyed) state dict
+    (no ``model.`` prefix) of numpy arrays.
 
     conv / linear: U(+-1/sqrt(fan_in)); BN: gamma U(0.9,1.1), beta N(0,0.02^2),
     running_mean N(0,0.1^2), running_var U(0.5,1.5); PReLU U(0.2,0.3).
     """
     sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
-    for key, shape in state_dict_schema(architecture).items():
+    for key, shape in schema_for(architecture, model_type).items():
         r = _rng(seed, key)
         leaf = key.rsplit(".", 1)[1]
         if leaf == "num_batches_tracked":
             sd[key] = np.array(0, dtype=np.int64)
             continue
-        if len(shape) >= 2 or key.endswith("output_layer.3.bias"):
+        if len(shape) >= 2 or key in ("output_layer.3.bias", "fc.bias"):
             fan_in = int(np.prod(shape[1:])) if len(shape) >= 2 else 512 * 49
             bound = 1.0 / np.sqrt(fan_in)
             v = r.uniform(-bound, bound, size=shape)
-        elif ".res_layer.3." in key or key.startswith("input_layer.2."):
+        elif ".res_layer.3." in key or key.startswith("input_layer.2.") or key.endswith("prelu.weight"):
             v = r.uniform(0.2, 0.3, size=shape)            # PReLU slope
         elif leaf == "weight":
             v = r.uniform(0.9, 1.1, size=shape)            # BN gamma
@@ -68,6 +70,26 @@ def load_checkpoint_state_dict(model_path: str) -> Dict[str, np.ndarray]:
     ckpt = torch.load(model_path, map_location="cpu", weights_only=True)
     statedict = ckpt["state_dict"]
     return {k[6:]: v.detach().cpu().numpy() for k, v in statedict.items() if k.startswith("model.")}
+
+
+def load_arcface_state_dict(model_path: str) -> Dict[str, np.ndarray]:
+    """IResNet weights for the ArcFace branch from an ``arcface_torch`` ``backbone.pth``
+    (plain state dict, optionally under ``'state_dict'`` and/or ``module.``-prefixed).
+
+    The reference loads ONNX exports of the same network (``face_embedder.py:64-81``); an
+    ONNX graph has BN folded into anonymous initialisers, so its weights cannot be mapped
+    back to this schema without onnx tooling that is absent here."""
+    import torch
+    if model_path.endswith(".onnx"):
+        raise NotImplementedError("ArcFace .onnx models need onnxruntime; pass the arcface_torch backbone.pth "
+                                  "state dict of the same network instead")
+    ckpt = torch.load(model_path, map_location="cpu", weights_only=True)
+    sd = ckpt.get("state_dict", ckpt) if isinstance(ckpt, dict) else ckpt
+    out = {}
+    for k, v in sd.items():
+        k = k[7:] if k.startswith("module.") else k
+        out[k] = v.detach().cpu().numpy()
+    return out
 
 
 def save_checkpoint(state_dict: Dict[str, np.ndarray], path: str) -> None:

@@ -44,13 +44,15 @@ typedef struct fr_handle fr_handle;
 
 /* Build an empty model.  Replaces FaceEmbedder.__init__'s
  * `net.build_model(architecture)` (face_embedder.py:27-49).
- * architecture: "ir_50" | "ir_101" (also "ir_18", "ir_34"); model_type: "adaface"
- * ("arcface" -> FR_ERR_UNSUPPORTED: the ORT path is parity-unpinned).
+ * architecture: "ir_50" | "ir_101" (also "ir_18", "ir_34"); model_type: "adaface" (AdaFace
+ * net.py keys) or "arcface" (the insightface arcface_torch IResNet behind the reference's ONNX
+ * files, face_embedder.py:64-88: (x-127.5)/127.5 input, conv downsample in every stage, affine
+ * BN1d, no L2 inside the model; keys conv1, bn1, prelu, layerS.U.{bn1,conv1,...}, bn2, fc, features).
  * max_batch: images per internal forward chunk (workspace sizing), 1..512. */
 int fr_create(const char* architecture, const char* model_type, int device, int max_batch, fr_handle** out);
 int fr_destroy(fr_handle* h);
 
-/* One AdaFace state-dict tensor, key WITHOUT the "model." prefix, float32
+/* One state-dict tensor (AdaFace: key WITHOUT the "model." prefix), float32
  * host data in PyTorch's layout (conv weights [out][in][kh][kw]).  Replaces
  * `self.model.load_state_dict(model_statedict)` (face_embedder.py:51-53);
  * num_batches_tracked keys are accepted and ignored. */
@@ -74,6 +76,27 @@ int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width
  * src_is_device: 1 if E is a device pointer.  G == 0 clears the gallery. */
 int fr_gallery_set(fr_handle* h, const float* E, int G, int D, int src_is_device, void* stream);
 int fr_gallery_size(fr_handle* h, int* G);
+/* Incremental gallery maintenance, so an enrollment change does not re-upload (or, across
+ * GPUs, re-broadcast) the whole matrix.  Rows are in get_gallery_embeddings order (dict
+ * insertion order, gallery_manager.py:177-187).
+ * write_rows: rows [row0, row0+n) := E (row0 <= G; rows past G extend the gallery) -- add_student
+ *   appends (:71-102), add_student(overwrite=True) / update_embeddings rewrite in place (:124-158).
+ * delete_rows: drop rows [row0, row0+n), later rows move up -- delete_student (:160-169).
+ * read: copy rows out (host or device). */
+int fr_gallery_write_rows(fr_handle* h, int row0, int n, const float* E, int src_is_device, void* stream);
+int fr_gallery_delete_rows(fr_handle* h, int row0, int n, void* stream);
+int fr_gallery_read(fr_handle* h, int row0, int n, float* out, int dst_is_device, void* stream);
+
+/* GalleryManager._aggregate_embeddings (gallery_manager.py:297-317) incl. the quality
+ * filter (:104-122) for n_students at once (bulk enrollment).  emb: device [total][512] f32,
+ * student i = rows [offsets[i], offsets[i+1]) (host offsets, offsets[0] = 0, 1..1024 rows
+ * each); templates: device [n_students][512]; kept: device [n_students] rows surviving the
+ * filter, or NULL.  Synchronises. */
+#define FR_TEMPLATE_MEAN 0
+#define FR_TEMPLATE_MEDIAN 1
+#define FR_TEMPLATE_WEIGHTED_MEAN 2
+int fr_build_templates(fr_handle* h, const float* emb, const int32_t* offsets, int n_students, int method,
+                       float min_similarity, float* templates, int32_t* kept, void* stream);
 
 /* Batched GalleryManager.search (gallery_manager.py:189-205): q/(||q||+1e-8),
  * S = E.q (fp32), top-k by descending score (ties: lower gallery index first).

@@ -34,7 +34,8 @@ def test_capi_reports_errors_without_gpu():
     h = ctypes.c_void_p()
     assert lib.fr_create(b"ir_7", b"adaface", 0, 8, ctypes.byref(h)) == _lib.FR_ERR_INVALID_ARGUMENT
     assert b"Unknown architecture" in lib.fr_last_error(None)
-    assert lib.fr_create(b"ir_50", b"arcface", 0, 8, ctypes.byref(h)) == _lib.FR_ERR_UNSUPPORTED
+    assert lib.fr_create(b"ir_50", b"resnet", 0, 8, ctypes.byref(h)) == _lib.FR_ERR_INVALID_ARGUMENT
+    assert b"Unknown model_type" in lib.fr_last_error(None)
     with pytest.raises(ValueError):
         _lib.check(_lib.FR_ERR_INVALID_ARGUMENT)
 
@@ -108,3 +109,66 @@ def test_reference_backup_json_loads(tmp_path, golden_dir):
 def test_slice_semantics_of_top_k():
     from facerecognitionpipeline_amd.gallery_manager import _slice_len
     assert [_slice_len(3, k) for k in (5, 3, 1, 0, -1, -5)] == [3, 3, 1, 0, 2, 0]
+
+
+def test_torch_library_ops_shapes_without_gpu():
+    """frhip::embed / match_topk / embed_match (SURVEY §8(b)) are registered torch ops whose
+    fake implementations give the output shapes (traceable without running a kernel)."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from facerecognitionpipeline_amd import torch_ops  # noqa: F401  (registers the ops)
+    with FakeTensorMode():
+        x = torch.empty(6, 112, 112, 3, dtype=torch.uint8)
+        e = torch.ops.frhip.embed(x, 1, True)
+        assert e.shape == (6, 512) and e.dtype == torch.float32
+        i, s = torch.ops.frhip.match_topk(e, 1, 5)
+        assert i.shape == (6, 5) and i.dtype == torch.int32 and s.dtype == torch.float32
+        i, s, e2 = torch.ops.frhip.embed_match(x, 1, 3)
+        assert i.shape == (6, 3) and e2.shape == (6, 512)
+    with pytest.raises(ValueError):
+        torch.ops.frhip.embed(torch.zeros(1, 112, 112, 3, dtype=torch.uint8), 10 ** 6, True)
+
+
+def test_gallery_delta_replays_random_mutations(tmp_path):
+    """pending_delta + apply_gallery_delta_matrix reproduce get_gallery_embeddings after any
+    sequence of add / overwrite / update / delete (the incremental HBM sync's contract)."""
+    import torch
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager, apply_gallery_delta_matrix
+
+    class TagOnly:
+        device = torch.device("cpu")
+        gallery_tag = None
+
+    rng = np.random.default_rng(11)
+    gm = GalleryManager(gallery_path=str(tmp_path / "g" / "s.npz"), verbose=False)
+    gm.attach_handle(TagOnly())
+    for i in range(4):
+        gm.add_student(f"S{i}", "n", rng.normal(size=(2, 512)).astype(np.float32))
+    assert gm.pending_delta() is None          # nothing on the device yet: full upload
+    E = torch.from_numpy(gm.get_gallery_embeddings()[0].astype(np.float32))
+    gm._mark_synced(list(gm.students))
+    nxt = 4
+    for _round in range(30):
+        for _ in range(int(rng.integers(1, 6))):
+            op = rng.integers(0, 4)
+            ids = list(gm.students)
+            if op == 0 or not ids:
+                gm.add_student(f"S{nxt}", "n", rng.normal(size=(int(rng.integers(1, 5)), 512)).astype(np.float32))
+                nxt += 1
+            elif op == 1:
+                gm.add_student(ids[rng.integers(len(ids))], "m", rng.normal(size=(3, 512)).astype(np.float32),
+                               overwrite=True)
+            elif op == 2:
+                gm.update_embeddings(ids[rng.integers(len(ids))], rng.normal(size=(1, 512)).astype(np.float32))
+            else:
+                gm.delete_student(ids[rng.integers(len(ids))])
+        d = gm.pending_delta()
+        assert d is not None
+        ops, rows, new_ids = d
+        E = apply_gallery_delta_matrix(E, ops, rows)
+        want = gm.get_gallery_embeddings()[0]
+        assert new_ids == list(gm.students)
+        assert np.array_equal(E.numpy(), np.asarray(want, np.float32).reshape(-1, 512))
+        gm._mark_synced(new_ids)
+    gm._touch()  # a bulk change (load / load_backup) always falls back to a full upload
+    assert gm.pending_delta() is None

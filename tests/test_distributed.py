@@ -76,3 +76,72 @@ def test_gloo_broadcast_shard_gather_matches_single_rank(world, golden_dir):
     f = np.load(golden)
     assert np.array_equal(idx, f["search_idx"])
     assert np.abs(score - f["search_score"]).max() <= 1e-6
+
+
+class _TagOnlyHandle:
+    """Stands in for a libfrhip handle on CPU: only the gallery tag the sync protocol reads."""
+    device = torch.device("cpu")
+    gallery_tag = None
+
+
+def _sync_worker(rank, world, port, tmp, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from facerecognitionpipeline_amd.distributed import sync_gallery
+        from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+        dev = torch.device("cpu")
+        rng = np.random.default_rng(5)
+        gm = None
+        if rank == 0:
+            gm = GalleryManager(gallery_path=os.path.join(tmp, "g", "s.npz"), verbose=False)
+            gm.attach_handle(_TagOnlyHandle())
+            for i in range(5):
+                gm.add_student(f"S{i}", f"N{i}", rng.normal(size=(3, 512)).astype(np.float32))
+        modes, M = [], None
+        M = sync_gallery(gm, None, dev, matrix=M)                    # first: full
+        modes.append(M.shape[0])
+        if rank == 0:
+            gm.add_student("S5", "N5", rng.normal(size=(2, 512)).astype(np.float32))
+            gm.update_embeddings("S1", rng.normal(size=(1, 512)).astype(np.float32))
+            gm.delete_student("S2")
+            gm.add_student("S6", "N6", rng.normal(size=(4, 512)).astype(np.float32))
+            gm.add_student("S0", "N0b", rng.normal(size=(3, 512)).astype(np.float32), overwrite=True)
+            gm.add_student("S7", "N7", rng.normal(size=(1, 512)).astype(np.float32))
+            gm.delete_student("S7")
+            assert gm.pending_delta() is not None
+        M = sync_gallery(gm, None, dev, matrix=M)                    # delta
+        modes.append(M.shape[0])
+        M2 = sync_gallery(gm, None, dev, matrix=M)                   # nothing changed
+        assert M2 is M
+        want = None
+        if rank == 0:
+            want = torch.from_numpy(gm.get_gallery_embeddings()[0].astype(np.float32))
+        q.put((rank, modes, M.numpy(), None if want is None else want.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_gallery_delta_sync(tmp_path):
+    """Enrollment changes on rank 0 reach every rank as a row delta (gallery lifecycle,
+    SURVEY §8(f) rank 3), and every rank ends with rank 0's template matrix."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sync_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict()
+    for _ in range(world):
+        r, modes, M, want = q.get(timeout=120)
+        out[r] = (modes, M, want)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = out[0][2]
+    assert want.shape == (6, 512)
+    for r in range(world):
+        assert out[r][0] == [5, 6]
+        assert np.array_equal(out[r][1], want)

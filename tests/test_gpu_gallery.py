@@ -1,0 +1,144 @@
+"""Device gallery lifecycle against the oracle and the reference's KATs.
+
+* ``fr_build_templates`` vs ``GalleryManager._aggregate_embeddings`` restated
+  (oracle/reference_path.py, gallery_manager.py:104-122, 297-317) and the reference's
+  own templates of its committed backups (tests/golden/backup_*.npz).
+* incremental HBM sync (row writes / deletes) vs a full upload after random
+  enrollment changes.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import reference_path as rp
+
+pytestmark = pytest.mark.gpu
+BACKUPS = ("adaface_ir_101", "adaface_ir_50", "arcface_ir_101", "arcface_ir_50")
+
+
+@pytest.fixture(scope="module")
+def handle():
+    from facerecognitionpipeline_amd import _lib
+    return _lib.Handle("ir_50", "adaface", torch.device("cuda", 0), max_batch=1)
+
+
+@pytest.mark.parametrize("name", BACKUPS)
+def test_build_templates_backup_kat(handle, name, golden_dir):
+    f = np.load(os.path.join(golden_dir, f"backup_{name}.npz"))
+    E = f["embeddings"]                                   # [students, 8, 512] from the reference's JSON
+    S, n = E.shape[:2]
+    tpl, kept = handle.build_templates(torch.from_numpy(E.reshape(-1, 512)).cuda(), np.arange(S + 1) * n, "mean")
+    tpl = tpl.cpu().numpy()
+    want_kept = [len(rp.filter_quality_embeddings(e)) for e in E]
+    assert kept.cpu().numpy().tolist() == want_kept
+    assert np.abs(tpl - f["ref_template"]).max() <= 1e-7        # reference GalleryManager output
+    assert np.abs(tpl - f["stored_template"]).max() <= 1e-7     # the committed templates
+
+
+@pytest.mark.parametrize("method", ["mean", "median", "weighted_mean"])
+def test_build_templates_random_vs_oracle(handle, method):
+    """Ragged students (1..40 samples), clusters loose enough that the 0.70 filter drops
+    rows and sometimes falls back to the top-2 rows."""
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(1, 41, size=64)
+    sizes[:4] = [1, 2, 3, 40]
+    embs = []
+    for i, n in enumerate(sizes):
+        base = rng.normal(size=512)
+        spread = 0.4 + 1.2 * (i % 4) / 3
+        e = base[None] + spread * rng.normal(size=(n, 512))
+        e /= np.linalg.norm(e, axis=1, keepdims=True)
+        embs.append(e.astype(np.float32))
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    tpl, kept = handle.build_templates(torch.from_numpy(np.concatenate(embs)).cuda(), off, method)
+    tpl, kept = tpl.cpu().numpy(), kept.cpu().numpy()
+    fallbacks = 0
+    for i, e in enumerate(embs):
+        filt = rp.filter_quality_embeddings(e) if len(e) > 1 else e
+        assert kept[i] == len(filt)
+        fallbacks += len(e) > 2 and len(filt) == 2
+        want = rp.aggregate_template(e, method)
+        tol = 1e-7 if method == "mean" else 1e-6
+        assert np.abs(tpl[i] - want).max() <= tol, (i, len(e), method)
+    assert fallbacks > 0 and (kept < sizes).any()
+
+
+def test_build_templates_rejects_bad_offsets(handle):
+    e = torch.zeros((4, 512), device="cuda")
+    with pytest.raises(ValueError):
+        handle.build_templates(e, [0, 2, 2, 4])        # empty student
+    with pytest.raises(ValueError):
+        handle.build_templates(e, [1, 4])              # offsets[0] != 0
+    with pytest.raises(ValueError):
+        handle.build_templates(torch.zeros((1025, 512), device="cuda"), [0, 1025])
+
+
+def test_incremental_sync_equals_full_upload(tmp_path):
+    from facerecognitionpipeline_amd import _lib
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    h = _lib.Handle("ir_50", "adaface", torch.device("cuda", 0), max_batch=1)
+    calls = {"full": 0}
+    orig = h.gallery_set
+
+    def counting_set(E, tag=None):
+        calls["full"] += 1
+        return orig(E, tag)
+
+    h.gallery_set = counting_set
+    gm = GalleryManager(gallery_path=str(tmp_path / "a" / "s.npz"), device="cuda:0", verbose=False)
+    gm.attach_handle(h)
+    rng = np.random.default_rng(9)
+
+    def emb(n):
+        e = rng.normal(size=(n, 512)).astype(np.float32)
+        return e / np.linalg.norm(e, axis=1, keepdims=True)
+
+    for i in range(50):
+        gm.add_student(f"S{i}", f"N{i}", emb(3))
+    q = emb(16)
+    gm.search_batch(q, 5)
+    assert calls["full"] == 1
+    nxt = 50
+    for _round in range(20):
+        for _ in range(int(rng.integers(1, 8))):
+            ids = list(gm.students)
+            op = rng.integers(0, 4)
+            if op == 0:
+                gm.add_student(f"S{nxt}", "x", emb(int(rng.integers(1, 6))))
+                nxt += 1
+            elif op == 1:
+                gm.add_student(ids[rng.integers(len(ids))], "y", emb(4), overwrite=True)
+            elif op == 2:
+                gm.update_embeddings(ids[rng.integers(len(ids))], emb(2))
+            else:
+                gm.delete_student(ids[rng.integers(len(ids))])
+        got = gm.search_batch(q, 5)
+        dev = h.gallery_read().cpu().numpy()
+        assert np.array_equal(dev, np.asarray(gm.get_gallery_embeddings()[0], np.float32))
+        fresh = GalleryManager(gallery_path=str(tmp_path / "b" / "s.npz"), device="cuda:0", verbose=False)
+        fresh.students = dict(gm.students)
+        fresh._touch()
+        assert fresh.search_batch(q, 5) == got
+    assert calls["full"] == 1          # every change after the first upload went as row ops
+
+
+def test_add_students_batch_matches_add_student(tmp_path):
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    rng = np.random.default_rng(4)
+    entries = []
+    for i in range(40):
+        base = rng.normal(size=512)
+        e = base[None] + 0.5 * rng.normal(size=(int(rng.integers(1, 12)), 512))
+        entries.append((f"S{i}", f"N{i}", (e / np.linalg.norm(e, axis=1, keepdims=True)).astype(np.float32)))
+    a = GalleryManager(gallery_path=str(tmp_path / "a" / "s.npz"), device="cuda:0", verbose=False)
+    b = GalleryManager(gallery_path=str(tmp_path / "b" / "s.npz"), device="cuda:0", verbose=False)
+    assert a.add_students_batch(entries) == 40
+    assert a.add_students_batch(entries[:3]) == 0              # existing ids skipped
+    for sid, name, e in entries:
+        b.add_student(sid, name, e)
+    Ea, Eb = a.get_gallery_embeddings()[0], b.get_gallery_embeddings()[0]
+    assert np.abs(Ea - Eb).max() <= 1e-7
+    q = np.stack([e[0] for _s, _n, e in entries])
+    assert [[r[0] for r in x] for x in a.search_batch(q, 3)] == [[r[0] for r in x] for x in b.search_batch(q, 3)]

@@ -155,7 +155,7 @@ def test_edge_cases(arch_embedder, tmp_path):
         FaceEmbedder(architecture="ir_7", model_path="synthetic")
     with pytest.raises(ValueError):
         FaceEmbedder(architecture="ir_50", model_type="nope")
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(FileNotFoundError):  # face_embedder.py:72-73: the registry's ONNX file is absent
         FaceEmbedder(architecture="ir_50", model_type="arcface")
     with pytest.raises(RuntimeError):
         sd = W.synthetic_state_dict("ir_50")
@@ -192,3 +192,23 @@ def test_bf16x3_mode_drift_vs_golden(arch, golden_dir):
     assert np.array_equal(np.argsort(-S, axis=1)[:, :5], g["search_idx"])
     with pytest.raises(ValueError):
         FaceEmbedder(architecture=arch, model_path="synthetic", precision="fp8")
+
+
+def test_torch_library_ops_match_python_api(arch_embedder):
+    """torch.ops.frhip.* run the same kernels as FaceEmbedder / GalleryManager."""
+    from facerecognitionpipeline_amd import torch_ops
+    arch, emb = arch_embedder
+    hid = torch_ops.register(emb)
+    try:
+        base = W.synthetic_crops(8)
+        rgb = torch.from_numpy(W.probe_crops(base, 8)).to(emb.device)
+        e = torch.ops.frhip.embed(rgb, hid, True)
+        assert torch.equal(e, emb.embed_tensor(rgb))
+        emb.model.gallery_set(emb.embed_tensor(torch.from_numpy(base).to(emb.device)))
+        idx, score = torch.ops.frhip.match_topk(e, hid, 3)
+        assert (idx[:, 0].cpu().numpy() == np.arange(8)).all()
+        i2, s2, e2 = torch.ops.frhip.embed_match(rgb, hid, 3)
+        assert torch.equal(i2, idx) and torch.equal(s2, score) and torch.equal(e2, e)
+    finally:
+        torch_ops.unregister(hid)
+        emb.model.gallery_set(torch.empty((0, 512), device=emb.device))
