@@ -31,6 +31,7 @@ sys.path.insert(0, REPO)
 
 from facerecognitionpipeline_amd import weights as W  # noqa: E402
 from facerecognitionpipeline_amd.arch import flop_per_face  # noqa: E402
+from facerecognitionpipeline_amd.detector_arch import detector_macs  # noqa: E402
 
 METRIC = "faces/sec embed+match (IR-101, 112×112, gallery=1k) at 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3
@@ -44,8 +45,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c3",
                     help="BASELINE.json config: c2 IR-50 embed-only B=256; c3 IR-101 embed+match B=256 G=1k "
-                         "(default, the headline metric); c4 1080p frames -> align + blur/quality gate + "
-                         "embed + match (detector excluded: not rebuilt); c5 IR-101 embed+match B=256/GPU G=100k")
+                         "(default, the headline metric); c4 1080p frames -> SCRFD-10G detect -> align + "
+                         "blur/quality gate + embed + match; c5 IR-101 embed+match B=256/GPU G=100k")
     ap.add_argument("--model-type", choices=["adaface", "arcface"], default="adaface",
                     help="embedding family (arcface = insightface IResNet weights, face_embedder.py:64-88)")
     ap.add_argument("--faces-per-frame", type=int, default=8, help="c4: faces per 1080p frame")
@@ -163,17 +164,28 @@ def main():
     score = torch.empty((args.batch, k), dtype=torch.float32, device=dev)
     e_out = torch.empty((args.batch, 512), dtype=torch.float32, device=dev)
 
+    det_stats = {"detected": 0, "padded": 0}
     if args.config == "c4":
+        from facerecognitionpipeline_amd.face_recognition import FaceDetector
         frames, lms = c4_inputs(args.batch, args.faces_per_frame, dev)
         crops = torch.empty((args.batch, 112, 112, 3), dtype=torch.uint8, device=dev)
+        detector = FaceDetector(device=dev, max_frames=min(32, frames.shape[0]), max_faces=64)
 
     def step():
         if args.config == "c4":
-            # per frame: device alignment of its faces; then blur + gate on all crops; one embed+match
+            # SCRFD on every frame (batched); each frame's top faces_per_frame detections are aligned
+            # (a frame with fewer is topped up with the synthetic placements so every step embeds
+            # exactly `batch` faces); blur + gate on all crops; one embed+match
+            dets, counts = detector.model.detect(frames, detector.det_thresh, detector.max_faces)
             o = 0
             for f in range(frames.shape[0]):
                 nf = min(args.faces_per_frame, args.batch - o)
-                emb.model.align_faces(frames[f], lms[f][:nf], 112, crops[o:o + nf])
+                nd = min(int(counts[f]), nf)
+                lm = lms[f][:nf].copy()
+                lm[:nd] = dets[f, :nd, 5:15].reshape(nd, 5, 2)
+                det_stats["detected"] += nd
+                det_stats["padded"] += nf - nd
+                emb.model.align_faces(frames[f], lm, 112, crops[o:o + nf])
                 o += nf
             blur = emb.model.blur_scores(crops)
             if not (blur >= 0).all():
@@ -232,7 +244,7 @@ def main():
             traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
         out = {
             "metric": METRIC if args.config == "c3" and args.model_type == "adaface" else (
-                f"faces/sec align+quality+embed+match from 1080p frames (IR-101, gallery={G}; detector excluded)"
+                f"faces/sec detect+align+quality+embed+match from 1080p frames (IR-101, gallery={G})"
                 if args.config == "c4" else
                 f"faces/sec embed-only ({args.arch.upper().replace('_', '-')}, 112×112)" if G == 0 else
                 f"faces/sec embed+match ({args.arch.upper().replace('_', '-')}, 112×112, gallery={G})"),
@@ -246,20 +258,25 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32" if args.precision == "fp32" else "bf16x3 (f32 operands split hi+lo, f32 accumulate)",
-            "data": ("synthetic (seeded random 1080p uint8 frames + seeded 5-point landmarks; seeded random-init "
-                     "AdaFace weights)" if args.config == "c4" else
+            "data": ("synthetic (seeded random 1080p uint8 frames; seeded random-init SCRFD-10G and AdaFace "
+                     "weights; frames with fewer detections than faces-per-frame are topped up with seeded "
+                     "5-point placements)" if args.config == "c4" else
                      "synthetic (seeded uint8 crops; seeded random-init AdaFace weights)"),
             "config": {"workload": (f"{args.config.upper()}: "
-                                    + (f"1080p frames ({args.faces_per_frame} faces each) -> device align + blur/"
-                                       "quality gate + " if args.config == "c4" else "")
+                                    + (f"1080p frames ({args.faces_per_frame} faces each) -> SCRFD-10G detect "
+                                       "(640x640 letterbox) -> device align + blur/quality gate + "
+                                       if args.config == "c4" else "")
                                     + f"{args.arch.upper().replace('_', '-')} "
                                     + ("AdaFace" if args.model_type == "adaface" else "ArcFace (IResNet)") + " embed"
                                     + (f" + cosine top-{k} match vs {G}-row gallery" if G > 0 else " only")
-                                    + f", batch {args.batch}/GPU, 112x112 uint8 RGB"
-                                    + (" (detector excluded: SCRFD not rebuilt)" if args.config == "c4" else "")),
+                                    + f", batch {args.batch}/GPU, 112x112 uint8 RGB"),
                        "arch": args.arch, "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "gallery": G, "top_k": k, "parallelism": f"dp{world}",
-                       "gallery_exchange": "rccl broadcast" if world > 1 else "none"},
+                       "gallery_exchange": "rccl broadcast" if world > 1 else "none",
+                       **({"frames_per_step": int(frames.shape[0]),
+                           "detector_gflop_per_frame": round(2 * detector_macs() / 1e9, 3),
+                           "aligned_from_detections": det_stats["detected"],
+                           "aligned_from_padding": det_stats["padded"]} if args.config == "c4" else {})},
             "flop_per_face": flop_per_face(args.arch, G, args.model_type),
             "path_tflops": round(faces / tmax * flop_per_face(args.arch, G, args.model_type) / 1e12, 2),
             "top1_self_match": top1_ok,

@@ -45,6 +45,7 @@ _SIGNATURES = {
     "fr_align_faces": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P, _P]),
     "fr_warp_affine": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P]),
     "fr_blur_scores": (_I, [_P, _P, _I, _I, _P]),
+    "fr_detect": (_I, [_P, _P, _I, _I, _I, ctypes.c_float, _I, _P, _P, _P]),
     "fr_set_precision": (_I, [_P, _I]),
     "fr_profile_enable": (_I, [_P, _I]),
     "fr_profile_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -219,6 +220,22 @@ class Handle:
         out = np.empty(n, dtype=np.float64)
         check(self._lib.fr_blur_scores(self.h, ptr(crops), n, crops.shape[1], out.ctypes.data), self.h)
         return out
+
+    # -- detector (arch "scrfd_10g") ---------------------------------------
+    def detect(self, frames: torch.Tensor, det_thresh: float = 0.5, max_faces: int = 256):
+        """frames: uint8 [n,H,W,3] RGB on the device -> (dets f32 [n,max_faces,15], counts int32 [n]);
+        row i < min(counts[f], max_faces) of frame f = x1 y1 x2 y2 score, 5 x (x, y)."""
+        import numpy as np
+        if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
+            raise ValueError("expected uint8 [n,H,W,3] RGB frames")
+        frames = frames.to(self.device).contiguous()
+        n = frames.shape[0]
+        dets = np.zeros((n, max_faces, 15), dtype=np.float32)
+        counts = np.zeros(n, dtype=np.int32)
+        check(self._lib.fr_detect(self.h, ptr(frames), n, frames.shape[1], frames.shape[2], float(det_thresh),
+                                  int(max_faces), dets.ctypes.data, counts.ctypes.data, stream_of(self.device)),
+              self.h)
+        return dets, counts
 
     def set_precision(self, mode: str) -> None:
         modes = {"fp32": 0, "f32": 0, "bf16x3": 1}

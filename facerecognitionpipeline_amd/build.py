@@ -22,8 +22,8 @@ LIB = os.path.join(PKG, "libfrhip.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = "gfx950"
-SOURCES = ["conv_f32_w4.hip", "conv_f32_w8.hip", "conv_bf16x3.hip", "conv_mfma.hip", "embed_misc.hip",
-           "align.hip", "gallery.hip", "frhip_runtime.cpp"]
+SOURCES = ["conv_f32_w4.hip", "conv_f32_w8.hip", "conv_bf16x3.hip", "conv_det.hip", "conv_mfma.hip",
+           "embed_misc.hip", "align.hip", "gallery.hip", "detect.hip", "frhip_runtime.cpp", "detector.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
 LDFLAGS = ["-shared", f"--offload-arch={ARCH}", f"-Wl,-rpath,{ROCM}/lib", "-Wl,--no-undefined"]
@@ -32,6 +32,7 @@ LDFLAGS = ["-shared", f"--offload-arch={ARCH}", f"-Wl,-rpath,{ROCM}/lib", "-Wl,-
 def _digest(path: str) -> str:
     h = hashlib.sha256()
     for p in [path, os.path.join(CSRC, "frhip_kernels.h"), os.path.join(CSRC, "conv_mfma_impl.h"),
+              os.path.join(CSRC, "runtime.h"),
               os.path.join(REPO, "include", "frhip.h"), os.path.join(REPO, "include", "frhip_testing.h")]:
         with open(p, "rb") as f:
             h.update(f.read())

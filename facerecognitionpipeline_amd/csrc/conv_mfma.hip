@@ -7,6 +7,7 @@ namespace frhip {
 hipError_t launch_conv_f32_w4(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s);
 hipError_t launch_conv_f32_w8(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s);
 hipError_t launch_conv_bf16x3(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s);
+hipError_t launch_conv_det(const ConvParams& p, ConvTile tile, Epi epi, int nsplit, hipStream_t s);
 
 hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s,
                        Precision prec) {
@@ -15,6 +16,11 @@ hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, in
       (long long)p.B * p.H * p.W * p.Cin * 4 >= (1ll << 31) ||
       (long long)p.Cout * p.KH * p.KW * p.Cin * 4 >= (1ll << 31) || (p.sk_cus > 0 && nsplit != 1))
     return hipErrorInvalidValue;
+  // detector instances (f32 only, whatever the handle's precision)
+  if (epi == EPI_AFFINE_RES_PRELU || (epi == EPI_AFFINE_PRELU && !pre)) {
+    if (pre) return hipErrorInvalidValue;
+    return launch_conv_det(p, tile, epi, nsplit, s);
+  }
   if (prec == PREC_BF16X3) return launch_conv_bf16x3(p, tile, pre, epi, nsplit, s);
   if (tile >= TILE_128x128_W8) return launch_conv_f32_w8(p, tile, pre, epi, nsplit, s);
   return launch_conv_f32_w4(p, tile, pre, epi, nsplit, s);

@@ -341,7 +341,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
         sc = p.post_scale[n];
         sh = p.post_shift[n];
       }
-      if constexpr (EPI == EPI_AFFINE_PRELU) al = p.prelu[n];
+      if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) al = p.prelu[n];
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
 #pragma unroll
@@ -355,6 +355,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
             v = v * sc + sh;
             if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
             if constexpr (EPI == EPI_AFFINE_RES) v += p.res[(long long)m * p.Cout + n];
+            if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
+              v += p.res[(long long)m * p.Cout + n];
+              v = v > 0.f ? v : v * al;
+            }
             if constexpr (EPI == EPI_AFFINE_RES_SUB) {
               const int bb = m / HoWo;
               const int rem = m - bb * HoWo;
@@ -466,7 +470,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool SPLIT>
+// SET selects the (PRE, EPI) instances a translation unit compiles: 0 = the embedding
+// network's, 1 = the detector's (no pre-BN; ReLU via zero PReLU slopes).
+template <int BM, int BN, int WM, int WN, bool SPLIT, int SET = 0>
 static hipError_t launch_tile(const ConvParams& p0, bool pre, Epi epi, int nsplit, hipStream_t s) {
   constexpr int NTHREADS = 64 * WM * WN;
   ConvParams p = p0;
@@ -482,12 +488,19 @@ static hipError_t launch_tile(const ConvParams& p0, bool pre, Epi epi, int nspli
 #define FR_OCC_CASE(PRE_, EPI_) \
   if (pre == PRE_ && epi == EPI_) \
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_mfma_kernel<BM, BN, WM, WN, PRE_, EPI_, SPLIT>, NTHREADS, 0);
-      FR_OCC_CASE(true, EPI_AFFINE_PRELU)
-      FR_OCC_CASE(false, EPI_AFFINE_RES)
-      FR_OCC_CASE(false, EPI_AFFINE_RES_SUB)
-      FR_OCC_CASE(false, EPI_AFFINE)
-      FR_OCC_CASE(true, EPI_RAW)
-      FR_OCC_CASE(false, EPI_RAW)
+      if constexpr (SET == 0) {
+        FR_OCC_CASE(true, EPI_AFFINE_PRELU)
+        FR_OCC_CASE(false, EPI_AFFINE_RES)
+        FR_OCC_CASE(false, EPI_AFFINE_RES_SUB)
+        FR_OCC_CASE(false, EPI_AFFINE)
+        FR_OCC_CASE(true, EPI_RAW)
+        FR_OCC_CASE(false, EPI_RAW)
+      } else {
+        FR_OCC_CASE(false, EPI_AFFINE)
+        FR_OCC_CASE(false, EPI_AFFINE_PRELU)
+        FR_OCC_CASE(false, EPI_AFFINE_RES)
+        FR_OCC_CASE(false, EPI_AFFINE_RES_PRELU)
+      }
 #undef FR_OCC_CASE
       if (e != hipSuccess || o < 1) o = 1;
     }
@@ -515,12 +528,19 @@ static hipError_t launch_tile(const ConvParams& p0, bool pre, Epi epi, int nspli
     hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, PRE_, EPI_, SPLIT>), grid, block, 0, s, p); \
     return hipGetLastError();                                                                       \
   }
-  FR_CONV_CASE(true, EPI_AFFINE_PRELU)
-  FR_CONV_CASE(false, EPI_AFFINE_RES)
-  FR_CONV_CASE(false, EPI_AFFINE_RES_SUB)
-  FR_CONV_CASE(false, EPI_AFFINE)
-  FR_CONV_CASE(true, EPI_RAW)
-  FR_CONV_CASE(false, EPI_RAW)
+  if constexpr (SET == 0) {
+    FR_CONV_CASE(true, EPI_AFFINE_PRELU)
+    FR_CONV_CASE(false, EPI_AFFINE_RES)
+    FR_CONV_CASE(false, EPI_AFFINE_RES_SUB)
+    FR_CONV_CASE(false, EPI_AFFINE)
+    FR_CONV_CASE(true, EPI_RAW)
+    FR_CONV_CASE(false, EPI_RAW)
+  } else {
+    FR_CONV_CASE(false, EPI_AFFINE)
+    FR_CONV_CASE(false, EPI_AFFINE_PRELU)
+    FR_CONV_CASE(false, EPI_AFFINE_RES)
+    FR_CONV_CASE(false, EPI_AFFINE_RES_PRELU)
+  }
 #undef FR_CONV_CASE
   return hipErrorInvalidValue;
 }

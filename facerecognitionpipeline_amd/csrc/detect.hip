@@ -1,0 +1,304 @@
+// SCRFD face detector glue kernels on gfx950 (FaceDetector.detect, face_recognition.py:31-48;
+// insightface SCRFD.detect / forward / nms restated in oracle/scrfd.py).  The conv
+// pyramid itself runs on the implicit-GEMM MFMA kernel (detector.cpp); these are the
+// HBM-bound pieces around it:
+//
+//   letterbox_kernel   cv2.resize(INTER_LINEAR) of each frame into the top-left of a
+//                      zero det_w x det_h canvas, in OpenCV's fixed point (11-bit
+//                      coefficients from the host; SSE2 vertical rounding for the
+//                      vectorised part of each row, scalar rounding for its tail)
+//   det_stem_kernel    blobFromImage ((x - 127.5) / 128, RGB) fused into conv3x3 s2
+//                      3->C + BN + ReLU (K = 27 is too small for MFMA)
+//   maxpool3_kernel    MaxPool2d(3, 2, 1), NHWC
+//   upsample_add       FPN top-down: big += nearest-2x(small), NHWC
+//   decode_kernel      sigmoid(score) >= thresh -> distance2bbox / distance2kps at the
+//                      anchor centres, / det_scale, appended to a per-frame list
+//   nms_kernel         sort by (score desc, anchor asc), greedy IoU NMS (numpy f32
+//                      arithmetic of SCRFD.nms), one workgroup per frame
+#include "frhip_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace frhip {
+
+__global__ __launch_bounds__(256) void letterbox_kernel(const uint8_t* __restrict__ frames, int H, int W,
+                                                        const int* __restrict__ xtab, const int* __restrict__ ytab,
+                                                        int new_w, int new_h, int simd_end, int dw, int dh,
+                                                        uint8_t* __restrict__ out) {
+  const int f = blockIdx.y;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // element of the canvas
+  const int row = dw * 3;
+  if (e >= (long long)dh * row) return;
+  const int y = (int)(e / row);
+  const int ex = (int)(e - (long long)y * row);
+  const int x = ex / 3, c = ex - x * 3;
+  uint8_t v = 0;
+  if (y < new_h && x < new_w) {
+    const uint8_t* src = frames + (long long)f * H * W * 3;
+    const int xs0 = xtab[4 * x], xs1 = xtab[4 * x + 1], a0 = xtab[4 * x + 2], a1 = xtab[4 * x + 3];
+    const int ys0 = ytab[4 * y], ys1 = ytab[4 * y + 1], b0 = ytab[4 * y + 2], b1 = ytab[4 * y + 3];
+    const uint8_t* r0 = src + (long long)ys0 * W * 3;
+    const uint8_t* r1 = src + (long long)ys1 * W * 3;
+    const int S0 = r0[xs0 * 3 + c] * a0 + r0[xs1 * 3 + c] * a1;
+    const int S1 = r1[xs0 * 3 + c] * a0 + r1[xs1 * 3 + c] * a1;
+    int r;
+    if (ex < simd_end)
+      r = ((((S0 >> 4) * b0) >> 16) + (((S1 >> 4) * b1) >> 16) + 2) >> 2;
+    else
+      r = (int)(((long long)S0 * b0 + (long long)S1 * b1 + (1 << 21)) >> 22);
+    v = (uint8_t)min(max(r, 0), 255);
+  }
+  out[(long long)f * dh * row + e] = v;
+}
+
+// One block per (frame, output row); thread t: channel group t & 3 (8 channels), pixels (t >> 2) + 64 j.
+__global__ __launch_bounds__(256) void det_stem_kernel(const uint8_t* __restrict__ img, int H, int W, int C,
+                                                       const float* __restrict__ w27xC,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, float* __restrict__ y) {
+  extern __shared__ float smem[];
+  float* s_w = smem;              // [27][C]
+  float* s_in = smem + 27 * C;    // [3][W + 2][3]
+  const int Ho = H / 2, Wo = W / 2;
+  const int f = blockIdx.x / Ho;
+  const int oy = blockIdx.x - f * Ho;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 27 * C; i += 256) s_w[i] = w27xC[i];
+  const uint8_t* src = img + (long long)f * H * W * 3;
+  for (int i = tid; i < 3 * (W + 2) * 3; i += 256) {
+    const int r = i / ((W + 2) * 3);
+    const int rem = i - r * (W + 2) * 3;
+    const int xx = rem / 3, c = rem - xx * 3;
+    const int iy = 2 * oy - 1 + r, ix = xx - 1;
+    float v = 0.f;
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      v = ((float)src[((long long)iy * W + ix) * 3 + c] - 127.5f) * 0.0078125f;
+    s_in[i] = v;
+  }
+  __syncthreads();
+  const int cg = (tid & 3) * 8;
+  if (cg >= C) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = scale[cg + k];
+    sh[k] = shift[cg + k];
+  }
+  for (int ox = tid >> 2; ox < Wo; ox += 64) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) {
+          const float v = s_in[(ky * (W + 2) + 2 * ox + kx) * 3 + ci];
+          const float* wr = s_w + ((ky * 3 + kx) * 3 + ci) * C + cg;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] = __builtin_fmaf(v, wr[k], acc[k]);
+        }
+    float* dst = y + (((long long)f * Ho + oy) * Wo + ox) * C + cg;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dst[k] = fmaxf(__builtin_fmaf(acc[k], sc[k], sh[k]), 0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool3_kernel(const float* __restrict__ x, int B, int H, int W, int C,
+                                                       float* __restrict__ y) {
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)B * Ho * Wo * C) return;
+  const int c = (int)(i % C);
+  long long r = i / C;
+  const int ox = (int)(r % Wo);
+  r /= Wo;
+  const int oy = (int)(r % Ho);
+  const int b = (int)(r / Ho);
+  float m = -INFINITY;
+  for (int dy = -1; dy <= 1; ++dy)
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int iy = 2 * oy + dy, ix = 2 * ox + dx;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+        m = fmaxf(m, x[(((long long)b * H + iy) * W + ix) * C + c]);
+    }
+  y[i] = m;
+}
+
+__global__ __launch_bounds__(256) void upsample_add_kernel(float* __restrict__ big, const float* __restrict__ small,
+                                                           int B, int h, int w, int C) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)B * 4 * h * w * C) return;
+  const int c = (int)(i % C);
+  long long r = i / C;
+  const int x = (int)(r % (2 * w));
+  r /= 2 * w;
+  const int yy = (int)(r % (2 * h));
+  const int b = (int)(r / (2 * h));
+  big[i] = big[i] + small[(((long long)b * h + yy / 2) * w + x / 2) * C + c];
+}
+
+// Head outputs per level: [B][H*W][32] f32 = [cls a0, cls a1, bbox a0 (4), bbox a1 (4),
+// kps a0 (10), kps a1 (10), pad 2] logits / distances in stride units.
+__global__ __launch_bounds__(256) void decode_kernel(DetDecodeParams p) {
+  const int f = blockIdx.y;
+  int loc = blockIdx.x * 256 + threadIdx.x;
+  int lv = 0;
+  while (lv < 3 && loc >= p.hw[lv]) {
+    loc -= p.hw[lv];
+    ++lv;
+  }
+  if (lv >= 3) return;
+  const int Wl = p.w[lv];
+  const float stride = (float)p.stride[lv];
+  const float* h = p.head[lv] + ((long long)f * p.hw[lv] + loc) * 32;
+  const int gy = loc / Wl, gx = loc - gy * Wl;
+  const float cx = (float)gx * stride, cy = (float)gy * stride;
+  const float ds = p.det_scale;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const float score = 1.0f / (1.0f + expf(-h[a]));
+    if (!(score >= p.thresh)) continue;
+    const int slot = atomicAdd(p.count + f, 1);
+    if (slot >= p.cap) continue;
+    float* o = p.cand + ((long long)f * p.cap + slot) * 16;
+    o[0] = score;
+    o[1] = __int_as_float(p.anchor_base[lv] + loc * 2 + a);
+    const float* bp = h + 2 + 4 * a;
+    o[2] = (cx - bp[0] * stride) / ds;
+    o[3] = (cy - bp[1] * stride) / ds;
+    o[4] = (cx + bp[2] * stride) / ds;
+    o[5] = (cy + bp[3] * stride) / ds;
+    const float* kp = h + 10 + 10 * a;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      o[6 + 2 * k] = (cx + kp[2 * k] * stride) / ds;
+      o[7 + 2 * k] = (cy + kp[2 * k + 1] * stride) / ds;
+    }
+  }
+}
+
+// One workgroup (1024 threads) per frame.  Key = (~score_bits << 32) | (anchor << 12 | slot):
+// ascending order = score descending, then anchor ascending (scores are positive, so their
+// bits order like the values); the slot (arrival order of decode_kernel) rides along.
+__global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ cand, const int* __restrict__ count,
+                                                   int cap, float iou_thresh, int max_out,
+                                                   float* __restrict__ out, int* __restrict__ out_count) {
+  __shared__ unsigned long long keys[DET_MAX_CANDIDATES];
+  __shared__ unsigned char removed[DET_MAX_CANDIDATES];
+  __shared__ int s_nkeep;
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int n = min(count[f], cap);
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  const float* C = cand + (long long)f * cap * 16;
+  for (int i = tid; i < np2; i += 1024) {
+    if (i < n) {
+      const unsigned sb = __float_as_uint(C[i * 16]);
+      const unsigned anchor = (unsigned)__float_as_int(C[i * 16 + 1]);
+      keys[i] = ((unsigned long long)(~sb) << 32) | (anchor << 12) | (unsigned)i;
+    } else {
+      keys[i] = ~0ull;
+    }
+    removed[i] = 0;
+  }
+  if (tid == 0) s_nkeep = 0;
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < np2; i += 1024) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = keys[i], b = keys[l];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            keys[i] = b;
+            keys[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = 0; i < n; ++i) {
+    if (removed[i]) continue;  // uniform: removed[] is stable between barriers
+    const float* bi = C + (keys[i] & 0xfffu) * 16;
+    const float x1 = bi[2], y1 = bi[3], x2 = bi[4], y2 = bi[5];
+    const float area_i = (x2 - x1 + 1.f) * (y2 - y1 + 1.f);
+    if (tid == 0) {
+      const int k = s_nkeep;
+      if (k < max_out) {
+        float* o = out + ((long long)f * max_out + k) * 15;
+        o[0] = x1;
+        o[1] = y1;
+        o[2] = x2;
+        o[3] = y2;
+        o[4] = bi[0];
+        for (int q = 0; q < 10; ++q) o[5 + q] = bi[6 + q];
+      }
+      s_nkeep = k + 1;
+    }
+    for (int j = i + 1 + tid; j < n; j += 1024) {
+      if (removed[j]) continue;
+      const float* bj = C + (keys[j] & 0xfffu) * 16;
+      const float area_j = (bj[4] - bj[2] + 1.f) * (bj[5] - bj[3] + 1.f);
+      const float xx1 = fmaxf(x1, bj[2]), yy1 = fmaxf(y1, bj[3]);
+      const float xx2 = fminf(x2, bj[4]), yy2 = fminf(y2, bj[5]);
+      const float w = fmaxf(0.f, xx2 - xx1 + 1.f), h = fmaxf(0.f, yy2 - yy1 + 1.f);
+      const float inter = w * h;
+      const float ovr = inter / (area_i + area_j - inter);
+      if (!(ovr <= iou_thresh)) removed[j] = 1;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) out_count[f] = s_nkeep;
+}
+
+hipError_t launch_letterbox(const uint8_t* frames, int n, int H, int W, const int* xtab, const int* ytab, int new_w,
+                            int new_h, int simd_end, int dw, int dh, uint8_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const long long elems = (long long)dh * dw * 3;
+  hipLaunchKernelGGL(letterbox_kernel, dim3((unsigned)((elems + 255) / 256), n), dim3(256), 0, s, frames, H, W, xtab,
+                     ytab, new_w, new_h, simd_end, dw, dh, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_det_stem(const uint8_t* img, int n, int H, int W, int C, const float* w27xC, const float* scale,
+                           const float* shift, float* y, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (C % 8 != 0 || C > 32 || H % 2 || W % 2) return hipErrorInvalidValue;
+  const size_t lds = (27 * C + 3 * (W + 2) * 3) * sizeof(float);
+  hipLaunchKernelGGL(det_stem_kernel, dim3(n * (H / 2)), dim3(256), lds, s, img, H, W, C, w27xC, scale, shift, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_maxpool3(const float* x, int B, int H, int W, int C, float* y, hipStream_t s) {
+  const long long total = (long long)B * ((H - 1) / 2 + 1) * ((W - 1) / 2 + 1) * C;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(maxpool3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, B, H, W, C, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_upsample_add(float* big, const float* small, int B, int h, int w, int C, hipStream_t s) {
+  const long long total = (long long)B * 4 * h * w * C;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, big, small, B, h,
+                     w, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode(const DetDecodeParams& p, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int locs = p.hw[0] + p.hw[1] + p.hw[2];
+  hipLaunchKernelGGL(decode_kernel, dim3((locs + 255) / 256, n), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_nms(const float* cand, const int* count, int n, int cap, float iou_thresh, int max_out, float* out,
+                      int* out_count, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (cap > DET_MAX_CANDIDATES) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(nms_kernel, dim3(n), dim3(1024), 0, s, cand, count, cap, iou_thresh, max_out, out, out_count);
+  return hipGetLastError();
+}
+
+}  // namespace frhip

@@ -12,6 +12,7 @@ enum Epi : int {
   EPI_AFFINE_RES = 2,    // y = acc*scale + shift + res[m]             (conv2 + BN + identity / conv shortcut)
   EPI_AFFINE_RES_SUB = 3,// y = acc*scale + shift + res[b, 2oy, 2ox]   (conv2 + BN + MaxPool2d(1,2) shortcut)
   EPI_RAW = 4,           // y[split] = acc                             (split-K partial / gallery scores)
+  EPI_AFFINE_RES_PRELU = 5,  // y = prelu(acc*scale + shift + res[m])  (detector BasicBlock conv2 + BN + add + ReLU)
 };
 
 // One convolution (or GEMM, as a 1x1 conv over a 1x1 image) in NHWC f32.
@@ -99,5 +100,30 @@ constexpr int TEMPLATE_MAX_SAMPLES = 1024;
 enum TemplateMethod : int { TEMPLATE_MEAN = 0, TEMPLATE_MEDIAN = 1, TEMPLATE_WEIGHTED_MEAN = 2 };
 hipError_t launch_templates(const float* emb, const int* offsets, int n_students, int method, float min_sim,
                             float* out, int* kept, hipStream_t s);
+
+// ---- SCRFD detector glue (detect.hip)
+constexpr int DET_MAX_CANDIDATES = 4096;  // per frame, above det_thresh, before NMS
+
+struct DetDecodeParams {
+  const float* head[3];  // per level [B][hw][32]
+  int hw[3], w[3], stride[3], anchor_base[3];
+  float thresh, det_scale;
+  int cap;
+  int* count;   // [B] candidates found (may exceed cap)
+  float* cand;  // [B][cap][16]: score, anchor (int bits), x1 y1 x2 y2, 5 x (x, y)
+};
+
+// cv2.resize INTER_LINEAR (fixed point) of n frames into the top-left new_w x new_h of
+// zero dw x dh canvases; xtab/ytab: device [new_w|new_h][4] = (src0, src1, w0, w1).
+hipError_t launch_letterbox(const uint8_t* frames, int n, int H, int W, const int* xtab, const int* ytab, int new_w,
+                            int new_h, int simd_end, int dw, int dh, uint8_t* out, hipStream_t s);
+// (x - 127.5)/128 -> conv3x3 s2 p1 3->C (C % 8 == 0, <= 32; weights [27][C]) -> BN -> ReLU, NHWC.
+hipError_t launch_det_stem(const uint8_t* img, int n, int H, int W, int C, const float* w27xC, const float* scale,
+                           const float* shift, float* y, hipStream_t s);
+hipError_t launch_maxpool3(const float* x, int B, int H, int W, int C, float* y, hipStream_t s);
+hipError_t launch_upsample_add(float* big, const float* small, int B, int h, int w, int C, hipStream_t s);
+hipError_t launch_decode(const DetDecodeParams& p, int n, hipStream_t s);
+hipError_t launch_nms(const float* cand, const int* count, int n, int cap, float iou_thresh, int max_out, float* out,
+                      int* out_count, hipStream_t s);
 
 }  // namespace frhip

@@ -22,16 +22,14 @@
 #include "../../include/frhip.h"
 #include "../../include/frhip_testing.h"
 #include "frhip_kernels.h"
+#include "runtime.h"
 
 using namespace frhip;
+using namespace frhip_rt;
 
-namespace {
+namespace frhip_rt {
 
 thread_local std::string g_create_error;
-
-struct BlockSpec {
-  int cin, depth, stride;
-};
 
 std::vector<BlockSpec> block_specs(const std::string& arch, bool* ok) {
   int units[4];
@@ -63,119 +61,9 @@ std::vector<BlockSpec> block_specs(const std::string& arch, bool* ok) {
   return v;
 }
 
-// Device-side folded parameters of one conv.
-struct ConvW {
-  float* w = nullptr;  // [Cout][KH][KW][Cin]
-  float* pre_scale = nullptr;
-  float* pre_shift = nullptr;
-  float* post_scale = nullptr;
-  float* post_shift = nullptr;
-  float* prelu = nullptr;
-  int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
-};
+}  // namespace frhip_rt
 
-struct BlockW {
-  BlockSpec spec;
-  ConvW conv1, conv2, sc;
-  bool has_sc_conv = false;
-};
-
-struct ProfEvent {
-  hipEvent_t a, b;
-  double flop;
-  bool conv;
-};
-
-}  // namespace
-
-struct fr_handle {
-  std::mutex mu;
-  std::string arch, model_type, err;
-  bool arcface = false;  // insightface IResNet keys/semantics (face_embedder.py:64-88)
-  int device = 0;
-  int max_batch = 256;
-  bool finalized = false;
-  std::vector<BlockSpec> specs;
-  std::map<std::string, size_t> expected;  // key -> numel
-  std::map<std::string, std::vector<float>> params;
-
-  // device arena with every folded weight
-  float* arena = nullptr;
-  size_t arena_floats = 0;
-  float *lut = nullptr, *stem_w = nullptr, *stem_scale = nullptr, *stem_shift = nullptr, *stem_prelu = nullptr;
-  std::vector<BlockW> blocks;
-  ConvW head;  // BN2d pre-affine + FC as 7x7 valid conv
-  float *fc_bias = nullptr, *bn1d_scale = nullptr, *bn1d_shift = nullptr;
-
-  // workspace
-  float *act[3] = {nullptr, nullptr, nullptr};
-  float* sc_buf = nullptr;
-  float* partial = nullptr;
-  int head_split = 49;
-  uint8_t* in_stage = nullptr;
-  float* emb_stage = nullptr;
-
-  // gallery + match workspace
-  float* gallery = nullptr;
-  int G = 0;
-  size_t gallery_cap = 0;
-  float* qn = nullptr;
-  size_t qn_cap = 0;
-  float* scores = nullptr;
-  size_t scores_cap = 0;
-  void* match_io = nullptr;
-  size_t match_io_cap = 0;
-  void* gallery_tmp = nullptr;  // tail staging for row deletes
-  size_t gallery_tmp_cap = 0;
-  void* tpl_offsets = nullptr;  // CSR offsets of fr_build_templates
-  size_t tpl_offsets_cap = 0;
-
-  // alignment / quality workspace
-  void* align_m = nullptr;  // [n][6] inverse affine maps (double)
-  size_t align_m_cap = 0;
-  void* blur_out = nullptr;  // [n] double
-  size_t blur_out_cap = 0;
-
-  // stream-K workspace shared by every body conv launch (launches are stream-ordered)
-  int cus = 0;
-  float* sk_ws = nullptr;
-  long long sk_ws_floats = 0;
-  int* sk_cnt = nullptr;
-  int sk_cnt_cap = 0;
-  bool stream_k = true;
-  Precision prec = PREC_F32;
-
-  // profiling
-  bool prof = false;
-  std::vector<ProfEvent> events;
-  std::vector<hipEvent_t> pool;
-
-  ~fr_handle() {
-    for (auto& e : events) {
-      (void)hipEventDestroy(e.a);
-      (void)hipEventDestroy(e.b);
-    }
-    for (auto e : pool) (void)hipEventDestroy(e);
-    (void)hipFree(arena);
-    for (auto p : act) (void)hipFree(p);
-    (void)hipFree(sc_buf);
-    (void)hipFree(partial);
-    (void)hipFree(in_stage);
-    (void)hipFree(emb_stage);
-    (void)hipFree(gallery);
-    (void)hipFree(qn);
-    (void)hipFree(scores);
-    (void)hipFree(match_io);
-    (void)hipFree(gallery_tmp);
-    (void)hipFree(tpl_offsets);
-    (void)hipFree(sk_ws);
-    (void)hipFree(sk_cnt);
-    (void)hipFree(align_m);
-    (void)hipFree(blur_out);
-  }
-};
-
-namespace {
+namespace frhip_rt {
 
 int fail(fr_handle* h, int code, const std::string& msg) {
   if (h)
@@ -185,27 +73,9 @@ int fail(fr_handle* h, int code, const std::string& msg) {
   return code;
 }
 
-#define FR_HIP(h, call)                                                                          \
-  do {                                                                                           \
-    hipError_t e_ = (call);                                                                      \
-    if (e_ != hipSuccess)                                                                        \
-      return fail(h, FR_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));             \
-  } while (0)
 
-// Restores the caller's current device on scope exit.
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
 
-void add_bn(std::map<std::string, size_t>& m, const std::string& p, int c, bool affine = true) {
+void add_bn(std::map<std::string, size_t>& m, const std::string& p, int c, bool affine) {
   if (affine) {
     m[p + ".weight"] = c;
     m[p + ".bias"] = c;
@@ -301,17 +171,6 @@ UnitKeys unit_keys(bool arcface, const std::vector<BlockSpec>& specs, size_t i) 
           p + "downsample.0.weight", p + "downsample.1"};
 }
 
-// Host staging of every folded tensor before one upload into the arena.
-struct Packer {
-  std::vector<float> buf;
-  std::vector<std::pair<float**, size_t>> fix;  // (destination pointer, float offset)
-  void put(float** dst, const std::vector<float>& v) {
-    size_t off = (buf.size() + 3) & ~size_t(3);  // 16-B alignment for float4 loads
-    buf.resize(off);
-    buf.insert(buf.end(), v.begin(), v.end());
-    fix.push_back({dst, off});
-  }
-};
 
 // PyTorch CPU eval BatchNorm computes alpha = gamma/sqrt(var+eps), beta = bias - mean*alpha
 // in the input dtype and applies x*alpha + beta (ATen batch_norm_cpu_collect_linear_and_constant_terms).
@@ -654,15 +513,19 @@ int fr_create(const char* architecture, const char* model_type, int device, int 
   *out = nullptr;
   const std::string arch = architecture ? architecture : "";
   const std::string mt = model_type ? model_type : "";
-  bool ok = false;
-  auto specs = block_specs(arch, &ok);
+  const bool detector = arch == "scrfd_10g";
+  bool ok = detector;
+  auto specs = detector ? std::vector<BlockSpec>{} : block_specs(arch, &ok);
   if (!ok)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT,
-                "Unknown architecture: " + arch + ". Available: ['ir_50', 'ir_101']");
-  if (mt != "adaface" && mt != "arcface")
-    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "Unknown model_type: " + mt + ". Must be 'adaface' or 'arcface'");
+                "Unknown architecture: " + arch + ". Available: ['ir_50', 'ir_101', 'scrfd_10g']");
+  if (detector ? mt != "scrfd" : (mt != "adaface" && mt != "arcface"))
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT,
+                "Unknown model_type: " + mt + (detector ? ". scrfd_10g takes 'scrfd'" : ". Must be 'adaface' or 'arcface'"));
   if (max_batch < 1 || max_batch > 512)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "max_batch must be in [1, 512]");
+  if (detector && max_batch > 64)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "scrfd_10g: max_batch (frames per forward) must be in [1, 64]");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(nullptr, FR_ERR_HIP, "no HIP device available");
@@ -674,7 +537,8 @@ int fr_create(const char* architecture, const char* model_type, int device, int 
   h->device = device;
   h->max_batch = max_batch;
   h->specs = specs;
-  h->expected = h->arcface ? schema_arcface(specs) : schema(specs);
+  h->detector = detector;
+  h->expected = detector ? detector_schema() : h->arcface ? schema_arcface(specs) : schema(specs);
   *out = h.release();
   return FR_OK;
 }
@@ -715,6 +579,12 @@ int fr_finalize(fr_handle* h) {
   }
   if (!missing.empty()) return fail(h, FR_ERR_MISSING_PARAM, "Missing key(s) in state_dict: " + missing);
   DeviceGuard dg(h->device);
+  if (h->detector) {
+    int rc = detector_finalize(h);
+    if (rc) return rc;
+    h->finalized = true;
+    return FR_OK;
+  }
 
   Packer pk;
   std::vector<float> sc, sh;
@@ -825,6 +695,7 @@ int fr_embed(fr_handle* h, const uint8_t* rgb, int n, int height, int width, flo
              void* stream) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
+  if (h->detector) return fail(h, FR_ERR_STATE, "this handle is a detector (scrfd_10g); use fr_detect");
   if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
   if (height != 112 || width != 112)
     return fail(h, FR_ERR_INVALID_ARGUMENT, "input must be 112x112x3 (resize is done by the caller)");
@@ -836,6 +707,7 @@ int fr_embed(fr_handle* h, const uint8_t* rgb, int n, int height, int width, flo
 int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
+  if (h->detector) return fail(h, FR_ERR_STATE, "this handle is a detector (scrfd_10g); use fr_detect");
   if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
   if (height != 112 || width != 112)
     return fail(h, FR_ERR_INVALID_ARGUMENT, "input must be 112x112x3 (resize is done by the caller)");
@@ -1016,6 +888,7 @@ int fr_embed_match(fr_handle* h, const uint8_t* rgb, int n, int k, int32_t* idx,
                    void* stream) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
+  if (h->detector) return fail(h, FR_ERR_STATE, "this handle is a detector (scrfd_10g); use fr_detect");
   if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
   if (n < 0 || (n > 0 && (!rgb || !idx || !score))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
   if (h->G <= 0) return fail(h, FR_ERR_STATE, "gallery is empty (fr_gallery_set first)");
@@ -1097,6 +970,20 @@ int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* 
   FR_HIP(h, hipMemcpyAsync(scores, h->blur_out, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s));
   FR_HIP(h, hipStreamSynchronize(s));
   return FR_OK;
+}
+
+int fr_detect(fr_handle* h, const uint8_t* frames, int n, int height, int width, float det_thresh, int max_faces,
+              float* dets, int32_t* counts, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->detector) return fail(h, FR_ERR_STATE, "not a detector handle (fr_create(\"scrfd_10g\", \"scrfd\", ...))");
+  if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
+  if (n < 0 || (n > 0 && (!frames || !counts || (max_faces > 0 && !dets))) || height < 2 || width < 2 ||
+      max_faces < 0)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "bad frames / sizes / output buffers");
+  if (n == 0) return FR_OK;
+  DeviceGuard dg(h->device);
+  return detector_run(h, frames, n, height, width, det_thresh, max_faces, dets, counts, (hipStream_t)stream);
 }
 
 int fr_set_precision(fr_handle* h, int mode) {
@@ -1212,6 +1099,16 @@ int frt_fit_similarity(const float* src, const float* dst, int n, double* M) {
   if (n < 2 || n > 8) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "n in [2, 8]");
   fit_similarity(src, dst, n, M);
   return FR_OK;
+}
+
+int frt_detector_forward(fr_handle* h, const uint8_t* frames, int n, int height, int width, float* heads,
+                         uint8_t* canvas, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->detector || !h->finalized) return fail(h, FR_ERR_STATE, "not a finalised detector handle");
+  if (n < 1 || !frames || !heads || height < 2 || width < 2) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad arguments");
+  DeviceGuard dg(h->device);
+  return detector_forward(h, frames, n, height, width, heads, canvas, (hipStream_t)stream);
 }
 
 int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, void* stream) {

@@ -1,0 +1,194 @@
+// Internals shared by the libfrhip runtime translation units (frhip_runtime.cpp,
+// detector.cpp): the handle, folded-parameter types and the launch helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/frhip.h"
+#include "frhip_kernels.h"
+
+namespace frhip_rt {
+
+struct BlockSpec {
+  int cin, depth, stride;
+};
+
+// Device-side folded parameters of one conv.
+struct ConvW {
+  float* w = nullptr;  // [Cout][KH][KW][Cin]
+  float* pre_scale = nullptr;
+  float* pre_shift = nullptr;
+  float* post_scale = nullptr;
+  float* post_shift = nullptr;
+  float* prelu = nullptr;
+  int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
+};
+
+struct BlockW {
+  BlockSpec spec;
+  ConvW conv1, conv2, sc;
+  bool has_sc_conv = false;
+};
+
+struct ProfEvent {
+  hipEvent_t a, b;
+  double flop;
+  bool conv;
+};
+
+struct Detector;  // detector.cpp
+void detector_destroy(Detector* d);
+
+}  // namespace frhip_rt
+
+struct fr_handle {
+  std::mutex mu;
+  std::string arch, model_type, err;
+  bool arcface = false;
+  bool detector = false;  // arch "scrfd_10g": a face detector, not an embedding model  // insightface IResNet keys/semantics (face_embedder.py:64-88)
+  int device = 0;
+  int max_batch = 256;
+  bool finalized = false;
+  std::vector<frhip_rt::BlockSpec> specs;
+  std::map<std::string, size_t> expected;  // key -> numel
+  std::map<std::string, std::vector<float>> params;
+
+  // device arena with every folded weight
+  float* arena = nullptr;
+  size_t arena_floats = 0;
+  float *lut = nullptr, *stem_w = nullptr, *stem_scale = nullptr, *stem_shift = nullptr, *stem_prelu = nullptr;
+  std::vector<frhip_rt::BlockW> blocks;
+  frhip_rt::ConvW head;  // BN2d pre-affine + FC as 7x7 valid conv
+  float *fc_bias = nullptr, *bn1d_scale = nullptr, *bn1d_shift = nullptr;
+
+  // workspace
+  float *act[3] = {nullptr, nullptr, nullptr};
+  float* sc_buf = nullptr;
+  float* partial = nullptr;
+  int head_split = 49;
+  uint8_t* in_stage = nullptr;
+  float* emb_stage = nullptr;
+
+  // gallery + match workspace
+  float* gallery = nullptr;
+  int G = 0;
+  size_t gallery_cap = 0;
+  float* qn = nullptr;
+  size_t qn_cap = 0;
+  float* scores = nullptr;
+  size_t scores_cap = 0;
+  void* match_io = nullptr;
+  size_t match_io_cap = 0;
+  void* gallery_tmp = nullptr;  // tail staging for row deletes
+  size_t gallery_tmp_cap = 0;
+  void* tpl_offsets = nullptr;  // CSR offsets of fr_build_templates
+  size_t tpl_offsets_cap = 0;
+
+  // alignment / quality workspace
+  void* align_m = nullptr;  // [n][6] inverse affine maps (double)
+  size_t align_m_cap = 0;
+  void* blur_out = nullptr;  // [n] double
+  size_t blur_out_cap = 0;
+
+  // stream-K workspace shared by every body conv launch (launches are stream-ordered)
+  int cus = 0;
+  float* sk_ws = nullptr;
+  long long sk_ws_floats = 0;
+  int* sk_cnt = nullptr;
+  int sk_cnt_cap = 0;
+  bool stream_k = true;
+  frhip::Precision prec = frhip::PREC_F32;
+
+  // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
+  frhip_rt::Detector* det = nullptr;
+
+  // profiling
+  bool prof = false;
+  std::vector<frhip_rt::ProfEvent> events;
+  std::vector<hipEvent_t> pool;
+
+  ~fr_handle() {
+    frhip_rt::detector_destroy(det);
+    for (auto& e : events) {
+      (void)hipEventDestroy(e.a);
+      (void)hipEventDestroy(e.b);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+    (void)hipFree(arena);
+    for (auto p : act) (void)hipFree(p);
+    (void)hipFree(sc_buf);
+    (void)hipFree(partial);
+    (void)hipFree(in_stage);
+    (void)hipFree(emb_stage);
+    (void)hipFree(gallery);
+    (void)hipFree(qn);
+    (void)hipFree(scores);
+    (void)hipFree(match_io);
+    (void)hipFree(gallery_tmp);
+    (void)hipFree(tpl_offsets);
+    (void)hipFree(sk_ws);
+    (void)hipFree(sk_cnt);
+    (void)hipFree(align_m);
+    (void)hipFree(blur_out);
+  }
+};
+
+namespace frhip_rt {
+
+int fail(fr_handle* h, int code, const std::string& msg);
+
+#define FR_HIP(h, call)                                                                          \
+  do {                                                                                           \
+    hipError_t e_ = (call);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return ::frhip_rt::fail(h, FR_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Host staging of every folded tensor before one upload into an arena.
+struct Packer {
+  std::vector<float> buf;
+  std::vector<std::pair<float**, size_t>> fix;  // (destination pointer, float offset)
+  void put(float** dst, const std::vector<float>& v) {
+    size_t off = (buf.size() + 3) & ~size_t(3);  // 16-B alignment for float4 loads
+    buf.resize(off);
+    buf.insert(buf.end(), v.begin(), v.end());
+    fix.push_back({dst, off});
+  }
+};
+
+void add_bn(std::map<std::string, size_t>& m, const std::string& p, int c, bool affine = true);
+void bn_fold(const std::vector<float>* gamma, const std::vector<float>* beta, const std::vector<float>& mean,
+             const std::vector<float>& var, std::vector<float>& scale, std::vector<float>& shift);
+std::vector<float> repack_oihw(const std::vector<float>& w, int O, int I, int kh, int kw);
+int ensure_buf(fr_handle* h, void** p, size_t* cap, size_t bytes);
+int ensure_stream_k(int device, int* cus, float** ws, long long* ws_floats, int** cnt, int* cnt_cap);
+int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, frhip::Epi epi,
+             const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s);
+const std::vector<float>* getp(fr_handle* h, const std::string& k);
+
+// detector.cpp
+std::map<std::string, size_t> detector_schema();
+int detector_finalize(fr_handle* h);
+int detector_run(fr_handle* h, const uint8_t* frames, int n, int height, int width, float det_thresh, int max_faces,
+                 float* dets, int32_t* counts, hipStream_t s);
+int detector_forward(fr_handle* h, const uint8_t* frames, int n, int height, int width, float* heads,
+                     uint8_t* canvas, hipStream_t s);
+
+}  // namespace frhip_rt

@@ -6,9 +6,12 @@ and the blur score (cv2.Laplacian variance, :94-99) run on the GPU through
 once yields crops that stay in HBM for ``FaceEmbedder.embed_tensor``.  Pose
 angles and the threshold logic are scalar host code, as in the reference.
 
-The detector (insightface ``FaceAnalysis('buffalo_l')`` SCRFD, :19-48) is not
-rebuilt yet (no weights or insightface offline):
-``FaceProcessor`` takes any detector object with the reference's
+``FaceDetector`` replaces insightface ``FaceAnalysis('buffalo_l')`` (SCRFD
+det_10g, :19-48) with the SCRFD-10G network on the GPU (``fr_detect``:
+letterbox, MFMA conv pyramid, anchor decode, NMS).  No weights exist offline,
+so it runs seeded synthetic weights unless ``model_path`` / ``state_dict``
+gives a state dict in ``detector_arch`` keys; ``FaceProcessor`` also accepts
+any detector object with the reference's
 ``detect(image_rgb) -> [{'bbox','landmarks','det_score',...}]`` contract.
 
 Parity of the OpenCV arithmetic is UNPINNED (cv2 absent); the kernels are
@@ -137,15 +140,65 @@ class FaceQualityFilter:
         return True, m
 
 
+class FaceDetector:
+    """``FaceDetector`` (face_recognition.py:19-48) on the GPU: SCRFD-10G at ``det_size``,
+    ``det_thresh``, NMS IoU 0.4; ``providers`` is accepted for signature parity."""
+
+    def __init__(self, det_size=(640, 640), det_thresh=0.5, providers=None, model_path: Optional[str] = None,
+                 state_dict=None, device=None, max_frames: int = 16, max_faces: int = 256):
+        from .detector_arch import synthetic_detector_state_dict
+        if tuple(det_size) != (640, 640):
+            raise NotImplementedError("the MI355X detector is built for det_size=(640, 640) (the reference's setting)")
+        self.det_size = tuple(det_size)
+        self.det_thresh = float(det_thresh)
+        self.max_faces = int(max_faces)
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+        if state_dict is None:
+            if model_path is not None:
+                sd = torch.load(model_path, map_location="cpu", weights_only=True)
+                state_dict = sd.get("state_dict", sd) if isinstance(sd, dict) else sd
+            else:
+                state_dict = synthetic_detector_state_dict()
+        self.model = _lib.Handle("scrfd_10g", "scrfd", self.device, max_batch=max_frames)
+        self.model.load_state_dict({k: v for k, v in state_dict.items()})
+
+    @staticmethod
+    def _to_rgb(image: np.ndarray) -> np.ndarray:
+        if image.ndim == 2:  # cv2.COLOR_GRAY2BGR replicates the channel (face_recognition.py:32-33)
+            image = np.repeat(image[:, :, None], 3, axis=2)
+        if image.ndim != 3 or image.shape[2] != 3:
+            raise ValueError(f"expected an HxW or HxWx3 image, got {image.shape}")
+        return np.ascontiguousarray(image, dtype=np.uint8)
+
+    @staticmethod
+    def _faces(dets: np.ndarray, count: int) -> List[Dict]:
+        out = []
+        for i in range(count):
+            d = dets[i]
+            out.append({"bbox": d[:4].astype(np.int32), "landmarks": d[5:15].reshape(5, 2).astype(np.float32),
+                        "det_score": float(d[4]), "pose": None, "age": None, "gender": None})
+        return out
+
+    def detect(self, image: np.ndarray) -> List[Dict]:
+        """RGB (or gray) uint8 image -> [{'bbox' int32 x1y1x2y2, 'landmarks' f32 (5,2), 'det_score', ...}]
+        in descending score order, like face_recognition.py:31-48."""
+        frame = torch.from_numpy(self._to_rgb(image)).to(self.device)
+        return self.detect_batch(frame[None])[0]
+
+    def detect_batch(self, frames: torch.Tensor) -> List[List[Dict]]:
+        """Device form: uint8 [n,H,W,3] RGB frames (one size) -> per-frame face lists."""
+        dets, counts = self.model.detect(frames, self.det_thresh, self.max_faces)
+        return [self._faces(dets[f], min(int(counts[f]), self.max_faces)) for f in range(dets.shape[0])]
+
+
 class FaceProcessor:
     """detect -> align -> quality (face_recognition.py:160-216) with device alignment and blur."""
 
     def __init__(self, output_size=224, det_size=(640, 640), det_thresh=0.5,
                  quality_filter_config: Optional[Dict] = None, providers=None, detector=None, device=None):
-        if detector is None:
-            raise NotImplementedError("the SCRFD detector is not rebuilt yet: pass detector=<object with "
-                                      "detect(image_rgb) -> list of {'bbox','landmarks','det_score'}>")
-        self.detector = detector
+        self.detector = detector if detector is not None else FaceDetector(det_size, det_thresh, providers,
+                                                                           device=device)
         self.aligner = FaceAligner(output_size=output_size, device=device)
         self.quality_filter = FaceQualityFilter(**(quality_filter_config or {}), device=device)
 

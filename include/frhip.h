@@ -129,6 +129,17 @@ int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, co
  * scores: host double [n].  Synchronises. */
 int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* scores);
 
+/* FaceDetector.detect (face_recognition.py:31-48: insightface SCRFD det_10g at det_size
+ * 640x640, det_thresh, NMS IoU 0.4) for n frames of one size.  The handle is created with
+ * fr_create("scrfd_10g", "scrfd", device, max_frames (1..64), &h) and loaded with the
+ * state dict of oracle/scrfd.py's network (fr_set_param / fr_finalize).
+ * frames: device uint8 [n][height][width][3] RGB.  Per frame f, counts[f] = detections
+ * after NMS (score order) and dets[f][i][0..14] = x1 y1 x2 y2 score, then 5 landmarks
+ * (x, y), in frame pixels, for i < min(counts[f], max_faces) (host buffers; synchronises).
+ * More than 4096 anchors above det_thresh in one frame -> FR_ERR_UNSUPPORTED. */
+int fr_detect(fr_handle* h, const uint8_t* frames, int n, int height, int width, float det_thresh, int max_faces,
+              float* dets, int32_t* counts, void* stream);
+
 /* Conv arithmetic of this handle.  FR_PRECISION_F32 (default): exact f32 products and f32
  * accumulation on fp32 MFMA -- the parity path.  FR_PRECISION_BF16X3 (opt-in fast mode):
  * each f32 operand split into bf16 hi + lo, x.y ~= hi.hi + hi.lo + lo.hi on bf16 MFMA with f32

@@ -39,6 +39,14 @@ int frt_fit_similarity(const float* src, const float* dst, int n, double* M);
 /* Row-wise top-k of a [n][G] score matrix (score desc, index asc). */
 int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, void* stream);
 
+/* Detector internals of fr_detect for n <= max_frames frames: letterbox + network only.
+ * heads: device f32, the three levels' maps back to back, each [n][H/s][W/s][32] for
+ * s = 8, 16, 32 (channels: cls a0, cls a1 logits | bbox a0 (4), a1 (4) | kps a0 (10), a1 (10)
+ * in stride units | 2 zero pads); canvas: device uint8 [n][640][640][3] letterboxed frames,
+ * or NULL.  Synchronises. */
+int frt_detector_forward(fr_handle* h, const uint8_t* frames, int n, int height, int width, float* heads,
+                         uint8_t* canvas, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,8 @@ def lib():
         L.frt_stem.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P, _P]
         L.frt_topk.restype = _I
         L.frt_topk.argtypes = [_P, _I, _I, _I, _P, _P, _P]
+        L.frt_detector_forward.restype = _I
+        L.frt_detector_forward.argtypes = [_P, _P, _I, _I, _I, _P, _P, _P]
         L._frt_ready = True
     return L
 
@@ -55,3 +57,19 @@ def topk(scores, k):
     val = torch.empty((n, k), dtype=torch.float32, device=scores.device)
     _lib.check(lib().frt_topk(_p(scores), n, G, k, _p(idx), _p(val), torch.cuda.current_stream().cuda_stream))
     return idx, val
+
+
+def detector_forward(handle, frames):
+    """Letterbox + SCRFD network on the GPU -> ([3 level maps [n,h,w,32]], canvas [n,640,640,3])."""
+    n, H, W = frames.shape[:3]
+    sizes = [(640 // s, 640 // s) for s in (8, 16, 32)]
+    heads = torch.empty(sum(n * h * w * 32 for h, w in sizes), dtype=torch.float32, device=frames.device)
+    canvas = torch.empty((n, 640, 640, 3), dtype=torch.uint8, device=frames.device)
+    rc = lib().frt_detector_forward(handle.h, _p(frames), n, H, W, _p(heads), _p(canvas),
+                                    torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc, handle.h)
+    out, off = [], 0
+    for h, w in sizes:
+        out.append(heads[off:off + n * h * w * 32].view(n, h, w, 32))
+        off += n * h * w * 32
+    return out, canvas
