@@ -47,6 +47,7 @@ _SIGNATURES = {
     "fr_blur_scores": (_I, [_P, _P, _I, _I, _P]),
     "fr_detect": (_I, [_P, _P, _I, _I, _I, ctypes.c_float, _I, _P, _P, _P]),
     "fr_set_precision": (_I, [_P, _I]),
+    "fr_set_conv_algorithm": (_I, [_P, _I]),
     "fr_profile_enable": (_I, [_P, _I]),
     "fr_profile_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
@@ -242,6 +243,12 @@ class Handle:
         if mode not in modes:
             raise ValueError(f"precision must be one of {sorted(modes)}")
         check(self._lib.fr_set_precision(self.h, modes[mode]), self.h)
+
+    def set_conv_algorithm(self, algo: str) -> None:
+        algos = {"direct": 0, "winograd": 1}
+        if algo not in algos:
+            raise ValueError(f"conv_algorithm must be one of {sorted(algos)}")
+        check(self._lib.fr_set_conv_algorithm(self.h, algos[algo]), self.h)
 
     # -- profiling ---------------------------------------------------------
     def profile_enable(self, on: bool = True) -> None:

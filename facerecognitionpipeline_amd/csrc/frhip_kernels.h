@@ -70,6 +70,28 @@ hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, in
 int conv_tile_bm(ConvTile t);
 int conv_tile_bn(ConvTile t);
 
+// Winograd F(2x2,3x3) stride-1 pad-1 conv in f32 (conv_winograd.hip), NHWC like ConvParams.
+//   u: transformed filters from launch_wino_weights (wino_weight_floats(Cout, Cin) floats).
+// Epilogues: EPI_AFFINE_PRELU (with pre-BN) and EPI_AFFINE_RES (without).
+struct WinoParams {
+  const float* x;
+  const float* u;
+  float* y;
+  const float* pre_scale;
+  const float* pre_shift;
+  const float* post_scale;
+  const float* post_shift;
+  const float* prelu;
+  const float* res;  // same shape as y
+  int B, H, W, Cin, Cout;
+  int TH, TW, ntiles, mblocks, nblocks;  // set by launch_wino
+};
+bool wino_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);
+size_t wino_weight_floats(int Cout, int Cin);
+// w: [Cout][3][3][Cin] f32 (device) -> u (device), fragment-ordered G g G^T.
+hipError_t launch_wino_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s);
+hipError_t launch_wino(const WinoParams& p, bool pre, Epi epi, hipStream_t s);
+
 // uint8 RGB HWC 112x112 -> (BGR, LUT normalise) -> conv3x3 3->64 -> BN -> PReLU, NHWC f32.
 hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64,
                        const float* bn_scale, const float* bn_shift, const float* prelu,

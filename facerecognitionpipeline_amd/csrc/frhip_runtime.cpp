@@ -301,6 +301,29 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // schedule (profiles/r01/sweep.txt): 8-wave 128x64 for the 64-channel
   // stage and the 128-channel residual convs, 8-wave 128x128 for the 1x1 shortcuts,
   // 8-wave 256x128 for every other 3x3 conv and the FC.
+  // Winograd F(2x2,3x3) for the stride-1 3x3 convs (f32 parity path only)
+  if (h->winograd && h->prec == PREC_F32 && cw.wino &&
+      ((epi == EPI_AFFINE_PRELU && cw.pre_scale) || (epi == EPI_AFFINE_RES && !cw.pre_scale && res_H == p.Ho))) {
+    WinoParams wp{};
+    wp.x = x;
+    wp.u = cw.wino;
+    wp.y = y;
+    wp.pre_scale = cw.pre_scale;
+    wp.pre_shift = cw.pre_shift;
+    wp.post_scale = cw.post_scale;
+    wp.post_shift = cw.post_shift;
+    wp.prelu = cw.prelu;
+    wp.res = res;
+    wp.B = B;
+    wp.H = H;
+    wp.W = W;
+    wp.Cin = cw.cin;
+    wp.Cout = cw.cout;
+    ProfScope ps(h, s, flop, true);
+    hipError_t e = launch_wino(wp, cw.pre_scale != nullptr, epi, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd launch: ") + hipGetErrorString(e));
+    return FR_OK;
+  }
   ConvTile tile = TILE_256x128_W8;
   if (cw.cout <= 64 || (cw.cout == 128 && epi == EPI_AFFINE_RES && cw.kh == 3))
     tile = TILE_128x64_W8;
@@ -675,6 +698,31 @@ int fr_finalize(fr_handle* h) {
   h->arena_floats = pk.buf.size();
   for (auto& f : pk.fix) *f.first = h->arena + f.second;
 
+  // Winograd filters G g G^T of every stride-1 3x3 conv, built on the device from the arena
+  std::vector<ConvW*> wconvs;
+  size_t wfloats = 0;
+  for (auto& b : h->blocks) {
+    for (ConvW* c : {&b.conv1, &b.conv2}) {
+      c->wino = nullptr;
+      if (wino_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
+        wconvs.push_back(c);
+        wfloats += wino_weight_floats(c->cout, c->cin);
+      }
+    }
+  }
+  if (h->wino_arena) FR_HIP(h, hipFree(h->wino_arena));
+  h->wino_arena = nullptr;
+  if (wfloats) {
+    FR_HIP(h, hipMalloc((void**)&h->wino_arena, wfloats * sizeof(float)));
+    size_t off = 0;
+    for (ConvW* c : wconvs) {
+      c->wino = h->wino_arena + off;
+      FR_HIP(h, launch_wino_weights(c->w, c->wino, c->cout, c->cin, nullptr));
+      off += wino_weight_floats(c->cout, c->cin);
+    }
+    FR_HIP(h, hipDeviceSynchronize());
+  }
+
   // workspace for max_batch crops
   const size_t mb = h->max_batch;
   if (!h->act[0]) {
@@ -995,6 +1043,15 @@ int fr_set_precision(fr_handle* h, int mode) {
   return FR_OK;
 }
 
+int fr_set_conv_algorithm(fr_handle* h, int algo) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (algo != FR_CONV_DIRECT && algo != FR_CONV_WINOGRAD)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "algorithm must be FR_CONV_DIRECT or FR_CONV_WINOGRAD");
+  h->winograd = algo == FR_CONV_WINOGRAD;
+  return FR_OK;
+}
+
 int fr_profile_enable(fr_handle* h, int enable) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -1085,6 +1142,43 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
   hipError_t e = launch_conv(p, (ConvTile)tile, pre_scale != nullptr, (Epi)epi, nsplit, (hipStream_t)stream,
                              precision == 1 ? PREC_BF16X3 : PREC_F32);
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
+                        const float* pre_scale, const float* pre_shift, const float* post_scale,
+                        const float* post_shift, const float* prelu, const float* res, int epi, void* stream) {
+  if (!wino_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
+      (epi == EPI_AFFINE_PRELU && (!pre_scale || !pre_shift || !prelu)) || (epi == EPI_AFFINE_RES && (pre_scale || !res)) ||
+      !post_scale || !post_shift || B < 1 || H < 1 || W < 1)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  float* u = nullptr;
+  if (hipMalloc((void**)&u, wino_weight_floats(cout, cin) * sizeof(float)) != hipSuccess)
+    return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd: allocation failed");
+  hipError_t e = launch_wino_weights(w, u, cout, cin, s);
+  if (e == hipSuccess) {
+    WinoParams p{};
+    p.x = x;
+    p.u = u;
+    p.y = y;
+    p.pre_scale = pre_scale;
+    p.pre_shift = pre_shift;
+    p.post_scale = post_scale;
+    p.post_shift = post_shift;
+    p.prelu = prelu;
+    p.res = res;
+    p.B = B;
+    p.H = H;
+    p.W = W;
+    p.Cin = cin;
+    p.Cout = cout;
+    e = launch_wino(p, pre_scale != nullptr, (Epi)epi, s);
+  }
+  const hipError_t se = hipStreamSynchronize(s);
+  (void)hipFree(u);
+  if (e == hipSuccess) e = se;
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd: ") + hipGetErrorString(e));
   return FR_OK;
 }
 

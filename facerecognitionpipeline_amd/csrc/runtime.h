@@ -25,6 +25,7 @@ struct ConvW {
   float* post_scale = nullptr;
   float* post_shift = nullptr;
   float* prelu = nullptr;
+  float* wino = nullptr;  // Winograd-transformed filters (stride-1 3x3 only), or null
   int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
 };
 
@@ -102,6 +103,8 @@ struct fr_handle {
   int sk_cnt_cap = 0;
   bool stream_k = true;
   frhip::Precision prec = frhip::PREC_F32;
+  bool winograd = true;          // FR_CONV_WINOGRAD for stride-1 3x3 convs
+  float* wino_arena = nullptr;   // transformed filters of every eligible conv
 
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
   frhip_rt::Detector* det = nullptr;
@@ -119,6 +122,7 @@ struct fr_handle {
     }
     for (auto e : pool) (void)hipEventDestroy(e);
     (void)hipFree(arena);
+    (void)hipFree(wino_arena);
     for (auto p : act) (void)hipFree(p);
     (void)hipFree(sc_buf);
     (void)hipFree(partial);

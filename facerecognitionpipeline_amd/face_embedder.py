@@ -51,7 +51,8 @@ def _as_device(device) -> torch.device:
 class FaceEmbedder:
     def __init__(self, architecture: str = "ir_101", model_path: Optional[str] = None,
                  model_type: str = "adaface", device=None, max_batch: int = 256,
-                 state_dict=None, weight_seed: Optional[int] = None, precision: str = "fp32"):
+                 state_dict=None, weight_seed: Optional[int] = None, precision: str = "fp32",
+                 conv_algorithm: str = "winograd"):
         self.device = _as_device(device)
         self.model_type = model_type
         self.architecture = architecture
@@ -78,6 +79,8 @@ class FaceEmbedder:
         self.model.load_state_dict(state_dict)
         self.precision = precision
         self.model.set_precision(precision)
+        self.conv_algorithm = conv_algorithm
+        self.model.set_conv_algorithm(conv_algorithm)
         self.input_size = INPUT_SIZE
         # face_embedder.py:60-61 (AdaFace) and :86-87 (ArcFace)
         self.mean, self.std = (0.5, 0.5) if model_type == "adaface" else (127.5, 127.5)

@@ -148,6 +148,15 @@ int fr_detect(fr_handle* h, const uint8_t* frames, int n, int height, int width,
 #define FR_PRECISION_BF16X3 1
 int fr_set_precision(fr_handle* h, int mode);
 
+/* Algorithm of the stride-1 3x3 convs (the bulk of the network's MACs).  Both compute in f32.
+ * FR_CONV_WINOGRAD (default): Winograd F(2x2,3x3) -- filters transformed once at
+ * fr_finalize, 16 f32-MFMA products per 2x2 tile instead of 36; embeddings within 1e-5 of the
+ * CPU reference (tests).  FR_CONV_DIRECT: the implicit-GEMM kernel for every conv.
+ * Ignored under FR_PRECISION_BF16X3 (direct split-bf16 everywhere). */
+#define FR_CONV_DIRECT 0
+#define FR_CONV_WINOGRAD 1
+int fr_set_conv_algorithm(fr_handle* h, int algo);
+
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).
  * enable=1 starts recording; fr_profile_read synchronises and returns, since the
  * last read: summed milliseconds and algorithmic FLOPs of the conv_mfma launches,

@@ -28,6 +28,14 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
                const float* post_shift, const float* prelu, const float* res, int res_h, int res_w, int epi,
                int nsplit, int tile, int stream_k, int precision, void* stream);
 
+/* Winograd F(2x2,3x3) stride-1 pad-1 conv (the FR_CONV_WINOGRAD path): same tensors as
+ * frt_conv2d with kh = kw = 3; w is the untransformed [cout][3][3][cin] filter (transformed
+ * into a scratch buffer here).  epi: 1 (needs pre) or 2 (no pre).  cin, cout % 32 == 0.
+ * Synchronises. */
+int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
+                        const float* pre_scale, const float* pre_shift, const float* post_scale,
+                        const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
+
 /* Fused preprocess + input_layer on uint8 RGB [B][112][112][3]; w27x64 is the
  * repacked [ky][kx][c_rgb][64] weight; lut the 256-entry normalisation table. */
 int frt_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, const float* bn_scale,

@@ -14,6 +14,8 @@ def lib():
     if not getattr(L, "_frt_ready", False):
         L.frt_conv2d.restype = _I
         L.frt_conv2d.argtypes = [_P, _P, _P] + [_I] * 9 + [_P] * 6 + [_I] * 7 + [_P]
+        L.frt_conv2d_winograd.restype = _I
+        L.frt_conv2d_winograd.argtypes = [_P, _P, _P] + [_I] * 5 + [_P] * 6 + [_I, _P]
         L.frt_stem.restype = _I
         L.frt_stem.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P, _P]
         L.frt_topk.restype = _I
@@ -41,6 +43,17 @@ def conv2d(x, w, B, H, W, cin, cout, kh, kw, stride, pad, pre=None, post=None, p
                           torch.cuda.current_stream().cuda_stream)
     _lib.check(rc)
     return y if nsplit > 1 else y[0]
+
+
+def conv2d_winograd(x, w, B, H, W, cin, cout, pre=None, post=None, prelu=None, res=None, epi=1):
+    """Winograd F(2x2,3x3) stride-1 conv; x NHWC cuda f32, w [cout][3][3][cin] cuda f32."""
+    y = torch.full((B, H, W, cout), float("nan"), device=x.device)
+    ps, ph = (pre if pre is not None else (None, None))
+    qs, qh = post
+    rc = lib().frt_conv2d_winograd(_p(x), _p(w), _p(y), B, H, W, cin, cout, _p(ps), _p(ph), _p(qs), _p(qh),
+                                   _p(prelu), _p(res), epi, torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc)
+    return y
 
 
 def stem(img, lut, w27x64, sc, sh, al):

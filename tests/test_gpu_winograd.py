@@ -1,0 +1,97 @@
+"""Winograd F(2x2,3x3) conv (FR_CONV_WINOGRAD, the default for stride-1 3x3 convs) vs PyTorch CPU.
+
+Same f32 tolerance as the direct kernel (tests/test_gpu_kernels.py): |d| <= 1e-5 * max|ref| + 1e-6.
+The transforms add a few f32 roundings per output (input: 2 adds, output: 4 adds, filter: rounded
+once from double), well inside that bar; the network-level check compares whole embeddings.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tests import _frt
+from tests.test_gpu_kernels import _close, _nhwc, _rand
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _wino_case(B, H, cin, cout, epi, seed, W=None):
+    W = W or H
+    x = _rand(B, cin, H, W, seed=seed)
+    w = _rand(cout, cin, 3, 3, seed=seed + 1) / (cin * 9) ** 0.5
+    pre_s, pre_b = _rand(cin, seed=seed + 2, lo=0.5, hi=1.5), _rand(cin, seed=seed + 3, lo=-0.2, hi=0.2)
+    post_s, post_b = _rand(cout, seed=seed + 4, lo=0.5, hi=1.5), _rand(cout, seed=seed + 5, lo=-0.2, hi=0.2)
+    al = _rand(cout, seed=seed + 6, lo=0.1, hi=0.4)
+    xin = x * pre_s.view(1, -1, 1, 1) + pre_b.view(1, -1, 1, 1) if epi == 1 else x
+    ref = F.conv2d(xin, w, padding=1) * post_s.view(1, -1, 1, 1) + post_b.view(1, -1, 1, 1)
+    res = None
+    if epi == 1:
+        ref = torch.where(ref > 0, ref, ref * al.view(1, -1, 1, 1))
+    else:
+        r = _rand(B, cout, H, W, seed=seed + 7)
+        ref = ref + r
+        res = _nhwc(r).to(DEV)
+    got = _frt.conv2d_winograd(_nhwc(x).to(DEV), w.permute(0, 2, 3, 1).contiguous().to(DEV), B, H, W, cin, cout,
+                               pre=(pre_s.to(DEV), pre_b.to(DEV)) if epi == 1 else None,
+                               post=(post_s.to(DEV), post_b.to(DEV)),
+                               prelu=al.to(DEV) if epi == 1 else None, res=res, epi=epi)
+    torch.cuda.synchronize()
+    return got.cpu(), _nhwc(ref)
+
+
+@pytest.mark.parametrize("B,H,cin,cout", [
+    (2, 14, 64, 64),     # NBW=2, ragged last block (2*49 = 98 tiles)
+    (3, 9, 128, 96),     # odd H (edge tiles half outside), Cout % 64 != 0 -> NBW=1
+    (4, 7, 512, 512),    # stage-4 shape: 4x4 tiles of a 7x7 map
+    (1, 28, 256, 256),   # stage-3 width
+    (2, 56, 64, 64),     # stage-1 shape
+    (1, 112, 64, 64),    # stage-1 unit-1 conv1 at input resolution
+    (1, 1, 32, 32),      # 1x1 map: a single tile, 3 of its 4 outputs outside
+])
+@pytest.mark.parametrize("epi", [1, 2])
+def test_winograd_conv_matches_cpu(B, H, cin, cout, epi):
+    got, ref = _wino_case(B, H, cin, cout, epi, seed=300 + H + cin + epi)
+    _close(got, ref)
+
+
+def test_winograd_non_square_map():
+    got, ref = _wino_case(2, 10, 64, 128, 1, seed=400, W=13)
+    _close(got, ref)
+
+
+def test_winograd_is_deterministic():
+    a, _ = _wino_case(2, 14, 128, 128, 2, seed=410)
+    b, _ = _wino_case(2, 14, 128, 128, 2, seed=410)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("arch", ["ir_50", "ir_101"])
+def test_network_winograd_vs_direct_vs_oracle(arch):
+    """Whole IR network: the Winograd default and the direct path both within 1e-5 of the
+    PyTorch-CPU oracle per embedding element, and identical top-5 gallery order."""
+    from facerecognitionpipeline_amd import weights as W
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    from oracle.adaface_net import load_oracle
+    from oracle import reference_path as rp
+
+    sd = W.synthetic_state_dict(arch)
+    crops = W.synthetic_crops(24, seed=W.CROP_SEED_GALLERY)
+    probes = W.probe_crops(crops, 24)
+    ref_g = rp.extract_embeddings_batch(load_oracle(arch, sd), list(crops))
+    ref_p = rp.extract_embeddings_batch(load_oracle(arch, sd), list(probes))
+    out = {}
+    for algo in ("winograd", "direct"):
+        emb = FaceEmbedder(architecture=arch, state_dict=sd, device="cuda:0", max_batch=32, conv_algorithm=algo)
+        g = emb.extract_embeddings_batch(list(crops))
+        p = emb.extract_embeddings_batch(list(probes))
+        assert np.abs(g - ref_g).max() <= 1e-5, (algo, np.abs(g - ref_g).max())
+        assert np.abs(p - ref_p).max() <= 1e-5, (algo, np.abs(p - ref_p).max())
+        out[algo] = (g, p)
+        del emb
+    ref_s = ref_p @ ref_g.T
+    ref_top = np.argsort(-ref_s, axis=1, kind="stable")[:, :5]
+    for algo, (g, p) in out.items():
+        s = p @ g.T
+        assert np.abs(s - ref_s).max() <= 1e-4, algo
+        assert np.array_equal(np.argsort(-s, axis=1, kind="stable")[:, :5], ref_top), algo
