@@ -19,13 +19,12 @@
 //   * 8 waves; wave w owns xi = 2w, 2w+1 and the whole 32 x BN tile of both, so its
 //     accumulators are 2 x NBW 32x32 MFMA blocks (32*NBW VGPRs) and no operand it reads
 //     is read by any other wave.
-//   * K-step = 16 input channels.  Thread (tile, channel group cg of 4, patch column j)
-//     loads its patch column as 4 x 16-B buffer loads (OOB offset -> 0 = zero padding;
-//     the pre-BN affine is applied only to in-image taps), mixes rows in registers and
-//     columns across its lane quad (DPP quad_perm), and writes 4 x float4 of V to LDS
-//     V[xi][tile][ch] (rows of 20 floats: the ds_read_b128 fragment reads are
-//     conflict-free; planes 648 floats apart: so are the ds_write_b128).  The transform is
-//     shared by all 16 GEMMs, which is why the 16 live in one workgroup.
+//   * K-step = 16 input channels.  Thread (tile = tid/16, ch = tid%16) loads the 4x4
+//     patch of its tile at its channel (buffer loads: OOB offset -> 0 = zero padding;
+//     the pre-BN affine is applied only to in-image taps), transforms it with 32 adds
+//     and writes the 16 V values to LDS V[xi][tile][ch] (rows of 20 floats: the
+//     ds_read_b128 fragment reads are conflict-free).  The transform is shared by all
+//     16 GEMMs, which is why the 16 live in one workgroup.
 //   * U (transformed filters, built once per model by wino_weight_kernel) never
 //     touches LDS: it is pre-permuted in HBM into MFMA-fragment order, so each wave
 //     fetches its own B fragments with fully coalesced 1 KiB buffer loads.
@@ -44,6 +43,7 @@
 // j (0..7) multiplies channel 8h + j: lane (m, h) reads V[xi][m][8h .. 8h+7] with two
 // ds_read_b128 and the matching 8 U values with two 16-B loads.
 #include "frhip_kernels.h"
+#define launch_wino launch_wino_x
 
 namespace frhip {
 namespace {
@@ -54,7 +54,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int WT = 32;             // 2x2 output tiles per workgroup (MFMA M)
 constexpr int WKC = 16;            // input channels per K-step
 constexpr int VROW = 20;           // LDS floats per (xi, tile) row: 16 channels + 4 pad
-constexpr int VPLANE = WT * VROW + 8;  // one xi plane; 648 = 8 mod 32: conflict-free b128 writes
+constexpr int VPLANE = WT * VROW;  // one xi plane
 constexpr int VBUF = 16 * VPLANE;  // one K-step of V (40 KiB)
 constexpr int MROW = 33;           // epilogue staging row: 32 couts + 1
 constexpr int MPLANE = WT * MROW;
@@ -67,18 +67,7 @@ __device__ __forceinline__ int wino_xcd_remap(int bid, int n) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-// Buffer descriptor from provably wave-uniform inputs (readfirstlane), so the compiler
-// keeps it in SGPRs instead of wrapping every buffer op in a waterfall loop.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* ptr, int bytes) {
-  const unsigned long long a = reinterpret_cast<unsigned long long>(ptr);
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-  const int n = __builtin_amdgcn_readfirstlane(bytes);
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, n,
-                                           0x00020000);
-}
-
-template <int NBW, bool PRE, int EPI>
+template <int NBW, bool PRE, int EPI, int MODE>
 __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
   constexpr int BN = 32 * NBW;
   constexpr bool RES = EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU;
@@ -94,73 +83,69 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
   const int KS = Cin / WKC;
   const int NB32 = p.Cout / 32;
 
-  // ---- transform role: thread (tile, channel group of 4, patch column j) ------------
-  // lane = j + 4*cg + 16*tile_in_wave: a quad holds the 4 columns of one (tile, cg), so
-  // the column half of the transform is a DPP quad exchange.
-  const int tj = tid & 3, tcg = (tid >> 2) & 3, tl = tid >> 4;
+  // ---- transform role: one (tile, channel) per thread --------------------------------
+  const int tl = tid >> 4, tc = tid & 15;
   const int T = mb * WT + tl;
   int base = 0;
-  unsigned mask = 0;  // bit i: patch pixel (row i, column tj) is inside the image
+  unsigned mask = 0;
   if (T < p.ntiles) {
     const int n = T / per_img;
     const int r = T - n * per_img;
     const int ty = r / p.TW, tx = r - ty * p.TW;
-    const int y0 = 2 * ty - 1, x = 2 * tx - 1 + tj;
+    const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if ((unsigned)(y0 + i) < (unsigned)H && (unsigned)x < (unsigned)W) mask |= 1u << i;
-    base = (((n * H + y0) * W + x) * Cin + 4 * tcg) * 4;  // only used at in-image taps
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((unsigned)(y0 + i) < (unsigned)H && (unsigned)(x0 + j) < (unsigned)W) mask |= 1u << (4 * i + j);
+    base = (((n * H + y0) * W + x0) * Cin + tc) * 4;  // only used at in-image taps
   }
-  const int rowb = W * Cin * 4;
-  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
-  const __amdgpu_buffer_rsrc_t ur = uniform_rsrc(p.u, 16 * p.Cout * Cin * 4);
-  auto f4 = [](u32x4 v) {
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-  };
+  const int rowb = W * Cin * 4, colb = Cin * 4;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.B * H * W * Cin * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, 16 * p.Cout * Cin * 4, 0x00020000);
 
-  auto load_in = [&](float4 (&d)[4], float4 (&ps)[2], int s) {
+  auto load_in = [&](float (&d)[16], float (&ps)[2], int s) {
     const unsigned m = s < KS ? mask : 0u;
     const int off = base + s * WKC * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      d[i] = f4(__builtin_amdgcn_raw_buffer_load_b128(xr, ((m >> i) & 1u) ? off + i * rowb : OOB, 0, 0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = (m >> (4 * i + j)) & 1u;
+        d[4 * i + j] =
+            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ok ? off + i * rowb + j * colb : OOB, 0, 0));
+      }
     if constexpr (PRE) {
-      const int c = min(s, KS - 1) * WKC + 4 * tcg;
-      ps[0] = *reinterpret_cast<const float4*>(p.pre_scale + c);
-      ps[1] = *reinterpret_cast<const float4*>(p.pre_shift + c);
+      const int c = min(s, KS - 1) * WKC + tc;
+      ps[0] = p.pre_scale[c];
+      ps[1] = p.pre_shift[c];
     }
   };
-  // V = B^T d B for this thread's column: rows mixed in registers (B^T d), columns
-  // mixed across the quad: V[.][j] = sa*r[.][j] + sb*r[.][partner], partner = (2,2,1,1)[j],
-  // (sa, sb) = (1,-1), (1,1), (1,-1), (-1,1).
-  const float sa = tj == 3 ? -1.f : 1.f, sb = (tj == 0 || tj == 2) ? -1.f : 1.f;
-  auto store_v = [&](const float4 (&d)[4], const float4 (&ps)[2], int buf) {
-    float4 v[4];
+  auto store_v = [&](const float (&d)[16], const float (&ps)[2], int buf) {
+    float v[16];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[i] = d[i];
-      if constexpr (PRE) {
-        const bool ok = (mask >> i) & 1u;
-        v[i].x = ok ? v[i].x * ps[0].x + ps[1].x : 0.f;
-        v[i].y = ok ? v[i].y * ps[0].y + ps[1].y : 0.f;
-        v[i].z = ok ? v[i].z * ps[0].z + ps[1].z : 0.f;
-        v[i].w = ok ? v[i].w * ps[0].w + ps[1].w : 0.f;
-      }
+    for (int e = 0; e < 16; ++e) {
+      v[e] = d[e];
+      if constexpr (PRE) v[e] = ((mask >> e) & 1u) ? v[e] * ps[0] + ps[1] : 0.f;
     }
-    float4 r[4];
-    r[0] = v[0] - v[2];
-    r[1] = v[1] + v[2];
-    r[2] = v[2] - v[1];
-    r[3] = v[1] - v[3];
-    float* dst = lds + buf * VBUF + tj * VPLANE + tl * VROW + 4 * tcg;
+    float m[16];
+    // B^T d (rows), then (.) B (columns)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      m[0 + j] = v[0 + j] - v[8 + j];
+      m[4 + j] = v[4 + j] + v[8 + j];
+      m[8 + j] = v[8 + j] - v[4 + j];
+      m[12 + j] = v[4 + j] - v[12 + j];
+    }
+    float* dst = lds + buf * VBUF + tl * VROW + tc;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float4 o;
-      o.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[i].x), 0x5A, 0xF, 0xF, false));
-      o.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[i].y), 0x5A, 0xF, 0xF, false));
-      o.z = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[i].z), 0x5A, 0xF, 0xF, false));
-      o.w = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[i].w), 0x5A, 0xF, 0xF, false));
-      *reinterpret_cast<float4*>(dst + 4 * i * VPLANE) = sa * r[i] + sb * o;
+      dst[(4 * i + 0) * VPLANE] = m[4 * i + 0] - m[4 * i + 2];
+      dst[(4 * i + 1) * VPLANE] = m[4 * i + 1] + m[4 * i + 2];
+      dst[(4 * i + 2) * VPLANE] = m[4 * i + 2] - m[4 * i + 1];
+      dst[(4 * i + 3) * VPLANE] = m[4 * i + 1] - m[4 * i + 3];
     }
   };
 
@@ -175,7 +160,9 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int idx = ((((2 * wid + xl) * NB32 + nb * NBW + b) * KS + s) * 2 + q) * 64 + lane;
-          u[xl][b][q] = f4(__builtin_amdgcn_raw_buffer_load_b128(ur, s < KS ? idx * 16 : OOB, 0, 0));
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ur, s < KS ? idx * 16 : OOB, 0, 0);
+          u[xl][b][q] =
+              make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
         }
   };
 
@@ -191,12 +178,10 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
   // ago), U(s) in `uc`.  Issues the loads of patch s+2 (into `dn`, free since V(s) was
   // written) and U(s+1), runs the MFMAs of s and, in their shadow, transforms patch s+1
   // into the other LDS buffer; one barrier.
-  auto step = [&](int s, const ufrag& uc, ufrag& un, const float4 (&dc)[4], const float4 (&pc)[2],
-                  float4 (&dn)[4], float4 (&pn)[2], int buf) {
-    // U(s+1) first: vmcnt retires in issue order, so the wait for U at the top of the next
-    // step must not also wait for this step's patch loads (which may come from HBM)
-    load_u(un, s + 1);
-    load_in(dn, pn, s + 2);
+  auto step = [&](int s, const ufrag& uc, ufrag& un, const float (&dc)[16], const float (&pc)[2],
+                  float (&dn)[16], float (&pn)[2], int buf) {
+    if constexpr (MODE & 1) load_in(dn, pn, s + 2);
+    if constexpr (MODE & 2) load_u(un, s + 1);
     const float* vb = lds + buf * VBUF + (lane & 31) * VROW + 8 * (lane >> 5);
     float4 a[2][2];
 #pragma unroll
@@ -213,15 +198,15 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
         for (int b = 0; b < NBW; ++b)
           acc[xl][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[xl][j >> 2][j & 3], uc[xl][b][j >> 2][j & 3],
                                                             acc[xl][b], 0, 0, 0);
-    store_v(dc, pc, buf ^ 1);
+    if constexpr (MODE & 4) store_v(dc, pc, buf ^ 1);
     // 4 fragment reads up front; then per MFMA: a share of the loads, of the transform
     // VALU and (in the second half) of its 16 LDS writes
     constexpr int NMFMA = 16 * NBW;
-    constexpr int NVMEM = 4 + 4 * NBW + (PRE ? 2 : 0);
+    constexpr int NVMEM = 16 + 4 * NBW + (PRE ? 2 : 0);
     constexpr int VM_PER = (NVMEM + NMFMA - 1) / NMFMA;
-    constexpr int VALU_PER = PRE ? 8 : 4;
+    constexpr int VALU_PER = PRE ? 6 : 4;
     constexpr int DSW_FROM = NMFMA / 2;
-    constexpr int DSW_PER = (4 + (NMFMA - DSW_FROM) - 1) / (NMFMA - DSW_FROM);
+    constexpr int DSW_PER = (16 + (NMFMA - DSW_FROM) - 1) / (NMFMA - DSW_FROM);
     __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
     for (int i = 0; i < NMFMA; ++i) {
@@ -231,12 +216,9 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
       if (i >= DSW_FROM) __builtin_amdgcn_sched_group_barrier(0x200, DSW_PER, 0);
     }
     __syncthreads();
-    // nothing crosses a step boundary: VALU of the next step hoisted above the barrier
-    // would wait on loads issued in this one
-    __builtin_amdgcn_sched_barrier(0);
   };
 
-  float4 dA[4], dB[4], pA[2], pB[2];
+  float dA[16], dB[16], pA[2] = {1.f, 0.f}, pB[2] = {1.f, 0.f};
   ufrag uA, uB;
   load_in(dA, pA, 0);
   load_u(uA, 0);
@@ -254,7 +236,8 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
   // residuals are loaded before the staging barrier so their latency overlaps it
   int pix[2], okm[2];
   float rv[NBW][2][4];
-  const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, RES ? p.B * H * W * p.Cout * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.res, (short)0, RES ? p.B * H * W * p.Cout * 4 : 0, 0x00020000);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int Tq = mb * WT + (tid >> 5) + 16 * q;
@@ -367,45 +350,44 @@ __global__ void wino_weight_kernel(const float* __restrict__ w, float* __restric
 }
 
 }  // namespace
-
-bool wino_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
-  return kh == 3 && kw == 3 && stride == 1 && pad == 1 && Cin % 32 == 0 && Cin >= 32 && Cout % 32 == 0 &&
-         Cout >= 32;
-}
-
-hipError_t launch_wino_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s) {
-  if (Cout % 32 || Cin % 32) return hipErrorInvalidValue;
-  const int n = Cout * Cin;
-  hipLaunchKernelGGL(wino_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, u, Cout, Cin);
-  return hipGetLastError();
-}
-
-hipError_t launch_wino(const WinoParams& p0, bool pre, Epi epi, hipStream_t s) {
-  WinoParams p = p0;
-  if (!wino_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
-      (long long)p.B * p.H * p.W * p.Cin * 4 >= (1ll << 31) ||
-      (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) || (long long)16 * p.Cout * p.Cin * 4 >= (1ll << 31))
-    return hipErrorInvalidValue;
-  p.TH = (p.H + 1) / 2;
-  p.TW = (p.W + 1) / 2;
-  p.ntiles = p.B * p.TH * p.TW;
-  p.mblocks = (p.ntiles + WT - 1) / WT;
-  const int nbw = (p.Cout % 64 == 0) ? 2 : 1;
-  p.nblocks = p.Cout / (32 * nbw);
-  const dim3 grid(p.mblocks * p.nblocks), block(512);
-#define FR_WINO_CASE(NBW_, PRE_, EPI_)                                         \
-  if (nbw == NBW_ && pre == PRE_ && epi == EPI_) {                             \
-    hipLaunchKernelGGL((wino_kernel<NBW_, PRE_, EPI_>), grid, block, 0, s, p); \
-    return hipGetLastError();                                                  \
-  }
-  FR_WINO_CASE(2, true, EPI_AFFINE_PRELU)
-  FR_WINO_CASE(2, false, EPI_AFFINE_RES)
-  FR_WINO_CASE(1, true, EPI_AFFINE_PRELU)
-  FR_WINO_CASE(1, false, EPI_AFFINE_RES)
-#undef FR_WINO_CASE
-  return hipErrorInvalidValue;
-}
-
-size_t wino_weight_floats(int Cout, int Cin) { return (size_t)16 * Cout * Cin; }
-
 }  // namespace frhip
+
+#include <cstdio>
+#include <cstdlib>
+using namespace frhip;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%d %s\n", __LINE__, hipGetErrorString(e_)); exit(1);} } while (0)
+__global__ void fillk(float* p, long long n, unsigned seed) {
+  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i < n) { unsigned x = (unsigned)i * 2654435761u ^ seed; x ^= x >> 13; x *= 0x5bd1e995; x ^= x >> 15; p[i] = ((x & 0xffffff) / 16777216.f - 0.5f); }
+}
+static float* dalloc(long long n, unsigned seed) { float* p; CK(hipMalloc(&p, n * 4)); fillk<<<(n + 255) / 256, 256>>>(p, n, seed); return p; }
+template <int MODE> void run(WinoParams p, int reps, const char* name) {
+  dim3 grid(p.mblocks * p.nblocks), block(512);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((wino_kernel<2, true, EPI_AFFINE_PRELU, MODE>), grid, block, 0, 0, p);
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); CK(hipEventRecord(a, 0));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((wino_kernel<2, true, EPI_AFFINE_PRELU, MODE>), grid, block, 0, 0, p);
+  CK(hipEventRecord(b, 0)); CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
+  const double us = 1e3 * ms / reps;
+  const double exe = 2.0 * p.ntiles * 16.0 * p.Cin * p.Cout;
+  printf("H=%3d C=%3d mode %-22s %8.1f us  exec %6.1f TF/s (%4.1f%%)\n", p.H, p.Cin, name, us, exe / us * 1e-6, exe / us * 1e-6 / 1.573);
+}
+int main(int argc, char** argv) {
+  const int B = 256;
+  int shapes[][2] = {{14, 256}, {56, 64}, {7, 512}};
+  for (auto& sh : shapes) {
+    const int H = sh[0], C = sh[1];
+    const long long act = (long long)B * H * H * C;
+    WinoParams p{};
+    p.x = dalloc(act, 1); p.y = dalloc(act, 2); p.res = p.y;
+    p.u = dalloc(16LL * C * C, 3);
+    p.pre_scale = dalloc(C, 4); p.pre_shift = dalloc(C, 5); p.post_scale = p.pre_scale; p.post_shift = p.pre_shift; p.prelu = p.pre_shift;
+    p.B = B; p.H = H; p.W = H; p.Cin = C; p.Cout = C;
+    p.TH = (H + 1) / 2; p.TW = p.TH; p.ntiles = B * p.TH * p.TW; p.mblocks = (p.ntiles + 31) / 32; p.nblocks = C / 64;
+    run<7>(p, 20, "full");
+    run<6>(p, 20, "no-input-loads");
+    run<5>(p, 20, "no-U-loads");
+    run<3>(p, 20, "no-transform");
+    run<0>(p, 20, "mfma+lds-read+barrier");
+  }
+  return 0;
+}
