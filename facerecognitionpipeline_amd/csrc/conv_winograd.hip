@@ -118,22 +118,29 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
   };
 
-  auto load_in = [&](float4 (&d)[4], float4 (&ps)[2], int s) {
-    const unsigned m = s < KS ? mask : 0u;
-    const int off = base + s * WKC * 4;
+  // per-lane offsets fixed for the whole K loop (OOB for out-of-image pixels); the K-step
+  // enters as a scalar soffset.  Prefetches past the last step re-load the last step
+  // (clamped), so no lane ever needs a per-step range select.
+  int voff[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      d[i] = f4(__builtin_amdgcn_raw_buffer_load_b128(xr, ((m >> i) & 1u) ? off + i * rowb : OOB, 0, 0));
+  for (int i = 0; i < 4; ++i) voff[i] = ((mask >> i) & 1u) ? base + i * rowb : OOB;
+  const __amdgpu_buffer_rsrc_t pr = uniform_rsrc(p.pre_scale, PRE ? Cin * 4 : 0);
+  const __amdgpu_buffer_rsrc_t qr = uniform_rsrc(p.pre_shift, PRE ? Cin * 4 : 0);
+  auto load_in = [&](float4 (&d)[4], float4 (&ps)[2], int s) {
+    const int so = min(s, KS - 1) * WKC * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = f4(__builtin_amdgcn_raw_buffer_load_b128(xr, voff[i], so, 0));
     if constexpr (PRE) {
-      const int c = min(s, KS - 1) * WKC + 4 * tcg;
-      ps[0] = *reinterpret_cast<const float4*>(p.pre_scale + c);
-      ps[1] = *reinterpret_cast<const float4*>(p.pre_shift + c);
+      ps[0] = f4(__builtin_amdgcn_raw_buffer_load_b128(pr, 16 * tcg, so, 0));
+      ps[1] = f4(__builtin_amdgcn_raw_buffer_load_b128(qr, 16 * tcg, so, 0));
     }
   };
   // V = B^T d B for this thread's column: rows mixed in registers (B^T d), columns
-  // mixed across the quad: V[.][j] = sa*r[.][j] + sb*r[.][partner], partner = (2,2,1,1)[j],
-  // (sa, sb) = (1,-1), (1,1), (1,-1), (-1,1).
-  const float sa = tj == 3 ? -1.f : 1.f, sb = (tj == 0 || tj == 2) ? -1.f : 1.f;
+  // mixed across the quad: V[.][j] = sa*(r[.][j] + c*r[.][partner]), partner = (2,2,1,1)[j],
+  // c = (-1, 1, -1, -1)[j], sa = -1 for j = 3 only.  sa is folded into the filters (U of
+  // the b = 3 transform elements is stored negated), so each element is one fma whose
+  // DPP operand the compiler folds into v_fmac_f32_dpp.
+  const float cq = tj == 1 ? 1.f : -1.f;
   auto store_v = [&](const float4 (&d)[4], const float4 (&ps)[2], int buf) {
     float4 v[4];
 #pragma unroll
@@ -153,30 +160,32 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
     r[2] = v[2] - v[1];
     r[3] = v[1] - v[3];
     float* dst = lds + buf * VBUF + tj * VPLANE + tl * VROW + 4 * tcg;
+    auto mix = [&](float x) {
+      const float o = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x5A, 0xF, 0xF, true));
+      return __builtin_fmaf(o, cq, x);
+    };
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float4 o;
-      o.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[i].x), 0x5A, 0xF, 0xF, false));
-      o.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[i].y), 0x5A, 0xF, 0xF, false));
-      o.z = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[i].z), 0x5A, 0xF, 0xF, false));
-      o.w = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[i].w), 0x5A, 0xF, 0xF, false));
-      *reinterpret_cast<float4*>(dst + 4 * i * VPLANE) = sa * r[i] + sb * o;
-    }
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float4*>(dst + 4 * i * VPLANE) = make_float4(mix(r[i].x), mix(r[i].y), mix(r[i].z), mix(r[i].w));
   };
 
   // ---- GEMM role: wave wid owns xi = 2*wid + xl ----------------------------------------
   // U fragment (xi, 32-col block, K-step s, half q): 64 lanes x float4, contiguous 1 KiB.
   typedef float4 ufrag[2][NBW][2];
+  int ubase[2][NBW];
+#pragma unroll
+  for (int xl = 0; xl < 2; ++xl)
+#pragma unroll
+    for (int b = 0; b < NBW; ++b) ubase[xl][b] = (((2 * wid + xl) * NB32 + nb * NBW + b) * KS * 2 * 64 + lane) * 16;
   auto load_u = [&](ufrag& u, int s) {
+    const int so = min(s, KS - 1) * 2 * 64 * 16;
 #pragma unroll
     for (int xl = 0; xl < 2; ++xl)
 #pragma unroll
       for (int b = 0; b < NBW; ++b)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int idx = ((((2 * wid + xl) * NB32 + nb * NBW + b) * KS + s) * 2 + q) * 64 + lane;
-          u[xl][b][q] = f4(__builtin_amdgcn_raw_buffer_load_b128(ur, s < KS ? idx * 16 : OOB, 0, 0));
-        }
+        for (int q = 0; q < 2; ++q)
+          u[xl][b][q] = f4(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[xl][b] + q * 64 * 16, so, 0));
   };
 
   floatx16 acc[2][NBW];
@@ -361,7 +370,8 @@ __global__ void wino_weight_kernel(const float* __restrict__ w, float* __restric
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int xi = 4 * a + b;
-      u[((((long long)(xi * NB32 + nb32) * KS + s) * 2 + q) * 64 + ln) * 4 + e] = (float)ua[b];
+      // b = 3 stored negated: wino_kernel's input transform produces -V for that column
+      u[((((long long)(xi * NB32 + nb32) * KS + s) * 2 + q) * 64 + ln) * 4 + e] = (float)(b == 3 ? -ua[b] : ua[b]);
     }
   }
 }

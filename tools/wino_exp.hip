@@ -19,12 +19,13 @@
 //   * 8 waves; wave w owns xi = 2w, 2w+1 and the whole 32 x BN tile of both, so its
 //     accumulators are 2 x NBW 32x32 MFMA blocks (32*NBW VGPRs) and no operand it reads
 //     is read by any other wave.
-//   * K-step = 16 input channels.  Thread (tile = tid/16, ch = tid%16) loads the 4x4
-//     patch of its tile at its channel (buffer loads: OOB offset -> 0 = zero padding;
-//     the pre-BN affine is applied only to in-image taps), transforms it with 32 adds
-//     and writes the 16 V values to LDS V[xi][tile][ch] (rows of 20 floats: the
-//     ds_read_b128 fragment reads are conflict-free).  The transform is shared by all
-//     16 GEMMs, which is why the 16 live in one workgroup.
+//   * K-step = 16 input channels.  Thread (tile, channel group cg of 4, patch column j)
+//     loads its patch column as 4 x 16-B buffer loads (OOB offset -> 0 = zero padding;
+//     the pre-BN affine is applied only to in-image taps), mixes rows in registers and
+//     columns across its lane quad (DPP quad_perm), and writes 4 x float4 of V to LDS
+//     V[xi][tile][ch] (rows of 20 floats: the ds_read_b128 fragment reads are
+//     conflict-free; planes 648 floats apart: so are the ds_write_b128).  The transform is
+//     shared by all 16 GEMMs, which is why the 16 live in one workgroup.
 //   * U (transformed filters, built once per model by wino_weight_kernel) never
 //     touches LDS: it is pre-permuted in HBM into MFMA-fragment order, so each wave
 //     fetches its own B fragments with fully coalesced 1 KiB buffer loads.
@@ -43,7 +44,6 @@
 // j (0..7) multiplies channel 8h + j: lane (m, h) reads V[xi][m][8h .. 8h+7] with two
 // ds_read_b128 and the matching 8 U values with two 16-B loads.
 #include "frhip_kernels.h"
-#define launch_wino launch_wino_x
 
 namespace frhip {
 namespace {
@@ -54,7 +54,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int WT = 32;             // 2x2 output tiles per workgroup (MFMA M)
 constexpr int WKC = 16;            // input channels per K-step
 constexpr int VROW = 20;           // LDS floats per (xi, tile) row: 16 channels + 4 pad
-constexpr int VPLANE = WT * VROW;  // one xi plane
+constexpr int VPLANE = WT * VROW + 8;  // one xi plane; 648 = 8 mod 32: conflict-free b128 writes
 constexpr int VBUF = 16 * VPLANE;  // one K-step of V (40 KiB)
 constexpr int MROW = 33;           // epilogue staging row: 32 couts + 1
 constexpr int MPLANE = WT * MROW;
@@ -65,6 +65,17 @@ __device__ __forceinline__ int wino_xcd_remap(int bid, int n) {
   const int xcd = bid & 7, loc = bid >> 3;
   const int q = n >> 3, r = n & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// Buffer descriptor from provably wave-uniform inputs (readfirstlane), so the compiler
+// keeps it in SGPRs instead of wrapping every buffer op in a waterfall loop.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* ptr, int bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(ptr);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, n,
+                                           0x00020000);
 }
 
 template <int NBW, bool PRE, int EPI, int MODE>
@@ -83,87 +94,98 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
   const int KS = Cin / WKC;
   const int NB32 = p.Cout / 32;
 
-  // ---- transform role: one (tile, channel) per thread --------------------------------
-  const int tl = tid >> 4, tc = tid & 15;
+  // ---- transform role: thread (tile, channel group of 4, patch column j) ------------
+  // lane = j + 4*cg + 16*tile_in_wave: a quad holds the 4 columns of one (tile, cg), so
+  // the column half of the transform is a DPP quad exchange.
+  const int tj = tid & 3, tcg = (tid >> 2) & 3, tl = tid >> 4;
   const int T = mb * WT + tl;
   int base = 0;
-  unsigned mask = 0;
+  unsigned mask = 0;  // bit i: patch pixel (row i, column tj) is inside the image
   if (T < p.ntiles) {
     const int n = T / per_img;
     const int r = T - n * per_img;
     const int ty = r / p.TW, tx = r - ty * p.TW;
-    const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+    const int y0 = 2 * ty - 1, x = 2 * tx - 1 + tj;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if ((unsigned)(y0 + i) < (unsigned)H && (unsigned)(x0 + j) < (unsigned)W) mask |= 1u << (4 * i + j);
-    base = (((n * H + y0) * W + x0) * Cin + tc) * 4;  // only used at in-image taps
+      if ((unsigned)(y0 + i) < (unsigned)H && (unsigned)x < (unsigned)W) mask |= 1u << i;
+    base = (((n * H + y0) * W + x) * Cin + 4 * tcg) * 4;  // only used at in-image taps
   }
-  const int rowb = W * Cin * 4, colb = Cin * 4;
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.B * H * W * Cin * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ur =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, 16 * p.Cout * Cin * 4, 0x00020000);
+  const int rowb = W * Cin * 4;
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
+  const __amdgpu_buffer_rsrc_t ur = uniform_rsrc(p.u, 16 * p.Cout * Cin * 4);
+  auto f4 = [](u32x4 v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+  };
 
-  auto load_in = [&](float (&d)[16], float (&ps)[2], int s) {
-    const unsigned m = s < KS ? mask : 0u;
-    const int off = base + s * WKC * 4;
+  // per-lane offsets fixed for the whole K loop (OOB for out-of-image pixels); the K-step
+  // enters as a scalar soffset.  Prefetches past the last step re-load the last step
+  // (clamped), so no lane ever needs a per-step range select.
+  int voff[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) voff[i] = ((mask >> i) & 1u) ? base + i * rowb : OOB;
+  const __amdgpu_buffer_rsrc_t pr = uniform_rsrc(p.pre_scale, PRE ? Cin * 4 : 0);
+  const __amdgpu_buffer_rsrc_t qr = uniform_rsrc(p.pre_shift, PRE ? Cin * 4 : 0);
+  auto load_in = [&](float4 (&d)[4], float4 (&ps)[2], int s) {
+    const int so = min(s, KS - 1) * WKC * 4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bool ok = (m >> (4 * i + j)) & 1u;
-        d[4 * i + j] =
-            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ok ? off + i * rowb + j * colb : OOB, 0, 0));
-      }
+    for (int i = 0; i < 4; ++i) d[i] = f4(__builtin_amdgcn_raw_buffer_load_b128(xr, voff[i], so, 0));
     if constexpr (PRE) {
-      const int c = min(s, KS - 1) * WKC + tc;
-      ps[0] = p.pre_scale[c];
-      ps[1] = p.pre_shift[c];
+      ps[0] = f4(__builtin_amdgcn_raw_buffer_load_b128(pr, 16 * tcg, so, 0));
+      ps[1] = f4(__builtin_amdgcn_raw_buffer_load_b128(qr, 16 * tcg, so, 0));
     }
   };
-  auto store_v = [&](const float (&d)[16], const float (&ps)[2], int buf) {
-    float v[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      v[e] = d[e];
-      if constexpr (PRE) v[e] = ((mask >> e) & 1u) ? v[e] * ps[0] + ps[1] : 0.f;
-    }
-    float m[16];
-    // B^T d (rows), then (.) B (columns)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      m[0 + j] = v[0 + j] - v[8 + j];
-      m[4 + j] = v[4 + j] + v[8 + j];
-      m[8 + j] = v[8 + j] - v[4 + j];
-      m[12 + j] = v[4 + j] - v[12 + j];
-    }
-    float* dst = lds + buf * VBUF + tl * VROW + tc;
+  // V = B^T d B for this thread's column: rows mixed in registers (B^T d), columns
+  // mixed across the quad: V[.][j] = sa*(r[.][j] + c*r[.][partner]), partner = (2,2,1,1)[j],
+  // c = (-1, 1, -1, -1)[j], sa = -1 for j = 3 only.  sa is folded into the filters (U of
+  // the b = 3 transform elements is stored negated), so each element is one fma whose
+  // DPP operand the compiler folds into v_fmac_f32_dpp.
+  const float cq = tj == 1 ? 1.f : -1.f;
+  auto store_v = [&](const float4 (&d)[4], const float4 (&ps)[2], int buf) {
+    float4 v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      dst[(4 * i + 0) * VPLANE] = m[4 * i + 0] - m[4 * i + 2];
-      dst[(4 * i + 1) * VPLANE] = m[4 * i + 1] + m[4 * i + 2];
-      dst[(4 * i + 2) * VPLANE] = m[4 * i + 2] - m[4 * i + 1];
-      dst[(4 * i + 3) * VPLANE] = m[4 * i + 1] - m[4 * i + 3];
+      v[i] = d[i];
+      if constexpr (PRE) {
+        const bool ok = (mask >> i) & 1u;
+        v[i].x = ok ? v[i].x * ps[0].x + ps[1].x : 0.f;
+        v[i].y = ok ? v[i].y * ps[0].y + ps[1].y : 0.f;
+        v[i].z = ok ? v[i].z * ps[0].z + ps[1].z : 0.f;
+        v[i].w = ok ? v[i].w * ps[0].w + ps[1].w : 0.f;
+      }
     }
+    float4 r[4];
+    r[0] = v[0] - v[2];
+    r[1] = v[1] + v[2];
+    r[2] = v[2] - v[1];
+    r[3] = v[1] - v[3];
+    float* dst = lds + buf * VBUF + tj * VPLANE + tl * VROW + 4 * tcg;
+    auto mix = [&](float x) {
+      const float o = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x5A, 0xF, 0xF, true));
+      return __builtin_fmaf(o, cq, x);
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float4*>(dst + 4 * i * VPLANE) = make_float4(mix(r[i].x), mix(r[i].y), mix(r[i].z), mix(r[i].w));
   };
 
   // ---- GEMM role: wave wid owns xi = 2*wid + xl ----------------------------------------
   // U fragment (xi, 32-col block, K-step s, half q): 64 lanes x float4, contiguous 1 KiB.
   typedef float4 ufrag[2][NBW][2];
+  int ubase[2][NBW];
+#pragma unroll
+  for (int xl = 0; xl < 2; ++xl)
+#pragma unroll
+    for (int b = 0; b < NBW; ++b) ubase[xl][b] = (((2 * wid + xl) * NB32 + nb * NBW + b) * KS * 2 * 64 + lane) * 16;
   auto load_u = [&](ufrag& u, int s) {
+    const int so = min(s, KS - 1) * 2 * 64 * 16;
 #pragma unroll
     for (int xl = 0; xl < 2; ++xl)
 #pragma unroll
       for (int b = 0; b < NBW; ++b)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int idx = ((((2 * wid + xl) * NB32 + nb * NBW + b) * KS + s) * 2 + q) * 64 + lane;
-          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ur, s < KS ? idx * 16 : OOB, 0, 0);
-          u[xl][b][q] =
-              make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-        }
+        for (int q = 0; q < 2; ++q)
+          u[xl][b][q] = f4(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[xl][b] + q * 64 * 16, so, 0));
   };
 
   floatx16 acc[2][NBW];
@@ -178,10 +200,12 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
   // ago), U(s) in `uc`.  Issues the loads of patch s+2 (into `dn`, free since V(s) was
   // written) and U(s+1), runs the MFMAs of s and, in their shadow, transforms patch s+1
   // into the other LDS buffer; one barrier.
-  auto step = [&](int s, const ufrag& uc, ufrag& un, const float (&dc)[16], const float (&pc)[2],
-                  float (&dn)[16], float (&pn)[2], int buf) {
-    if constexpr (MODE & 1) load_in(dn, pn, s + 2);
+  auto step = [&](int s, const ufrag& uc, ufrag& un, const float4 (&dc)[4], const float4 (&pc)[2],
+                  float4 (&dn)[4], float4 (&pn)[2], int buf) {
+    // U(s+1) first: vmcnt retires in issue order, so the wait for U at the top of the next
+    // step must not also wait for this step's patch loads (which may come from HBM)
     if constexpr (MODE & 2) load_u(un, s + 1);
+    if constexpr (MODE & 1) load_in(dn, pn, s + 2);
     const float* vb = lds + buf * VBUF + (lane & 31) * VROW + 8 * (lane >> 5);
     float4 a[2][2];
 #pragma unroll
@@ -202,11 +226,11 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
     // 4 fragment reads up front; then per MFMA: a share of the loads, of the transform
     // VALU and (in the second half) of its 16 LDS writes
     constexpr int NMFMA = 16 * NBW;
-    constexpr int NVMEM = 16 + 4 * NBW + (PRE ? 2 : 0);
+    constexpr int NVMEM = 4 + 4 * NBW + (PRE ? 2 : 0);
     constexpr int VM_PER = (NVMEM + NMFMA - 1) / NMFMA;
-    constexpr int VALU_PER = PRE ? 6 : 4;
+    constexpr int VALU_PER = PRE ? 8 : 4;
     constexpr int DSW_FROM = NMFMA / 2;
-    constexpr int DSW_PER = (16 + (NMFMA - DSW_FROM) - 1) / (NMFMA - DSW_FROM);
+    constexpr int DSW_PER = (4 + (NMFMA - DSW_FROM) - 1) / (NMFMA - DSW_FROM);
     __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
     for (int i = 0; i < NMFMA; ++i) {
@@ -216,9 +240,12 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
       if (i >= DSW_FROM) __builtin_amdgcn_sched_group_barrier(0x200, DSW_PER, 0);
     }
     __syncthreads();
+    // nothing crosses a step boundary: VALU of the next step hoisted above the barrier
+    // would wait on loads issued in this one
+    __builtin_amdgcn_sched_barrier(0);
   };
 
-  float dA[16], dB[16], pA[2] = {1.f, 0.f}, pB[2] = {1.f, 0.f};
+  float4 dA[4], dB[4], pA[2], pB[2];
   ufrag uA, uB;
   load_in(dA, pA, 0);
   load_u(uA, 0);
@@ -236,8 +263,7 @@ __global__ __launch_bounds__(512, 1) void wino_kernel(WinoParams p) {
   // residuals are loaded before the staging barrier so their latency overlaps it
   int pix[2], okm[2];
   float rv[NBW][2][4];
-  const __amdgpu_buffer_rsrc_t rr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.res, (short)0, RES ? p.B * H * W * p.Cout * 4 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, RES ? p.B * H * W * p.Cout * 4 : 0);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int Tq = mb * WT + (tid >> 5) + 16 * q;
@@ -344,14 +370,14 @@ __global__ void wino_weight_kernel(const float* __restrict__ w, float* __restric
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int xi = 4 * a + b;
-      u[((((long long)(xi * NB32 + nb32) * KS + s) * 2 + q) * 64 + ln) * 4 + e] = (float)ua[b];
+      // b = 3 stored negated: wino_kernel's input transform produces -V for that column
+      u[((((long long)(xi * NB32 + nb32) * KS + s) * 2 + q) * 64 + ln) * 4 + e] = (float)(b == 3 ? -ua[b] : ua[b]);
     }
   }
 }
 
 }  // namespace
 }  // namespace frhip
-
 #include <cstdio>
 #include <cstdlib>
 using namespace frhip;
