@@ -15,9 +15,9 @@ step() {
 STEPS=${STEPS:-"kernels pipeline bench"}
 for s in $STEPS; do
   case $s in
-    kernels)  step kernels 900 python -m pytest tests/test_gpu_kernels.py -q -rfE; rc=$? ;;
-    pipeline) step pipeline 1200 python -m pytest tests/test_gpu_pipeline.py -q -rfE; rc=$? ;;
-    allgpu)   step allgpu 1500 python -m pytest tests -m gpu -q -rfE; rc=$? ;;
+    kernels)  step kernels 900 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -rfE; rc=$? ;;
+    pipeline) step pipeline 1200 python -u -m pytest tests/test_gpu_pipeline.py -x -v --timeout 120 --timeout-method thread -rfE; rc=$? ;;
+    allgpu)   step allgpu 1500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -rfE; rc=$? ;;
     sweep)    step sweep 900 python tools/conv_sweep.py --json gpurun_out/sweep.json; rc=$? ;;
     smoke)    step smoke 600 python -c "import __graft_entry__ as g; g.smoke()"; rc=$? ;;
     bench)    step bench 900 python bench.py ${BENCH_ARGS:-}; rc=$? ;;
