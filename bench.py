@@ -9,10 +9,11 @@ the gallery and broadcasts it over RCCL (the path's only exchange step); each
 rank then processes its own probes independently (weak scaling).
 
 Also reported:
-  roofline      conv_mfma kernel family (every 3x3 / 1x1 conv and the FC, >99%
-                of the path's FLOPs): algorithmic FLOP / summed HIP-event time
-                of those launches inside the timed region, vs the 157.3 TF
-                dense fp32 MFMA peak.
+  roofline      the dominant conv kernel (wino_kernel for the stride-1 3x3 convs
+                under the f32 default): algorithmic (direct-conv) FLOP / summed
+                HIP-event time of its launches inside the timed region, vs the
+                157.3 TF dense fp32 MFMA peak; executed_* counts the MFMA work
+                Winograd actually performs.
   cpu_baseline  the oracle (PyTorch-CPU IR-101 + reference-style per-probe
                 search) on rank 0's host cores, on a bounded sample.
 """
@@ -56,6 +57,8 @@ def parse():
     ap.add_argument("--topk", type=int, default=5)
     ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32",
                     help="conv arithmetic: exact f32 MFMA (default, parity path) or opt-in split bf16x3")
+    ap.add_argument("--conv-algorithm", choices=["winograd4", "winograd", "direct"], default="winograd",
+                    help="stride-1 3x3 convs: Winograd F(4x4,3x3), F(2x2,3x3) or the direct implicit GEMM (all f32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=None,
@@ -138,7 +141,7 @@ def main():
     from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
     sd = W.synthetic_state_dict(args.arch, model_type=args.model_type)
     emb = FaceEmbedder(architecture=args.arch, model_type=args.model_type, state_dict=sd, device=dev, max_batch=args.batch,
-                       precision=args.precision)
+                       precision=args.precision, conv_algorithm=args.conv_algorithm)
 
     # gallery: rank 0 embeds min(G, 1000) synthetic gallery crops on its GPU and grows them to G
     # rows as normalize(e + 0.0214 z); RCCL broadcast to the other ranks
@@ -224,10 +227,16 @@ def main():
 
     if rank == 0:
         faces = world * args.batch * args.steps
+        # dominant kernel = the conv family with the most time in the timed region (HIP events on the
+        # launch stream): the Winograd kernel for the f32 default, the direct implicit-GEMM one otherwise
+        fams = {f: prof[f] for f in ("winograd", "direct") if prof[f]["launches"]}
+        dom = max(fams, key=lambda f: fams[f]["ms"])
+        kp = fams[dom]
+        alg_tflops = kp["flop"] / (kp["ms"] * 1e-3) / 1e12
+        exec_tflops = kp["exec_flop"] / (kp["ms"] * 1e-3) / 1e12
         conv_tflops = prof["conv_flop"] / (prof["conv_ms"] * 1e-3) / 1e12 if prof["conv_ms"] > 0 else 0.0
-        per_launch_flop = prof["conv_flop"] / max(prof["conv_launches"], 1)
-        # bf16x3 executes 3 bf16 MFMA products per algorithmic f32 product: frac against the
-        # dense bf16 MFMA peak counts the executed work (achieved stays algorithmic)
+        # bf16x3 executes 3 bf16 MFMA products per algorithmic f32 product: its executed fraction is
+        # taken against the dense bf16 MFMA peak
         peak, mult = (FP32_MFMA_PEAK_TFLOPS, 1.0) if args.precision == "fp32" else (BF16_MFMA_PEAK_TFLOPS, 3.0)
         traffic, traffic_src, alg_bytes = None, None, None
         tj = args.traffic_json
@@ -239,9 +248,39 @@ def main():
                 and G == 1000 and args.precision == "fp32"):
             with open(tj) as f:
                 pj = json.load(f)
-            traffic = pj.get("hbm_bytes_per_conv_launch")
-            alg_bytes = pj.get("alg_bytes_per_conv_launch")
-            traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
+            kj = pj.get("kernels", {}).get(dom, {})
+            traffic = kj.get("hbm_bytes_per_launch")
+            alg_bytes = kj.get("alg_bytes_per_launch")
+            if traffic is not None:
+                traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
+        kernel_name = {"winograd": ("wino4_kernel (Winograd F(4x4,3x3) f32, every stride-1 3x3 conv)"
+                                    if args.conv_algorithm == "winograd4" else
+                                    "wino_kernel (Winograd F(2x2,3x3) f32, every stride-1 3x3 conv)"),
+                       "direct": "conv_mfma_kernel (implicit-GEMM; every conv/FC launch in this mode)"}[dom]
+        roofline = {"bound": "mfma", "kernel": kernel_name,
+                    "achieved": round(alg_tflops, 3), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(alg_tflops * mult / peak, 4) if dom == "direct" else round(alg_tflops / peak, 4),
+                    "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_launch": alg_bytes,
+                    "launches": kp["launches"], "flop_per_launch": kp["flop"] / kp["launches"],
+                    "avg_launch_ms": round(kp["ms"] / kp["launches"], 5),
+                    "share_of_step": round(kp["ms"] / max(prof["total_ms"], 1e-9), 4)}
+        if dom == "winograd":
+            # achieved counts direct-conv FLOPs (the algorithmic work); Winograd performs
+            # 16 of every 36 products, so the MFMA pipe itself runs at executed_tflops
+            roofline["executed_tflops"] = round(exec_tflops, 3)
+            roofline["executed_frac"] = round(exec_tflops / peak, 4)
+            roofline["note"] = ("achieved/frac count direct-conv-equivalent FLOPs; Winograd executes "
+                                + ("36/144 (F(4x4,3x3), plus canvas padding)" if args.conv_algorithm == "winograd4"
+                                   else "16/36 (F(2x2,3x3))")
+                                + " of them on the MFMA pipe (executed_*), so frac can exceed 1")
+        if "direct" in fams and dom != "direct":
+            d = fams["direct"]
+            roofline["other_conv_kernel"] = {"kernel": "conv_mfma_kernel (stride-2 / 1x1 convs, FC, gallery scores)",
+                                             "tflops": round(d["flop"] / (d["ms"] * 1e-3) / 1e12, 3),
+                                             "frac": round(d["flop"] / (d["ms"] * 1e-3) / 1e12 / peak, 4),
+                                             "launches": d["launches"],
+                                             "share_of_step": round(d["ms"] / max(prof["total_ms"], 1e-9), 4)}
+        roofline["conv_family_tflops"] = round(conv_tflops, 3)
         out = {
             "metric": METRIC if args.config == "c3" and args.model_type == "adaface" else (
                 f"faces/sec detect+align+quality+embed+match from 1080p frames (IR-101, gallery={G})"
@@ -280,13 +319,7 @@ def main():
             "flop_per_face": flop_per_face(args.arch, G, args.model_type),
             "path_tflops": round(faces / tmax * flop_per_face(args.arch, G, args.model_type) / 1e12, 2),
             "top1_self_match": top1_ok,
-            "roofline": {"bound": "mfma", "kernel": "conv_mfma_kernel (all conv/FC launches)",
-                         "achieved": round(conv_tflops, 3), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(conv_tflops * mult / peak, 4), "traffic": traffic,
-                         "traffic_source": traffic_src, "alg_bytes_per_launch": alg_bytes,
-                         "launches": prof["conv_launches"], "flop_per_launch": per_launch_flop,
-                         "avg_launch_ms": round(prof["conv_ms"] / max(prof["conv_launches"], 1), 5),
-                         "conv_share_of_step": round(prof["conv_ms"] / max(prof["total_ms"], 1e-9), 4)},
+            "roofline": roofline,
         }
         if world == 1 and not args.no_cpu_baseline and args.model_type == "adaface":
             sample = W.probe_crops(gal_crops, 1024, seed=W.CROP_SEED_PROBE)

@@ -49,6 +49,8 @@ _SIGNATURES = {
     "fr_set_precision": (_I, [_P, _I]),
     "fr_set_conv_algorithm": (_I, [_P, _I]),
     "fr_profile_enable": (_I, [_P, _I]),
+    "fr_profile_kernel": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "fr_profile_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "fr_last_error": (ctypes.c_char_p, [_P]),
@@ -245,7 +247,7 @@ class Handle:
         check(self._lib.fr_set_precision(self.h, modes[mode]), self.h)
 
     def set_conv_algorithm(self, algo: str) -> None:
-        algos = {"direct": 0, "winograd": 1}
+        algos = {"direct": 0, "winograd": 1, "winograd4": 2}
         if algo not in algos:
             raise ValueError(f"conv_algorithm must be one of {sorted(algos)}")
         check(self._lib.fr_set_conv_algorithm(self.h, algos[algo]), self.h)
@@ -259,4 +261,11 @@ class Handle:
         cn = ctypes.c_int64()
         check(self._lib.fr_profile_read(self.h, ctypes.byref(cms), ctypes.byref(cfl), ctypes.byref(cn),
                                         ctypes.byref(tms)), self.h)
-        return {"conv_ms": cms.value, "conv_flop": cfl.value, "conv_launches": cn.value, "total_ms": tms.value}
+        out = {"conv_ms": cms.value, "conv_flop": cfl.value, "conv_launches": cn.value, "total_ms": tms.value}
+        for kind, name in ((0, "other"), (1, "direct"), (2, "winograd")):
+            ms, fl, ex = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            n = ctypes.c_int64()
+            check(self._lib.fr_profile_kernel(self.h, kind, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(ex),
+                                              ctypes.byref(n)), self.h)
+            out[name] = {"ms": ms.value, "flop": fl.value, "exec_flop": ex.value, "launches": n.value}
+        return out

@@ -1,0 +1,413 @@
+// Winograd F(4x4, 3x3) convolution in f32 on gfx950 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces the stride-1 3x3 Conv2d of net.BasicBlockIR (res_layer[1] and the stride-1
+// res_layer[4]; reached through `self.model(batch)`, face_embedder.py:157) with the same
+// fused pre-BN / post-BN / PReLU / residual epilogues as the direct and F(2x2) kernels.
+// The arithmetic stays f32 throughout.  Per 4x4 output tile and (cin, cout) pair the
+// algorithm does 36 products instead of 144 (F(2x2): 64), so the MFMA work drops 4x:
+//
+//   Y = A^T [ (G g G^T) (.) (B^T d B) ] A     d: 6x6 input patch, g: 3x3 filter
+//   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+//   G   = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1]
+//   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
+// (Lavin & Gray 2016, points 0, +-1, +-2, inf).  Simulated on the IR-101 oracle in f32 the
+// embeddings stay within 5e-7 of direct convolution.
+//
+// Tiles live on a "canvas": images laid out NC per canvas row with a period of P rows /
+// columns.  P = H when 4 | H (every tile inside one image); otherwise P = H + 1 -- one zero
+// separator row/column between neighbouring images is all a 3x3 pad-1 conv needs, so a 4x4
+// tile may straddle two images and 14x14 images waste 15²/14² instead of 16²/14² of the
+// products.  Patch pixels on a separator or outside the canvas load as 0.
+//
+// Per transform element xi = 6a + b (36 of them) the layer is one GEMM
+//   M_xi[tile][cout] = sum_cin V_xi[tile][cin] * U_xi[cin][cout]
+// and one workgroup owns WT = 32 tiles x 32 couts for all 36.
+//   * 4 waves, one per SIMD (512 registers each); wave w owns xi = 9w .. 9w+8, so its
+//     accumulators are 9 32x32 MFMA blocks and no operand it reads is read by another wave.
+//   * K-step = 16 input channels.  Thread (tile, channel pair) loads its 6x6 patch as 36
+//     8-byte buffer loads (OOB offset -> 0 = zero padding; the pre-BN affine only at
+//     in-image taps), transforms it in registers and writes 36 float2 of V to LDS
+//     V[xi][tile][16 ch], rows XOR-swizzled by 16-B slot so that the ds_read_b128 fragment
+//     reads and the ds_write_b64 stores are both conflict-free.
+//   * U (transformed filters, built once per model by wino4_weight_kernel) never touches
+//     LDS: it is stored in MFMA-fragment order, so each wave fetches its B fragments with
+//     fully coalesced 1 KiB buffer loads, one K-step ahead.
+//   * One barrier per K-step: the patch of step s+1 is loaded at the top of step s and
+//     transformed into the other LDS buffer in the shadow of step s's 72 MFMAs.
+//   * Epilogue: accumulators go through LDS as M[xi][tile][cout] (the whole 144 KiB), each
+//     thread inverse-transforms 4 (tile, cout) pairs and applies BN (+PReLU | + residual)
+//     at the in-image pixels of each tile.
+//
+// Lane map of 32x32x2 MFMA: A operand lane (m = l%32, h = l/32) = A[m][k=h], B operand
+// lane (n = l%32, h) = B[k=h][n].  MFMA j (0..7) of a K-step multiplies channel 8h + j:
+// lane (m, h) reads V[xi][m][8h .. 8h+7] with two ds_read_b128 and the matching 8 U values
+// with two 16-B loads (the fragment layout of the F(2x2) kernel, conv_winograd.hip).
+#include "frhip_kernels.h"
+
+namespace frhip {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NXI = 36;              // transform elements
+constexpr int WT = 32;               // 4x4 output tiles per workgroup (MFMA M)
+constexpr int KC = 16;               // input channels per K-step
+constexpr int XPW = 9;               // transform elements per wave
+constexpr int VPLANE = WT * KC;      // one xi plane of V: 512 floats
+constexpr int VBUF = NXI * VPLANE;   // one K-step of V: 18432 floats (72 KiB)
+constexpr int MPLANE = WT * 32;      // epilogue: one xi plane of M[tile][cout]
+constexpr int OOB = 0x80000000;      // buffer offset past any range: loads return 0
+static_assert(NXI * MPLANE <= 2 * VBUF, "epilogue staging must fit the V buffers");
+
+__device__ __forceinline__ int wino4_xcd_remap(int bid, int n) {
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q = n >> 3, r = n & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc4(const void* ptr, int bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(ptr);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, n,
+                                           0x00020000);
+}
+
+// Canvas coordinate v (a row or a column) of a tile whose origin lies in image slot `base`:
+// returns the in-image coordinate and sets `slot` (base or base + 1), or -1 for padding.
+__device__ __forceinline__ int canvas_coord(int v, int base, int P, int H, bool sep, int& slot) {
+  const int y = v - base * P;
+  slot = base;
+  if (y >= 0 && y < H) return y;
+  if (sep && y >= P && y - P < H) {
+    slot = base + 1;
+    return y - P;
+  }
+  return -1;
+}
+
+// 1-D input transform B^T d (6 -> 6)
+__device__ __forceinline__ void bt6(const f2 (&d)[6], f2 (&t)[6]) {
+  const f2 s1 = d[3] + d[4], s2 = d[1] + d[2];
+  const f2 s3 = d[4] - d[3], s4 = d[1] - d[2];
+  const f2 s5 = d[4] - d[2], s6 = d[3] - d[1];
+  t[0] = 4.f * d[0] - 5.f * d[2] + d[4];
+  t[1] = s1 - 4.f * s2;
+  t[2] = s3 + 4.f * s4;
+  t[3] = s5 + 2.f * s6;
+  t[4] = s5 - 2.f * s6;
+  t[5] = 4.f * d[1] - 5.f * d[3] + d[5];
+}
+
+// 1-D output transform A^T m (6 -> 4)
+__device__ __forceinline__ void at6(const float (&m)[6], float (&o)[4]) {
+  const float p12 = m[1] + m[2], m12 = m[1] - m[2];
+  const float p34 = m[3] + m[4], m34 = m[3] - m[4];
+  o[0] = m[0] + p12 + p34;
+  o[1] = m12 + 2.f * m34;
+  o[2] = p12 + 4.f * p34;
+  o[3] = m12 + 8.f * m34 + m[5];
+}
+
+template <bool PRE, int EPI>
+__global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * VBUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int t = wino4_xcd_remap(blockIdx.x, p.mblocks * p.nblocks);
+  const int mb = t % p.mblocks, nb = t / p.mblocks;
+  const int H = p.H, W = p.W, Cin = p.Cin;
+  const int KS = Cin / KC;
+  const int NB32 = p.Cout / 32;
+  const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
+
+  // ---- transform role: thread (tile tl, channel pair cp) ------------------------------
+  const int tl = tid >> 3, cp = tid & 7;
+  int off[6][6];
+  unsigned long long vmask = 0;  // bit 6i+j: patch pixel (i, j) is inside an image
+  {
+    const int T = mb * WT + tl;
+    const int tr = T / p.TWc, tc = T - tr * p.TWc;
+    const int R0 = 4 * tr - 1, C0 = 4 * tc - 1;
+    const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
+    int rp[6], cpx[6];
+    unsigned rv = 0, cv = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      int slot;
+      const int y = canvas_coord(R0 + i, ir0, p.Pr, H, sep_r, slot);
+      rp[i] = (slot * p.NC * H + y) * W;
+      if (y >= 0 && T < p.ntiles) rv |= 1u << i;
+      const int x = canvas_coord(C0 + i, ic0, p.Pc, W, sep_c, slot);
+      cpx[i] = slot * H * W + x;
+      if (x >= 0 && slot < p.NC) cv |= 1u << i;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const bool ok = ((rv >> i) & 1u) && ((cv >> j) & 1u);
+        off[i][j] = ok ? ((rp[i] + cpx[j]) * Cin + 2 * cp) * 4 : OOB;
+        if (ok) vmask |= 1ull << (6 * i + j);
+      }
+  }
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc4(p.x, p.B * H * W * Cin * 4);
+  const __amdgpu_buffer_rsrc_t ur = uniform_rsrc4(p.u, NXI * p.Cout * Cin * 4);
+  const __amdgpu_buffer_rsrc_t pr = uniform_rsrc4(p.pre_scale, PRE ? Cin * 4 : 0);
+  const __amdgpu_buffer_rsrc_t qr = uniform_rsrc4(p.pre_shift, PRE ? Cin * 4 : 0);
+  auto f2u = [](u32x2 v) { return f2{__uint_as_float(v.x), __uint_as_float(v.y)}; };
+  auto f4u = [](u32x4 v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+  };
+
+  f2 d[6][6];
+  f2 psc, psh;
+  auto load_patch = [&](int s) {
+    const int so = min(s, KS - 1) * KC * 4;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) d[i][j] = f2u(__builtin_amdgcn_raw_buffer_load_b64(xr, off[i][j], so, 0));
+    if constexpr (PRE) {
+      psc = f2u(__builtin_amdgcn_raw_buffer_load_b64(pr, 8 * cp, so, 0));
+      psh = f2u(__builtin_amdgcn_raw_buffer_load_b64(qr, 8 * cp, so, 0));
+    }
+  };
+  // physical float offset of this thread's channel pair inside its V row (16-B slot XOR)
+  const int vslot = (((cp >> 1) ^ ((tl >> 2) & 3)) << 2) + ((cp & 1) << 1);
+  auto store_v = [&](int buf) {
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const bool ok = (vmask >> (6 * i + j)) & 1ull;
+          const f2 v = d[i][j] * psc + psh;
+          d[i][j] = ok ? v : f2{0.f, 0.f};
+        }
+    }
+    f2 tcol[6][6];  // tcol[a][j] = (B^T d)[a][j]
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      f2 c[6], o[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) c[i] = d[i][j];
+      bt6(c, o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) tcol[a][j] = o[a];
+    }
+    float* dst = lds + buf * VBUF + tl * KC + vslot;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      f2 v[6];
+      bt6(tcol[a], v);
+#pragma unroll
+      for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(dst + (6 * a + b) * VPLANE) = v[b];
+    }
+  };
+
+  // ---- GEMM role: wave wid owns xi = 9*wid + x ------------------------------------------
+  int ubase[XPW];
+#pragma unroll
+  for (int x = 0; x < XPW; ++x) ubase[x] = ((((XPW * wid + x) * NB32 + nb) * KS) * 2 * 64 + lane) * 16;
+  float4 u[XPW][2];
+  auto load_u = [&](int x, int s) {
+    const int so = min(s, KS - 1) * 2 * 64 * 16;
+    u[x][0] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x], so, 0));
+    u[x][1] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x] + 64 * 16, so, 0));
+  };
+  const int m = lane & 31, h = lane >> 5;
+  const int rq = (m >> 2) & 3;
+  const float* vrd0 = lds + m * KC + (((2 * h) ^ rq) << 2);
+  const float* vrd1 = lds + m * KC + (((2 * h + 1) ^ rq) << 2);
+
+  floatx16 acc[XPW];
+#pragma unroll
+  for (int x = 0; x < XPW; ++x)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[x][e] = 0.f;
+
+  load_patch(0);
+#pragma unroll
+  for (int x = 0; x < XPW; ++x) load_u(x, 0);
+  store_v(0);
+  __syncthreads();
+
+  for (int s = 0; s < KS; ++s) {
+    const int buf = s & 1;
+    load_patch(s + 1);
+#pragma unroll
+    for (int x = 0; x < XPW; ++x) {
+      const int xo = buf * VBUF + (XPW * wid + x) * VPLANE;
+      const float4 a0 = *reinterpret_cast<const float4*>(vrd0 + xo);
+      const float4 a1 = *reinterpret_cast<const float4*>(vrd1 + xo);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bv[8] = {u[x][0].x, u[x][0].y, u[x][0].z, u[x][0].w, u[x][1].x, u[x][1].y, u[x][1].z, u[x][1].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc[x], 0, 0, 0);
+      load_u(x, s + 1);
+    }
+    store_v(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: inverse transform + BN (+PReLU | +residual) -------------------------
+#pragma unroll
+  for (int x = 0; x < XPW; ++x) {
+    float* dst = lds + (XPW * wid + x) * MPLANE + m;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2) + 4 * h) * 32] = acc[x][r];
+  }
+  __syncthreads();
+  const int ec = tid & 31;
+  const int cout = nb * 32 + ec;
+  const float sc = p.post_scale[cout], sh = p.post_shift[cout];
+  float al = 0.f;
+  if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) al = p.prelu[cout];
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q) {
+    const int tile = (tid >> 5) + 8 * q;
+    const int T = mb * WT + tile;
+    if (T >= p.ntiles) continue;
+    const int tr = T / p.TWc, tc = T - tr * p.TWc;
+    const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
+    int orow[4], ocol[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int slot;
+      const int y = canvas_coord(4 * tr + i, ir0, p.Pr, H, sep_r, slot);
+      const int nimg = slot * p.NC;
+      orow[i] = (y >= 0 && nimg < p.B) ? (nimg * H + y) * W : -1;
+      const int xx = canvas_coord(4 * tc + i, ic0, p.Pc, W, sep_c, slot);
+      ocol[i] = (xx >= 0 && slot < p.NC) ? slot * H * W + xx : -1;
+    }
+    float mv[6][6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b < 6; ++b) mv[a][b] = lds[(6 * a + b) * MPLANE + tile * 32 + ec];
+    float z[6][4];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) at6(mv[a], z[a]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float col[6], o[4];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) col[a] = z[a][c];
+      at6(col, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (orow[r] < 0 || ocol[c] < 0) continue;
+        const int pix = orow[r] + ocol[c];
+        if (pix >= p.B * H * W) continue;
+        const long long oo = (long long)pix * p.Cout + cout;
+        float v = o[r] * sc + sh;
+        if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
+        if constexpr (EPI == EPI_AFFINE_RES) v += p.res[oo];
+        if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
+          v += p.res[oo];
+          v = v > 0.f ? v : v * al;
+        }
+        p.y[oo] = v;
+      }
+    }
+  }
+}
+
+// G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into
+// the fragment order wino4_kernel reads: [xi][Cout/32][Cin/16][q][lane][4] with
+// lane = 32*(c/8) + cout%32, q = (c%8)/4, element = c%4 for c = cin%16.
+__global__ void wino4_weight_kernel(const float* __restrict__ w, float* __restrict__ u, int Cout, int Cin) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= Cout * Cin) return;
+  const int o = idx / Cin, i = idx - o * Cin;
+  const double G[6][3] = {{0.25, 0.0, 0.0},
+                          {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                          {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                          {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                          {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                          {0.0, 0.0, 1.0}};
+  double g[3][3];
+#pragma unroll
+  for (int y = 0; y < 3; ++y)
+#pragma unroll
+    for (int x = 0; x < 3; ++x) g[y][x] = w[((long long)(o * 3 + y) * 3 + x) * Cin + i];
+  double tg[6][3];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int x = 0; x < 3; ++x) tg[a][x] = G[a][0] * g[0][x] + G[a][1] * g[1][x] + G[a][2] * g[2][x];
+  const int NB32 = Cout / 32, KS = Cin / KC;
+  const int nb32 = o >> 5, n = o & 31;
+  const int s = i / KC, c = i % KC;
+  const int ln = 32 * (c >> 3) + n, q = (c & 7) >> 2, e = c & 3;
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const double v = tg[a][0] * G[b][0] + tg[a][1] * G[b][1] + tg[a][2] * G[b][2];
+      const int xi = 6 * a + b;
+      u[((((long long)(xi * NB32 + nb32) * KS + s) * 2 + q) * 64 + ln) * 4 + e] = (float)v;
+    }
+}
+
+}  // namespace
+
+bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
+  return kh == 3 && kw == 3 && stride == 1 && pad == 1 && Cin % KC == 0 && Cin >= KC && Cout % 32 == 0 && Cout >= 32;
+}
+
+size_t wino4_weight_floats(int Cout, int Cin) { return (size_t)NXI * Cout * Cin; }
+
+hipError_t launch_wino4_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s) {
+  if (Cout % 32 || Cin % KC) return hipErrorInvalidValue;
+  const int n = Cout * Cin;
+  hipLaunchKernelGGL(wino4_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, u, Cout, Cin);
+  return hipGetLastError();
+}
+
+// Canvas of a layer: P = H when 4 | H (tiles never straddle images), else P = H + 1 with NC
+// images per canvas row chosen so that the canvas width NC*P is a multiple of 4 (14 -> 4 x 15).
+void wino4_canvas(Wino4Params& p) {
+  auto period = [](int h) { return h % 4 == 0 ? h : h + 1; };
+  p.Pr = period(p.H);
+  p.Pc = period(p.W);
+  p.NC = 1;
+  if (p.Pc % 4) {
+    p.NC = (p.Pc % 2) ? 4 : 2;
+    if (p.NC > p.B) p.NC = p.B;
+  }
+  const int crow = (p.B + p.NC - 1) / p.NC;  // canvas rows of images
+  p.TWc = (p.NC * p.Pc + 3) / 4;
+  const int TRc = (crow * p.Pr + 3) / 4;
+  p.ntiles = TRc * p.TWc;
+}
+
+hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
+  Wino4Params p = p0;
+  if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
+      (long long)p.B * p.H * p.W * p.Cin * 4 >= (1ll << 31) ||
+      (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) || (long long)NXI * p.Cout * p.Cin * 4 >= (1ll << 31))
+    return hipErrorInvalidValue;
+  wino4_canvas(p);
+  p.mblocks = (p.ntiles + WT - 1) / WT;
+  p.nblocks = p.Cout / 32;
+  const dim3 grid(p.mblocks * p.nblocks), block(256);
+#define FR_WINO4_CASE(PRE_, EPI_)                                            \
+  if (pre == PRE_ && epi == EPI_) {                                          \
+    hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_>), grid, block, 0, s, p);    \
+    return hipGetLastError();                                                \
+  }
+  FR_WINO4_CASE(true, EPI_AFFINE_PRELU)
+  FR_WINO4_CASE(false, EPI_AFFINE_RES)
+#undef FR_WINO4_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace frhip

@@ -92,6 +92,29 @@ size_t wino_weight_floats(int Cout, int Cin);
 hipError_t launch_wino_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s);
 hipError_t launch_wino(const WinoParams& p, bool pre, Epi epi, hipStream_t s);
 
+// Winograd F(4x4,3x3) stride-1 pad-1 conv in f32 (conv_winograd4.hip), NHWC like ConvParams.
+//   u: transformed filters from launch_wino4_weights (wino4_weight_floats(Cout, Cin) floats).
+// Tiles are cut from a canvas of the batch (period Pr x Pc per image, NC images per canvas
+// row, one zero separator row/column when 4 does not divide H/W).
+struct Wino4Params {
+  const float* x;
+  const float* u;
+  float* y;
+  const float* pre_scale;
+  const float* pre_shift;
+  const float* post_scale;
+  const float* post_shift;
+  const float* prelu;
+  const float* res;  // same shape as y
+  int B, H, W, Cin, Cout;
+  int Pr, Pc, NC, TWc, ntiles, mblocks, nblocks;  // set by launch_wino4 (wino4_canvas)
+};
+bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);
+size_t wino4_weight_floats(int Cout, int Cin);
+void wino4_canvas(Wino4Params& p);
+hipError_t launch_wino4_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s);
+hipError_t launch_wino4(const Wino4Params& p, bool pre, Epi epi, hipStream_t s);
+
 // uint8 RGB HWC 112x112 -> (BGR, LUT normalise) -> conv3x3 3->64 -> BN -> PReLU, NHWC f32.
 hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64,
                        const float* bn_scale, const float* bn_shift, const float* prelu,

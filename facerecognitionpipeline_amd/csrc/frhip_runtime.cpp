@@ -241,12 +241,14 @@ struct ProfScope {
   hipStream_t s;
   ProfEvent ev{};
   bool on;
-  ProfScope(fr_handle* h_, hipStream_t s_, double flop, bool conv) : h(h_), s(s_), on(h_->prof) {
+  ProfScope(fr_handle* h_, hipStream_t s_, double flop, int kind, double exec_flop = -1.0)
+      : h(h_), s(s_), on(h_->prof) {
     if (!on) return;
     ev.a = take_event(h);
     ev.b = take_event(h);
     ev.flop = flop;
-    ev.conv = conv;
+    ev.exec_flop = exec_flop < 0 ? flop : exec_flop;
+    ev.kind = kind;
     if (!ev.a || !ev.b) {
       on = false;
       return;
@@ -301,6 +303,33 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // schedule (profiles/r01/sweep.txt): 8-wave 128x64 for the 64-channel
   // stage and the 128-channel residual convs, 8-wave 128x128 for the 1x1 shortcuts,
   // 8-wave 256x128 for every other 3x3 conv and the FC.
+  const bool wino_epi = (epi == EPI_AFFINE_PRELU && cw.pre_scale) || (epi == EPI_AFFINE_RES && !cw.pre_scale && res_H == p.Ho);
+  // Winograd F(4x4,3x3) for the stride-1 3x3 convs (f32 parity path only)
+  if (h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 && wino_epi) {
+    Wino4Params wp{};
+    wp.x = x;
+    wp.u = cw.wino4;
+    wp.y = y;
+    wp.pre_scale = cw.pre_scale;
+    wp.pre_shift = cw.pre_shift;
+    wp.post_scale = cw.post_scale;
+    wp.post_shift = cw.post_shift;
+    wp.prelu = cw.prelu;
+    wp.res = res;
+    wp.B = B;
+    wp.H = H;
+    wp.W = W;
+    wp.Cin = cw.cin;
+    wp.Cout = cw.cout;
+    Wino4Params cv = wp;
+    wino4_canvas(cv);
+    // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
+    const double exec = 2.0 * 36.0 * cv.ntiles * (double)cw.cin * cw.cout;
+    ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
+    hipError_t e = launch_wino4(wp, cw.pre_scale != nullptr, epi, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
+    return FR_OK;
+  }
   // Winograd F(2x2,3x3) for the stride-1 3x3 convs (f32 parity path only)
   if (h->winograd && h->prec == PREC_F32 && cw.wino &&
       ((epi == EPI_AFFINE_PRELU && cw.pre_scale) || (epi == EPI_AFFINE_RES && !cw.pre_scale && res_H == p.Ho))) {
@@ -319,7 +348,9 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.W = W;
     wp.Cin = cw.cin;
     wp.Cout = cw.cout;
-    ProfScope ps(h, s, flop, true);
+    // executed: 16 products per 2x2 output tile (padded tiles included) and (cin, cout) pair
+    const double exec = 2.0 * 16.0 * B * ((H + 1) / 2) * ((W + 1) / 2) * (double)cw.cin * cw.cout;
+    ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
     hipError_t e = launch_wino(wp, cw.pre_scale != nullptr, epi, s);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd launch: ") + hipGetErrorString(e));
     return FR_OK;
@@ -331,7 +362,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     tile = TILE_128x128_W8;
   else if (p.H == 1)
     tile = TILE_64x128;  // gallery scores (1x1 GEMM)
-  ProfScope ps(h, s, flop, true);
+  ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
   hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s, h->prec);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
   return FR_OK;
@@ -340,7 +371,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
 // One forward of up to max_batch crops: rgb (device) -> out (device) [n][512].
 int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int normalize, hipStream_t s) {
   {
-    ProfScope ps(h, s, 2.0 * n * 112.0 * 112.0 * 64 * 27, false);
+    ProfScope ps(h, s, 2.0 * n * 112.0 * 112.0 * 64 * 27, 0);
     hipError_t e = launch_stem(rgb, n, h->lut, h->stem_w, h->stem_scale, h->stem_shift, h->stem_prelu, h->act[0], s);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("stem launch: ") + hipGetErrorString(e));
   }
@@ -370,7 +401,7 @@ int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int norma
   int rc = run_conv(h, h->head, h->act[cur], h->partial, n, 7, 7, EPI_RAW, nullptr, 0, 0, h->head_split,
                     split_stride, s);
   if (rc) return rc;
-  ProfScope ps(h, s, 0.0, false);
+  ProfScope ps(h, s, 0.0, 0);
   hipError_t e = launch_head_reduce(h->partial, h->head_split, split_stride, h->fc_bias, h->bn1d_scale,
                                     h->bn1d_shift, out, n, normalize, !h->arcface, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("head launch: ") + hipGetErrorString(e));
@@ -397,7 +428,7 @@ int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float
   rc = ensure_buf(h, (void**)&h->scores, &h->scores_cap, (size_t)n * h->G * sizeof(float));
   if (rc) return rc;
   {
-    ProfScope ps(h, s, 0.0, false);
+    ProfScope ps(h, s, 0.0, 0);
     hipError_t e = launch_l2norm_rows(Q, h->qn, n, 512, s);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("l2norm launch: ") + hipGetErrorString(e));
   }
@@ -410,7 +441,7 @@ int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float
   g.pad = 0;
   rc = run_conv(h, g, h->qn, h->scores, n, 1, 1, EPI_RAW, nullptr, 0, 0, 1, 0, s);
   if (rc) return rc;
-  ProfScope ps(h, s, 0.0, false);
+  ProfScope ps(h, s, 0.0, 0);
   hipError_t e = launch_topk(h->scores, n, h->G, k, idx, score, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("topk launch: ") + hipGetErrorString(e));
   return FR_OK;
@@ -592,6 +623,32 @@ int fr_set_param(fr_handle* h, const char* name, const float* host_data, int64_t
   return FR_OK;
 }
 
+// F(4x4,3x3) filters of every eligible conv, built on the device from the arena the first
+// time the algorithm is selected after fr_finalize (36/9 = 4x the 3x3 weights).
+static int ensure_wino4(fr_handle* h) {
+  if (h->wino4_arena) return FR_OK;
+  std::vector<ConvW*> wconvs;
+  size_t wfloats = 0;
+  for (auto& b : h->blocks)
+    for (ConvW* c : {&b.conv1, &b.conv2}) {
+      c->wino4 = nullptr;
+      if (c->w && wino4_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
+        wconvs.push_back(c);
+        wfloats += wino4_weight_floats(c->cout, c->cin);
+      }
+    }
+  if (!wfloats) return FR_OK;
+  FR_HIP(h, hipMalloc((void**)&h->wino4_arena, wfloats * sizeof(float)));
+  size_t off = 0;
+  for (ConvW* c : wconvs) {
+    c->wino4 = h->wino4_arena + off;
+    FR_HIP(h, launch_wino4_weights(c->w, c->wino4, c->cout, c->cin, nullptr));
+    off += wino4_weight_floats(c->cout, c->cin);
+  }
+  FR_HIP(h, hipDeviceSynchronize());
+  return FR_OK;
+}
+
 int fr_finalize(fr_handle* h) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -712,6 +769,8 @@ int fr_finalize(fr_handle* h) {
   }
   if (h->wino_arena) FR_HIP(h, hipFree(h->wino_arena));
   h->wino_arena = nullptr;
+  if (h->wino4_arena) FR_HIP(h, hipFree(h->wino4_arena));
+  h->wino4_arena = nullptr;
   if (wfloats) {
     FR_HIP(h, hipMalloc((void**)&h->wino_arena, wfloats * sizeof(float)));
     size_t off = 0;
@@ -736,6 +795,10 @@ int fr_finalize(fr_handle* h) {
   if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
   h->finalized = true;
+  if (h->winograd && h->wino_m == 4 && ensure_wino4(h) != FR_OK) {
+    h->finalized = false;
+    return FR_ERR_HIP;
+  }
   return FR_OK;
 }
 
@@ -1046,9 +1109,11 @@ int fr_set_precision(fr_handle* h, int mode) {
 int fr_set_conv_algorithm(fr_handle* h, int algo) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
-  if (algo != FR_CONV_DIRECT && algo != FR_CONV_WINOGRAD)
-    return fail(h, FR_ERR_INVALID_ARGUMENT, "algorithm must be FR_CONV_DIRECT or FR_CONV_WINOGRAD");
-  h->winograd = algo == FR_CONV_WINOGRAD;
+  if (algo != FR_CONV_DIRECT && algo != FR_CONV_WINOGRAD && algo != FR_CONV_WINOGRAD4)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "algorithm must be FR_CONV_DIRECT, FR_CONV_WINOGRAD or FR_CONV_WINOGRAD4");
+  h->winograd = algo != FR_CONV_DIRECT;
+  h->wino_m = algo == FR_CONV_WINOGRAD4 ? 4 : 2;
+  if (h->wino_m == 4 && h->finalized) return ensure_wino4(h);
   return FR_OK;
 }
 
@@ -1063,26 +1128,40 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
   DeviceGuard dg(h->device);
-  double cms = 0, cfl = 0, tms = 0;
-  int64_t cn = 0;
+  double tms = 0;
+  for (int k = 0; k < 3; ++k) {
+    h->last_ms[k] = h->last_flop[k] = h->last_exec[k] = 0;
+    h->last_n[k] = 0;
+  }
   for (auto& e : h->events) {
     FR_HIP(h, hipEventSynchronize(e.b));
     float ms = 0.f;
     FR_HIP(h, hipEventElapsedTime(&ms, e.a, e.b));
     tms += ms;
-    if (e.conv) {
-      cms += ms;
-      cfl += e.flop;
-      ++cn;
-    }
+    const int k = e.kind >= 0 && e.kind < 3 ? e.kind : 0;
+    h->last_ms[k] += ms;
+    h->last_flop[k] += e.flop;
+    h->last_exec[k] += e.exec_flop;
+    ++h->last_n[k];
     h->pool.push_back(e.a);
     h->pool.push_back(e.b);
   }
   h->events.clear();
-  if (conv_ms) *conv_ms = cms;
-  if (conv_flop) *conv_flop = cfl;
-  if (conv_launches) *conv_launches = cn;
+  if (conv_ms) *conv_ms = h->last_ms[1] + h->last_ms[2];
+  if (conv_flop) *conv_flop = h->last_flop[1] + h->last_flop[2];
+  if (conv_launches) *conv_launches = h->last_n[1] + h->last_n[2];
   if (total_ms) *total_ms = tms;
+  return FR_OK;
+}
+
+int fr_profile_kernel(fr_handle* h, int kind, double* ms, double* flop, double* exec_flop, int64_t* launches) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  if (kind < 0 || kind > 2) return fail(h, FR_ERR_INVALID_ARGUMENT, "kind must be FR_PROF_OTHER/CONV_DIRECT/CONV_WINOGRAD");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (ms) *ms = h->last_ms[kind];
+  if (flop) *flop = h->last_flop[kind];
+  if (exec_flop) *exec_flop = h->last_exec[kind];
+  if (launches) *launches = h->last_n[kind];
   return FR_OK;
 }
 
@@ -1179,6 +1258,43 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
   (void)hipFree(u);
   if (e == hipSuccess) e = se;
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
+                        const float* pre_scale, const float* pre_shift, const float* post_scale,
+                        const float* post_shift, const float* prelu, const float* res, int epi, void* stream) {
+  if (!wino4_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
+      (epi == EPI_AFFINE_PRELU && (!pre_scale || !pre_shift || !prelu)) || (epi == EPI_AFFINE_RES && (pre_scale || !res)) ||
+      !post_scale || !post_shift || B < 1 || H < 1 || W < 1)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  float* u = nullptr;
+  if (hipMalloc((void**)&u, wino4_weight_floats(cout, cin) * sizeof(float)) != hipSuccess)
+    return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4: allocation failed");
+  hipError_t e = launch_wino4_weights(w, u, cout, cin, s);
+  if (e == hipSuccess) {
+    Wino4Params p{};
+    p.x = x;
+    p.u = u;
+    p.y = y;
+    p.pre_scale = pre_scale;
+    p.pre_shift = pre_shift;
+    p.post_scale = post_scale;
+    p.post_shift = post_shift;
+    p.prelu = prelu;
+    p.res = res;
+    p.B = B;
+    p.H = H;
+    p.W = W;
+    p.Cin = cin;
+    p.Cout = cout;
+    e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s);
+  }
+  const hipError_t se = hipStreamSynchronize(s);
+  (void)hipFree(u);
+  if (e == hipSuccess) e = se;
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd4: ") + hipGetErrorString(e));
   return FR_OK;
 }
 

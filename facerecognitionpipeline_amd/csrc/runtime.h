@@ -26,6 +26,7 @@ struct ConvW {
   float* post_shift = nullptr;
   float* prelu = nullptr;
   float* wino = nullptr;  // Winograd-transformed filters (stride-1 3x3 only), or null
+  float* wino4 = nullptr; // F(4x4,3x3) transformed filters (built on demand), or null
   int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
 };
 
@@ -35,10 +36,12 @@ struct BlockW {
   bool has_sc_conv = false;
 };
 
+// kind: 0 other launch, 1 direct implicit-GEMM conv, 2 Winograd conv (frhip.h FR_PROF_*)
 struct ProfEvent {
   hipEvent_t a, b;
-  double flop;
-  bool conv;
+  double flop;       // algorithmic (direct-conv) FLOPs
+  double exec_flop;  // FLOPs the MFMA pipe actually executes
+  int kind;
 };
 
 struct Detector;  // detector.cpp
@@ -103,8 +106,10 @@ struct fr_handle {
   int sk_cnt_cap = 0;
   bool stream_k = true;
   frhip::Precision prec = frhip::PREC_F32;
-  bool winograd = true;          // FR_CONV_WINOGRAD for stride-1 3x3 convs
+  bool winograd = true;          // FR_CONV_WINOGRAD / _WINOGRAD4 for stride-1 3x3 convs
+  int wino_m = 2;                // output tile of the Winograd algorithm: 2 = F(2x2,3x3), 4 = F(4x4,3x3)
   float* wino_arena = nullptr;   // transformed filters of every eligible conv
+  float* wino4_arena = nullptr;  // F(4x4) filters, built when that algorithm is selected
 
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
   frhip_rt::Detector* det = nullptr;
@@ -113,6 +118,8 @@ struct fr_handle {
   bool prof = false;
   std::vector<frhip_rt::ProfEvent> events;
   std::vector<hipEvent_t> pool;
+  double last_ms[3] = {0, 0, 0}, last_flop[3] = {0, 0, 0}, last_exec[3] = {0, 0, 0};
+  int64_t last_n[3] = {0, 0, 0};
 
   ~fr_handle() {
     frhip_rt::detector_destroy(det);
@@ -123,6 +130,7 @@ struct fr_handle {
     for (auto e : pool) (void)hipEventDestroy(e);
     (void)hipFree(arena);
     (void)hipFree(wino_arena);
+    (void)hipFree(wino4_arena);
     for (auto p : act) (void)hipFree(p);
     (void)hipFree(sc_buf);
     (void)hipFree(partial);

@@ -155,6 +155,7 @@ int fr_set_precision(fr_handle* h, int mode);
  * Ignored under FR_PRECISION_BF16X3 (direct split-bf16 everywhere). */
 #define FR_CONV_DIRECT 0
 #define FR_CONV_WINOGRAD 1
+#define FR_CONV_WINOGRAD4 2  /* F(4x4,3x3): 36 products per 4x4 tile (4x fewer than direct); filters built on selection */
 int fr_set_conv_algorithm(fr_handle* h, int algo);
 
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).
@@ -163,6 +164,13 @@ int fr_set_conv_algorithm(fr_handle* h, int algo);
  * their launch count, and the summed milliseconds of all launches. */
 int fr_profile_enable(fr_handle* h, int enable);
 int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* conv_launches, double* total_ms);
+/* Breakdown of the last fr_profile_read by kernel class: summed ms, algorithmic (direct-conv)
+ * FLOPs, FLOPs the MFMA pipe executed (Winograd: 16 products per 2x2 tile instead of 36) and
+ * launch count. */
+#define FR_PROF_OTHER 0
+#define FR_PROF_CONV_DIRECT 1
+#define FR_PROF_CONV_WINOGRAD 2
+int fr_profile_kernel(fr_handle* h, int kind, double* ms, double* flop, double* exec_flop, int64_t* launches);
 
 /* Last error message of this handle (or of the last failed fr_create if h is NULL). */
 const char* fr_last_error(fr_handle* h);

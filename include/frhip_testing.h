@@ -35,6 +35,10 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
 int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                         const float* pre_scale, const float* pre_shift, const float* post_scale,
                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
+/* Winograd F(4x4,3x3) (the FR_CONV_WINOGRAD4 path), same arguments; cin % 16 == 0, cout % 32 == 0. */
+int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
+                         const float* pre_scale, const float* pre_shift, const float* post_scale,
+                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
 
 /* Fused preprocess + input_layer on uint8 RGB [B][112][112][3]; w27x64 is the
  * repacked [ky][kx][c_rgb][64] weight; lut the 256-entry normalisation table. */

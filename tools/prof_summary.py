@@ -80,9 +80,11 @@ def main():
     L = layers(a.arch, a.batch)
     fwds = align(rows, L, a.batch)
     per = collections.defaultdict(list)
+    kname = {}
     for fw in fwds:
         for name, d in fw:
             per[name].append(int(d["End_Timestamp"]) - int(d["Start_Timestamp"]))
+            kname.setdefault(name, d["Kernel_Name"])
     # PMC: counters per dispatch of the aligned forwards in each PMC pass
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))  # counter -> layer -> [values]
     for d in a.pmc:
@@ -106,6 +108,7 @@ def main():
     summary, seen = [], set()
     tot_ns = tot_flop = conv_ns = conv_flop = 0.0
     conv_alg = conv_hbm = conv_n = 0.0
+    fam = collections.defaultdict(lambda: collections.defaultdict(float))  # kernel family -> totals per forward
     for name, flop, alg in L:
         if name in seen or not per[name]:
             continue
@@ -120,6 +123,21 @@ def main():
         row = {"layer": name, "per_fwd": cnt, "avg_us": avg_ns / 1e3, "tflops": tf, "alg_bytes": alg}
         line = f"{name:38s} {cnt:5d} {avg_ns / 1e3:9.1f} {tf:7.1f} {100 * tf / PEAK:6.1f} {100 * share:6.1f} {alg / 1e6:8.1f}"
         is_conv = "conv" in name or "shortcut" in name or "head.fc" in name
+        kn = kname.get(name, "")
+        family = "winograd" if "wino_kernel" in kn else ("direct" if is_conv else "other")
+        exec_flop = flop
+        if family == "winograd":  # 16 products per (padded) 2x2 tile instead of 36 per 4 pixels
+            hw = int(name.split("@")[1].split("/")[0])
+            exec_flop = flop * 16.0 / 36.0 * (2 * ((hw + 1) // 2)) ** 2 / hw ** 2
+        row["kernel"] = kn.split("(")[0][:60]
+        row["family"] = family
+        row["exec_tflops"] = exec_flop / (avg_ns * 1e-9) / 1e12 if avg_ns else 0.0
+        fa = fam[family]
+        fa["ns"] += avg_ns * cnt
+        fa["flop"] += flop * cnt
+        fa["exec_flop"] += exec_flop * cnt
+        fa["alg_bytes"] += alg * cnt
+        fa["launches"] += cnt
         if is_conv:
             conv_ns += avg_ns * cnt
             conv_flop += flop * cnt
@@ -129,6 +147,8 @@ def main():
             if fe and wr:
                 hbm = 2 * 1024 * sum(fe) / len(fe) + 1024 * sum(wr) / len(wr)
                 row["hbm_bytes"] = hbm
+                fa["hbm_bytes"] += hbm * cnt
+                fa["pmc_launches"] += cnt
                 line += f" {hbm / 1e6:8.1f} {hbm / alg:7.2f}"
                 if is_conv:
                     conv_alg += alg * cnt
@@ -146,6 +166,22 @@ def main():
         res["alg_bytes_per_conv_launch"] = conv_alg / conv_n
         print(f"PMC conv family per launch: HBM {conv_hbm / conv_n / 1e6:.1f} MB (FETCH x2 + WRITE) vs algorithmic "
               f"{conv_alg / conv_n / 1e6:.1f} MB -> {conv_hbm / conv_alg:.2f}x")
+    kernels = {}
+    for family, fa in fam.items():
+        k = {"launches_per_forward": int(fa["launches"]), "ms_per_forward": fa["ns"] / 1e6,
+             "avg_launch_ms": fa["ns"] / 1e6 / fa["launches"], "alg_flop_per_launch": fa["flop"] / fa["launches"],
+             "exec_flop_per_launch": fa["exec_flop"] / fa["launches"],
+             "alg_tflops": fa["flop"] / fa["ns"] / 1e3 if fa["ns"] else 0.0,
+             "exec_tflops": fa["exec_flop"] / fa["ns"] / 1e3 if fa["ns"] else 0.0,
+             "alg_bytes_per_launch": fa["alg_bytes"] / fa["launches"]}
+        if fa["pmc_launches"]:
+            k["hbm_bytes_per_launch"] = fa["hbm_bytes"] / fa["pmc_launches"]
+        kernels[family] = k
+        print(f"{family:9s}: {k['launches_per_forward']:3d} launches/fwd, {k['ms_per_forward']:.3f} ms/fwd, "
+              f"avg {k['avg_launch_ms']:.4f} ms, alg {k['alg_tflops']:.1f} TF/s, executed {k['exec_tflops']:.1f} TF/s"
+              + (f", HBM {k['hbm_bytes_per_launch'] / 1e6:.1f} MB/launch vs alg {k['alg_bytes_per_launch'] / 1e6:.1f}"
+                 if "hbm_bytes_per_launch" in k else ""))
+    res["kernels"] = kernels
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)
