@@ -25,15 +25,19 @@
 //   * 4 waves, one per SIMD (512 registers each); wave w owns xi = 9w .. 9w+8, so its
 //     accumulators are 9 32x32 MFMA blocks and no operand it reads is read by another wave.
 //   * K-step = 16 input channels.  Thread (tile, channel pair) loads its 6x6 patch as 36
-//     8-byte buffer loads (OOB offset -> 0 = zero padding; the pre-BN affine only at
-//     in-image taps), transforms it in registers and writes 36 float2 of V to LDS
+//     8-byte buffer loads (OOB offset -> 0 = zero padding), transforms it in registers
+//     and writes 36 float2 of V to LDS
 //     V[xi][tile][16 ch], rows XOR-swizzled by 16-B slot so that the ds_read_b128 fragment
 //     reads and the ds_write_b64 stores are both conflict-free.
 //   * U (transformed filters, built once per model by wino4_weight_kernel) never touches
 //     LDS: it is stored in MFMA-fragment order, so each wave fetches its B fragments with
 //     fully coalesced 1 KiB buffer loads, one K-step ahead.
 //   * One barrier per K-step: the patch of step s+1 is loaded at the top of step s and
-//     transformed into the other LDS buffer in the shadow of step s's 72 MFMAs.
+//     transformed into the other LDS buffer in the shadow of the second half of step s's
+//     72 MFMAs.
+//   * The pre-activation BatchNorm of conv1 is folded out of the K loop: its scale into the
+//     filters (U = G (g*sc) G^T), its shift into a per-(border class, cout) constant added
+//     in the epilogue (wino4_corr_kernel), so the transform is pure adds and fmas.
 //   * Epilogue: accumulators go through LDS as M[xi][tile][cout] (the whole 144 KiB), each
 //     thread inverse-transforms 4 (tile, cout) pairs and applies BN (+PReLU | + residual)
 //     at the in-image pixels of each tile.
@@ -59,7 +63,7 @@ constexpr int XPW = 9;               // transform elements per wave
 constexpr int VPLANE = WT * KC;      // one xi plane of V: 512 floats
 constexpr int VBUF = NXI * VPLANE;   // one K-step of V: 18432 floats (72 KiB)
 constexpr int MPLANE = WT * 32;      // epilogue: one xi plane of M[tile][cout]
-constexpr int OOB = 0x80000000;      // buffer offset past any range: loads return 0
+constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum with it is past the range
 static_assert(NXI * MPLANE <= 2 * VBUF, "epilogue staging must fit the V buffers");
 
 __device__ __forceinline__ int wino4_xcd_remap(int bid, int n) {
@@ -113,7 +117,7 @@ __device__ __forceinline__ void at6(const float (&m)[6], float (&o)[4]) {
   o[3] = m12 + 8.f * m34 + m[5];
 }
 
-template <bool PRE, int EPI>
+template <bool CORR, int EPI>
 __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
   __shared__ __attribute__((aligned(16))) float lds[2 * VBUF];
 
@@ -128,85 +132,56 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
   const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
 
   // ---- transform role: thread (tile tl, channel pair cp) ------------------------------
+  // byte offset of patch pixel (i, j) = roff[i] + coff[j]; an out-of-image row or column
+  // carries BIGOFF, which puts the sum past the buffer range (load returns 0)
   const int tl = tid >> 3, cp = tid & 7;
-  int off[6][6];
-  unsigned long long vmask = 0;  // bit 6i+j: patch pixel (i, j) is inside an image
+  int roff[6], coff[6];
   {
     const int T = mb * WT + tl;
     const int tr = T / p.TWc, tc = T - tr * p.TWc;
-    const int R0 = 4 * tr - 1, C0 = 4 * tc - 1;
     const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
-    int rp[6], cpx[6];
-    unsigned rv = 0, cv = 0;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       int slot;
-      const int y = canvas_coord(R0 + i, ir0, p.Pr, H, sep_r, slot);
-      rp[i] = (slot * p.NC * H + y) * W;
-      if (y >= 0 && T < p.ntiles) rv |= 1u << i;
-      const int x = canvas_coord(C0 + i, ic0, p.Pc, W, sep_c, slot);
-      cpx[i] = slot * H * W + x;
-      if (x >= 0 && slot < p.NC) cv |= 1u << i;
+      const int y = canvas_coord(4 * tr - 1 + i, ir0, p.Pr, H, sep_r, slot);
+      roff[i] = (y >= 0 && T < p.ntiles) ? (slot * p.NC * H + y) * W * Cin * 4 : BIGOFF;
+      const int x = canvas_coord(4 * tc - 1 + i, ic0, p.Pc, W, sep_c, slot);
+      coff[i] = (x >= 0 && slot < p.NC) ? ((slot * H * W + x) * Cin + 2 * cp) * 4 : BIGOFF;
     }
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const bool ok = ((rv >> i) & 1u) && ((cv >> j) & 1u);
-        off[i][j] = ok ? ((rp[i] + cpx[j]) * Cin + 2 * cp) * 4 : OOB;
-        if (ok) vmask |= 1ull << (6 * i + j);
-      }
   }
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc4(p.x, p.B * H * W * Cin * 4);
   const __amdgpu_buffer_rsrc_t ur = uniform_rsrc4(p.u, NXI * p.Cout * Cin * 4);
-  const __amdgpu_buffer_rsrc_t pr = uniform_rsrc4(p.pre_scale, PRE ? Cin * 4 : 0);
-  const __amdgpu_buffer_rsrc_t qr = uniform_rsrc4(p.pre_shift, PRE ? Cin * 4 : 0);
   auto f2u = [](u32x2 v) { return f2{__uint_as_float(v.x), __uint_as_float(v.y)}; };
   auto f4u = [](u32x4 v) {
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
   };
 
   f2 d[6][6];
-  f2 psc, psh;
   auto load_patch = [&](int s) {
     const int so = min(s, KS - 1) * KC * 4;
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
-      for (int j = 0; j < 6; ++j) d[i][j] = f2u(__builtin_amdgcn_raw_buffer_load_b64(xr, off[i][j], so, 0));
-    if constexpr (PRE) {
-      psc = f2u(__builtin_amdgcn_raw_buffer_load_b64(pr, 8 * cp, so, 0));
-      psh = f2u(__builtin_amdgcn_raw_buffer_load_b64(qr, 8 * cp, so, 0));
-    }
+      for (int j = 0; j < 6; ++j)
+        d[i][j] = f2u(__builtin_amdgcn_raw_buffer_load_b64(xr, (int)((unsigned)roff[i] + (unsigned)coff[j]), so, 0));
   };
   // physical float offset of this thread's channel pair inside its V row (16-B slot XOR)
   const int vslot = (((cp >> 1) ^ ((tl >> 2) & 3)) << 2) + ((cp & 1) << 1);
   auto store_v = [&](int buf) {
-    if constexpr (PRE) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-          const bool ok = (vmask >> (6 * i + j)) & 1ull;
-          const f2 v = d[i][j] * psc + psh;
-          d[i][j] = ok ? v : f2{0.f, 0.f};
-        }
-    }
-    f2 tcol[6][6];  // tcol[a][j] = (B^T d)[a][j]
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
+    for (int j = 0; j < 6; ++j) {  // columns: d[.][j] <- (B^T d)[.][j], in place
       f2 c[6], o[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) c[i] = d[i][j];
       bt6(c, o);
 #pragma unroll
-      for (int a = 0; a < 6; ++a) tcol[a][j] = o[a];
+      for (int i = 0; i < 6; ++i) d[i][j] = o[i];
     }
     float* dst = lds + buf * VBUF + tl * KC + vslot;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
       f2 v[6];
-      bt6(tcol[a], v);
+      bt6(d[a], v);
 #pragma unroll
       for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(dst + (6 * a + b) * VPLANE) = v[b];
     }
@@ -224,8 +199,8 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
   };
   const int m = lane & 31, h = lane >> 5;
   const int rq = (m >> 2) & 3;
-  const float* vrd0 = lds + m * KC + (((2 * h) ^ rq) << 2);
-  const float* vrd1 = lds + m * KC + (((2 * h + 1) ^ rq) << 2);
+  const float* vrd0 = lds + (XPW * wid) * VPLANE + m * KC + (((2 * h) ^ rq) << 2);
+  const float* vrd1 = lds + (XPW * wid) * VPLANE + m * KC + (((2 * h + 1) ^ rq) << 2);
 
   floatx16 acc[XPW];
 #pragma unroll
@@ -239,25 +214,74 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
   store_v(0);
   __syncthreads();
 
+  // One K-step: MFMAs of xi 0..4 (fragment reads one xi ahead, U of the next step behind),
+  // then -- with the patch loads of step s+1, issued at the top, now 40 MFMAs old -- the
+  // transform of that patch in 12 pieces (6 column passes, 6 row passes + V stores),
+  // pinned between the 32 MFMAs of xi 5..8 so it runs in their shadow; one barrier.
+  auto col_piece = [&](int j) {
+    f2 c[6], o[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) c[i] = d[i][j];
+    bt6(c, o);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) d[i][j] = o[i];
+  };
+  auto row_piece = [&](int a, int buf) {
+    float* dst = lds + buf * VBUF + tl * KC + vslot + 6 * a * VPLANE;
+    f2 v[6];
+    bt6(d[a], v);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(dst + b * VPLANE) = v[b];
+  };
   for (int s = 0; s < KS; ++s) {
-    const int buf = s & 1;
+    const int vb = (s & 1) * VBUF;
     load_patch(s + 1);
+    float4 fa[2][2];
+    fa[0][0] = *reinterpret_cast<const float4*>(vrd0 + vb);
+    fa[0][1] = *reinterpret_cast<const float4*>(vrd1 + vb);
+    auto frag_next = [&](int x) {
+      if (x + 1 < XPW) {
+        fa[(x + 1) & 1][0] = *reinterpret_cast<const float4*>(vrd0 + vb + (x + 1) * VPLANE);
+        fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd1 + vb + (x + 1) * VPLANE);
+      }
+    };
+    auto mfma = [&](int x, int j) {
+      const float4 q = fa[x & 1][j >> 2];
+      const float4 r = u[x][j >> 2];
+      const float av = (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
+      const float bv = (j & 3) == 0 ? r.x : (j & 3) == 1 ? r.y : (j & 3) == 2 ? r.z : r.w;
+      acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[x], 0, 0, 0);
+    };
 #pragma unroll
-    for (int x = 0; x < XPW; ++x) {
-      const int xo = buf * VBUF + (XPW * wid + x) * VPLANE;
-      const float4 a0 = *reinterpret_cast<const float4*>(vrd0 + xo);
-      const float4 a1 = *reinterpret_cast<const float4*>(vrd1 + xo);
-      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const float bv[8] = {u[x][0].x, u[x][0].y, u[x][0].z, u[x][0].w, u[x][1].x, u[x][1].y, u[x][1].z, u[x][1].w};
+    for (int x = 0; x < 5; ++x) {
+      frag_next(x);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc[x], 0, 0, 0);
+      for (int j = 0; j < 8; ++j) mfma(x, j);
       load_u(x, s + 1);
     }
-    store_v(buf ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const int nbuf = (s & 1) ^ 1;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int x = 5 + (k >> 3), j = k & 7;
+      if (j == 0) frag_next(x);
+      mfma(x, j);
+      if (j == 7) load_u(x, s + 1);
+      // piece i after MFMA floor(8i/3): 0,2,5,8,10,13,16,18,21,24,26,29
+      if ((3 * k) % 8 < 3) {
+        const int piece = (3 * k) / 8;
+        if (piece < 6)
+          col_piece(piece);
+        else
+          row_piece(piece - 6, nbuf);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
   }
 
-  // ---- epilogue: inverse transform + BN (+PReLU | +residual) -------------------------
+  // ---- epilogue: inverse transform (+ pre-BN correction) + BN (+PReLU | +residual) ---
 #pragma unroll
   for (int x = 0; x < XPW; ++x) {
     float* dst = lds + (XPW * wid + x) * MPLANE + m;
@@ -277,15 +301,17 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
     if (T >= p.ntiles) continue;
     const int tr = T / p.TWc, tc = T - tr * p.TWc;
     const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
-    int orow[4], ocol[4];
+    int orow[4], ocol[4], rcls[4], ccls[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int slot;
       const int y = canvas_coord(4 * tr + i, ir0, p.Pr, H, sep_r, slot);
       const int nimg = slot * p.NC;
       orow[i] = (y >= 0 && nimg < p.B) ? (nimg * H + y) * W : -1;
+      rcls[i] = ((y == 0) ? 1 : 0) | ((y == H - 1) ? 2 : 0);
       const int xx = canvas_coord(4 * tc + i, ic0, p.Pc, W, sep_c, slot);
       ocol[i] = (xx >= 0 && slot < p.NC) ? slot * H * W + xx : -1;
+      ccls[i] = ((xx == 0) ? 1 : 0) | ((xx == W - 1) ? 2 : 0);
     }
     float mv[6][6];
 #pragma unroll
@@ -307,7 +333,9 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
         const int pix = orow[r] + ocol[c];
         if (pix >= p.B * H * W) continue;
         const long long oo = (long long)pix * p.Cout + cout;
-        float v = o[r] * sc + sh;
+        float v = o[r];
+        if constexpr (CORR) v += p.corr[(rcls[r] * 4 + ccls[c]) * p.Cout + cout];
+        v = v * sc + sh;
         if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
         if constexpr (EPI == EPI_AFFINE_RES) v += p.res[oo];
         if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
@@ -320,10 +348,34 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
   }
 }
 
+// Pre-activation BatchNorm folded out of the transform (conv1 of every block):
+//   conv(sc*x + sh, zero padded) = conv(w*sc, x) + sum_{cin, in-image taps} w*sh
+// The second term depends only on which taps of the 3x3 window fall outside the image:
+// class = 4*rowcls + colcls, rowcls bit 0 = top row missing (y == 0), bit 1 = bottom row
+// missing (y == H-1); colcls likewise.  corr[class][cout], summed in double.
+__global__ void wino4_corr_kernel(const float* __restrict__ w, const float* __restrict__ shift,
+                                  float* __restrict__ corr, int Cout, int Cin) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 16 * Cout) return;
+  const int cls = idx / Cout, o = idx - cls * Cout;
+  const int rc = cls >> 2, cc = cls & 3;
+  double acc = 0.0;
+  for (int ky = 0; ky < 3; ++ky) {
+    if ((ky == 0 && (rc & 1)) || (ky == 2 && (rc & 2))) continue;
+    for (int kx = 0; kx < 3; ++kx) {
+      if ((kx == 0 && (cc & 1)) || (kx == 2 && (cc & 2))) continue;
+      const float* wr = w + ((long long)(o * 3 + ky) * 3 + kx) * Cin;
+      for (int i = 0; i < Cin; ++i) acc += (double)wr[i] * (double)shift[i];
+    }
+  }
+  corr[idx] = (float)acc;
+}
+
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into
 // the fragment order wino4_kernel reads: [xi][Cout/32][Cin/16][q][lane][4] with
 // lane = 32*(c/8) + cout%32, q = (c%8)/4, element = c%4 for c = cin%16.
-__global__ void wino4_weight_kernel(const float* __restrict__ w, float* __restrict__ u, int Cout, int Cin) {
+__global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __restrict__ pre_scale,
+                                    float* __restrict__ u, int Cout, int Cin) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= Cout * Cin) return;
   const int o = idx / Cin, i = idx - o * Cin;
@@ -338,6 +390,13 @@ __global__ void wino4_weight_kernel(const float* __restrict__ w, float* __restri
   for (int y = 0; y < 3; ++y)
 #pragma unroll
     for (int x = 0; x < 3; ++x) g[y][x] = w[((long long)(o * 3 + y) * 3 + x) * Cin + i];
+  if (pre_scale) {
+    const double ps = pre_scale[i];
+#pragma unroll
+    for (int y = 0; y < 3; ++y)
+#pragma unroll
+      for (int x = 0; x < 3; ++x) g[y][x] *= ps;
+  }
   double tg[6][3];
 #pragma unroll
   for (int a = 0; a < 6; ++a)
@@ -365,10 +424,14 @@ bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
 
 size_t wino4_weight_floats(int Cout, int Cin) { return (size_t)NXI * Cout * Cin; }
 
-hipError_t launch_wino4_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s) {
-  if (Cout % 32 || Cin % KC) return hipErrorInvalidValue;
+hipError_t launch_wino4_weights(const float* w, const float* pre_scale, const float* pre_shift, float* u,
+                                float* corr, int Cout, int Cin, hipStream_t s) {
+  if (Cout % 32 || Cin % KC || (pre_scale && (!pre_shift || !corr))) return hipErrorInvalidValue;
   const int n = Cout * Cin;
-  hipLaunchKernelGGL(wino4_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, u, Cout, Cin);
+  hipLaunchKernelGGL(wino4_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, pre_scale, u, Cout, Cin);
+  if (pre_scale)
+    hipLaunchKernelGGL(wino4_corr_kernel, dim3((16 * Cout + 255) / 256), dim3(256), 0, s, w, pre_shift, corr, Cout,
+                       Cin);
   return hipGetLastError();
 }
 
@@ -392,7 +455,7 @@ void wino4_canvas(Wino4Params& p) {
 hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
   Wino4Params p = p0;
   if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
-      (long long)p.B * p.H * p.W * p.Cin * 4 >= (1ll << 31) ||
+      (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF ||
       (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) || (long long)NXI * p.Cout * p.Cin * 4 >= (1ll << 31))
     return hipErrorInvalidValue;
   wino4_canvas(p);
@@ -404,6 +467,7 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
     hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_>), grid, block, 0, s, p);    \
     return hipGetLastError();                                                \
   }
+  if (pre && !p.corr) return hipErrorInvalidValue;
   FR_WINO4_CASE(true, EPI_AFFINE_PRELU)
   FR_WINO4_CASE(false, EPI_AFFINE_RES)
 #undef FR_WINO4_CASE

@@ -105,14 +105,18 @@ struct Wino4Params {
   const float* post_scale;
   const float* post_shift;
   const float* prelu;
-  const float* res;  // same shape as y
+  const float* res;   // same shape as y
+  const float* corr;  // [16][Cout] pre-BN shift correction (launch_wino4_weights), with pre-BN only
   int B, H, W, Cin, Cout;
   int Pr, Pc, NC, TWc, ntiles, mblocks, nblocks;  // set by launch_wino4 (wino4_canvas)
 };
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);
 size_t wino4_weight_floats(int Cout, int Cin);
 void wino4_canvas(Wino4Params& p);
-hipError_t launch_wino4_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s);
+// w: [Cout][3][3][Cin] -> u = G (w * pre_scale[cin]) G^T in fragment order; with pre-BN also
+// corr[16][Cout] (pre_shift through the in-image taps of each border class).
+hipError_t launch_wino4_weights(const float* w, const float* pre_scale, const float* pre_shift, float* u,
+                                float* corr, int Cout, int Cin, hipStream_t s);
 hipError_t launch_wino4(const Wino4Params& p, bool pre, Epi epi, hipStream_t s);
 
 // uint8 RGB HWC 112x112 -> (BGR, LUT normalise) -> conv3x3 3->64 -> BN -> PReLU, NHWC f32.

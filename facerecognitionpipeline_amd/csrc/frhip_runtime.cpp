@@ -309,6 +309,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     Wino4Params wp{};
     wp.x = x;
     wp.u = cw.wino4;
+    wp.corr = cw.wino4_corr;
     wp.y = y;
     wp.pre_scale = cw.pre_scale;
     wp.pre_shift = cw.pre_shift;
@@ -632,9 +633,10 @@ static int ensure_wino4(fr_handle* h) {
   for (auto& b : h->blocks)
     for (ConvW* c : {&b.conv1, &b.conv2}) {
       c->wino4 = nullptr;
+      c->wino4_corr = nullptr;
       if (c->w && wino4_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
         wconvs.push_back(c);
-        wfloats += wino4_weight_floats(c->cout, c->cin);
+        wfloats += wino4_weight_floats(c->cout, c->cin) + (c->pre_scale ? 16 * (size_t)c->cout : 0);
       }
     }
   if (!wfloats) return FR_OK;
@@ -642,8 +644,13 @@ static int ensure_wino4(fr_handle* h) {
   size_t off = 0;
   for (ConvW* c : wconvs) {
     c->wino4 = h->wino4_arena + off;
-    FR_HIP(h, launch_wino4_weights(c->w, c->wino4, c->cout, c->cin, nullptr));
     off += wino4_weight_floats(c->cout, c->cin);
+    if (c->pre_scale) {
+      c->wino4_corr = h->wino4_arena + off;
+      off += 16 * (size_t)c->cout;
+    }
+    FR_HIP(h, launch_wino4_weights(c->w, c->pre_scale, c->pre_shift, c->wino4, c->wino4_corr, c->cout, c->cin,
+                                   nullptr));
   }
   FR_HIP(h, hipDeviceSynchronize());
   return FR_OK;
@@ -1270,13 +1277,15 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   float* u = nullptr;
-  if (hipMalloc((void**)&u, wino4_weight_floats(cout, cin) * sizeof(float)) != hipSuccess)
+  if (hipMalloc((void**)&u, (wino4_weight_floats(cout, cin) + 16 * (size_t)cout) * sizeof(float)) != hipSuccess)
     return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4: allocation failed");
-  hipError_t e = launch_wino4_weights(w, u, cout, cin, s);
+  float* corr = pre_scale ? u + wino4_weight_floats(cout, cin) : nullptr;
+  hipError_t e = launch_wino4_weights(w, pre_scale, pre_shift, u, corr, cout, cin, s);
   if (e == hipSuccess) {
     Wino4Params p{};
     p.x = x;
     p.u = u;
+    p.corr = corr;
     p.y = y;
     p.pre_scale = pre_scale;
     p.pre_shift = pre_shift;

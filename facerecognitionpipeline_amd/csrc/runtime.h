@@ -27,6 +27,7 @@ struct ConvW {
   float* prelu = nullptr;
   float* wino = nullptr;  // Winograd-transformed filters (stride-1 3x3 only), or null
   float* wino4 = nullptr; // F(4x4,3x3) transformed filters (built on demand), or null
+  float* wino4_corr = nullptr;  // [16][Cout] pre-BN shift correction of the F(4x4) path (conv1 only)
   int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
 };
 

@@ -124,7 +124,7 @@ def main():
         line = f"{name:38s} {cnt:5d} {avg_ns / 1e3:9.1f} {tf:7.1f} {100 * tf / PEAK:6.1f} {100 * share:6.1f} {alg / 1e6:8.1f}"
         is_conv = "conv" in name or "shortcut" in name or "head.fc" in name
         kn = kname.get(name, "")
-        family = "winograd" if "wino_kernel" in kn else ("direct" if is_conv else "other")
+        family = "winograd" if "wino" in kn else ("direct" if is_conv else "other")
         exec_flop = flop
         if family == "winograd":  # 16 products per (padded) 2x2 tile instead of 36 per 4 pixels
             hw = int(name.split("@")[1].split("/")[0])
