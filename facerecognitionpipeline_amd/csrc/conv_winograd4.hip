@@ -1,4 +1,4 @@
-// Winograd F(4x4, 3x3) convolution in f32 on gfx950 MFMA (v_mfma_f32_32x32x2_f32).
+// Winograd F(4x4, 3x3) convolution in f32 on gfx950 MFMA (v_mfma_f32_16x16x4_f32).
 //
 // Replaces the stride-1 3x3 Conv2d of net.BasicBlockIR (res_layer[1] and the stride-1
 // res_layer[4]; reached through `self.model(batch)`, face_embedder.py:157) with the same
@@ -22,38 +22,52 @@
 // Per transform element xi = 6a + b (36 of them) the layer is one GEMM
 //   M_xi[tile][cout] = sum_cin V_xi[tile][cin] * U_xi[cin][cout]
 // and one workgroup owns WT = 32 tiles x 32 couts for all 36.
-//   * 4 waves, one per SIMD (512 registers each); wave w owns xi = 9w .. 9w+8, so its
-//     accumulators are 9 32x32 MFMA blocks and no operand it reads is read by another wave.
-//   * K-step = 16 input channels.  Thread (tile, channel pair) loads its 6x6 patch as 36
-//     8-byte buffer loads (OOB offset -> 0 = zero padding), transforms it in registers
-//     and writes 36 float2 of V to LDS
-//     V[xi][tile][16 ch], rows XOR-swizzled by 16-B slot so that the ds_read_b128 fragment
-//     reads and the ds_write_b64 stores are both conflict-free.
+//   * 8 waves, two per SIMD: wave w owns xi = 9(w%4) .. 9(w%4)+8 and couts 16(w/4) .. +15,
+//     i.e. 9 x 2 16x16 MFMA blocks (v_mfma_f32_16x16x4_f32), 72 accumulator registers; the
+//     two waves of a SIMD run the same schedule on different couts, so one's transform and
+//     memory waits hide under the other's MFMAs.
+//   * K-step = 16 input channels.  Thread (tile, channel) loads its 6x6 patch as 36 4-byte
+//     buffer loads (OOB offset -> 0 = zero padding), transforms it in registers and writes
+//     36 floats of V to LDS V[xi][tile][16 ch], rows XOR-swizzled by 16-B slot so that the
+//     ds_read_b128 fragment reads are conflict-free (the stores are by construction).
 //   * U (transformed filters, built once per model by wino4_weight_kernel) never touches
 //     LDS: it is stored in MFMA-fragment order, so each wave fetches its B fragments with
 //     fully coalesced 1 KiB buffer loads, one K-step ahead.
 //   * One barrier per K-step: the patch of step s+1 is loaded at the top of step s and
-//     transformed into the other LDS buffer in the shadow of the second half of step s's
-//     72 MFMAs.
+//     transformed into the other LDS buffer after the first 40 of step s's 72 MFMAs.
 //   * The pre-activation BatchNorm of conv1 is folded out of the K loop: its scale into the
 //     filters (U = G (g*sc) G^T), its shift into a per-(border class, cout) constant added
 //     in the epilogue (wino4_corr_kernel), so the transform is pure adds and fmas.
-//   * Epilogue: accumulators go through LDS as M[xi][tile][cout] (the whole 144 KiB), each
-//     thread inverse-transforms 4 (tile, cout) pairs and applies BN (+PReLU | + residual)
-//     at the in-image pixels of each tile.
+//   * Epilogue: accumulators go through LDS as M[xi][tile][cout], each thread
+//     inverse-transforms 2 (tile, cout) pairs and applies BN (+PReLU | + residual) at the
+//     in-image pixels of each tile.
 //
-// Lane map of 32x32x2 MFMA: A operand lane (m = l%32, h = l/32) = A[m][k=h], B operand
-// lane (n = l%32, h) = B[k=h][n].  MFMA j (0..7) of a K-step multiplies channel 8h + j:
-// lane (m, h) reads V[xi][m][8h .. 8h+7] with two ds_read_b128 and the matching 8 U values
-// with two 16-B loads (the fragment layout of the F(2x2) kernel, conv_winograd.hip).
+// Lane map of 16x16x4 MFMA: A operand lane l = A[m = l%16][k = l/16], B operand lane l =
+// B[k = l/16][n = l%16], C/D lane l register r = D[4(l/16) + r][l%16].  MFMA j (0..3) of a
+// K-step multiplies channel 4k + j, so lane (m, k) reads V[xi][tile][4k .. 4k+3] with one
+// ds_read_b128 and U[xi][4k .. 4k+3][cout] with one 16-B load.
 #include "frhip_kernels.h"
+
+#include <type_traits>
+
+#ifndef W4_SPLIT0
+#define W4_SPLIT0 4  // xi blocks before the transform, cout half 0
+#endif
+#ifndef W4_SPLIT1
+#define W4_SPLIT1 9  // ... cout half 1 (9 = after the last block)
+#endif
+
+#ifdef W4_MFMA_ONLY  // ablation (tools/w4_variants.sh): K loop of MFMAs + fragment reads only
+#define W4_NO_PATCH
+#define W4_NO_TRANSFORM
+#define W4_NO_ULOAD
+#define W4_NO_BARRIER
+#endif
 
 namespace frhip {
 namespace {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NXI = 36;              // transform elements
@@ -62,9 +76,18 @@ constexpr int KC = 16;               // input channels per K-step
 constexpr int XPW = 9;               // transform elements per wave
 constexpr int VPLANE = WT * KC;      // one xi plane of V: 512 floats
 constexpr int VBUF = NXI * VPLANE;   // one K-step of V: 18432 floats (72 KiB)
-constexpr int MPLANE = WT * 32;      // epilogue: one xi plane of M[tile][cout]
+constexpr int MROW = 33;             // epilogue staging row (32 couts + 1: conflict-free stores)
+constexpr int MPLANE = WT * MROW;    // epilogue: one xi plane of M[tile][cout]
+constexpr int LDS_FLOATS = (2 * VBUF > NXI * MPLANE) ? 2 * VBUF : NXI * MPLANE;
 constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum with it is past the range
-static_assert(NXI * MPLANE <= 2 * VBUF, "epilogue staging must fit the V buffers");
+static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+
+// XOR of the 16-B slot of a V row, by tile: every ds_read_b128 lane group of the 16x16x4 A
+// fragment (tiles t..t+15, channel quad k) then hits 16 distinct slots
+__device__ __forceinline__ int vswz(int tile) {
+  const int q = (tile >> 2) & 3;
+  return (0x1320 >> (4 * q)) & 3;  // [0, 2, 3, 1][q]
+}
 
 __device__ __forceinline__ int wino4_xcd_remap(int bid, int n) {
   const int xcd = bid & 7, loc = bid >> 3;
@@ -95,10 +118,10 @@ __device__ __forceinline__ int canvas_coord(int v, int base, int P, int H, bool 
 }
 
 // 1-D input transform B^T d (6 -> 6)
-__device__ __forceinline__ void bt6(const f2 (&d)[6], f2 (&t)[6]) {
-  const f2 s1 = d[3] + d[4], s2 = d[1] + d[2];
-  const f2 s3 = d[4] - d[3], s4 = d[1] - d[2];
-  const f2 s5 = d[4] - d[2], s6 = d[3] - d[1];
+__device__ __forceinline__ void bt6(const float (&d)[6], float (&t)[6]) {
+  const float s1 = d[3] + d[4], s2 = d[1] + d[2];
+  const float s3 = d[4] - d[3], s4 = d[1] - d[2];
+  const float s5 = d[4] - d[2], s6 = d[3] - d[1];
   t[0] = 4.f * d[0] - 5.f * d[2] + d[4];
   t[1] = s1 - 4.f * s2;
   t[2] = s3 + 4.f * s4;
@@ -118,8 +141,8 @@ __device__ __forceinline__ void at6(const float (&m)[6], float (&o)[4]) {
 }
 
 template <bool CORR, int EPI>
-__global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * VBUF];
+__global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -128,13 +151,13 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
   const int mb = t % p.mblocks, nb = t / p.mblocks;
   const int H = p.H, W = p.W, Cin = p.Cin;
   const int KS = Cin / KC;
-  const int NB32 = p.Cout / 32;
+  const int NB16 = p.Cout / 16;
   const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
 
-  // ---- transform role: thread (tile tl, channel pair cp) ------------------------------
+  // ---- transform role: thread (tile tl, channel ch) -----------------------------------
   // byte offset of patch pixel (i, j) = roff[i] + coff[j]; an out-of-image row or column
   // carries BIGOFF, which puts the sum past the buffer range (load returns 0)
-  const int tl = tid >> 3, cp = tid & 7;
+  const int tl = tid >> 4, ch = tid & 15;
   int roff[6], coff[6];
   {
     const int T = mb * WT + tl;
@@ -146,67 +169,85 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
       const int y = canvas_coord(4 * tr - 1 + i, ir0, p.Pr, H, sep_r, slot);
       roff[i] = (y >= 0 && T < p.ntiles) ? (slot * p.NC * H + y) * W * Cin * 4 : BIGOFF;
       const int x = canvas_coord(4 * tc - 1 + i, ic0, p.Pc, W, sep_c, slot);
-      coff[i] = (x >= 0 && slot < p.NC) ? ((slot * H * W + x) * Cin + 2 * cp) * 4 : BIGOFF;
+      coff[i] = (x >= 0 && slot < p.NC) ? ((slot * H * W + x) * Cin + ch) * 4 : BIGOFF;
     }
   }
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc4(p.x, p.B * H * W * Cin * 4);
   const __amdgpu_buffer_rsrc_t ur = uniform_rsrc4(p.u, NXI * p.Cout * Cin * 4);
-  auto f2u = [](u32x2 v) { return f2{__uint_as_float(v.x), __uint_as_float(v.y)}; };
   auto f4u = [](u32x4 v) {
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
   };
 
-  f2 d[6][6];
+  float d[6][6];
   auto load_patch = [&](int s) {
+#ifdef W4_NO_PATCH
+    if (s > 0) return;
+#endif
     const int so = min(s, KS - 1) * KC * 4;
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
       for (int j = 0; j < 6; ++j)
-        d[i][j] = f2u(__builtin_amdgcn_raw_buffer_load_b64(xr, (int)((unsigned)roff[i] + (unsigned)coff[j]), so, 0));
+        d[i][j] = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(xr, (int)((unsigned)roff[i] + (unsigned)coff[j]), so, 0));
   };
-  // physical float offset of this thread's channel pair inside its V row (16-B slot XOR)
-  const int vslot = (((cp >> 1) ^ ((tl >> 2) & 3)) << 2) + ((cp & 1) << 1);
+  // physical float offset of this thread's channel inside its V row (16-B slot XOR)
+  float* const vdst = lds + tl * KC + ((((ch >> 2) ^ vswz(tl)) << 2) | (ch & 3));
   auto store_v = [&](int buf) {
+#ifdef W4_NO_TRANSFORM
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b < 6; ++b) vdst[buf * VBUF + (6 * a + b) * VPLANE] = d[a][b];
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < 6; ++j) {  // columns: d[.][j] <- (B^T d)[.][j], in place
-      f2 c[6], o[6];
+      float c[6], o[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) c[i] = d[i][j];
       bt6(c, o);
 #pragma unroll
       for (int i = 0; i < 6; ++i) d[i][j] = o[i];
     }
-    float* dst = lds + buf * VBUF + tl * KC + vslot;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
-      f2 v[6];
+      float v[6];
       bt6(d[a], v);
 #pragma unroll
-      for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(dst + (6 * a + b) * VPLANE) = v[b];
+      for (int b = 0; b < 6; ++b) vdst[buf * VBUF + (6 * a + b) * VPLANE] = v[b];
     }
   };
 
-  // ---- GEMM role: wave wid owns xi = 9*wid + x ------------------------------------------
+  // ---- GEMM role: wave (xi group g, cout half hf) ----------------------------------------
+  const int g = wid & 3, hf = wid >> 2;
   int ubase[XPW];
 #pragma unroll
-  for (int x = 0; x < XPW; ++x) ubase[x] = ((((XPW * wid + x) * NB32 + nb) * KS) * 2 * 64 + lane) * 16;
-  float4 u[XPW][2];
+  for (int x = 0; x < XPW; ++x) ubase[x] = ((((XPW * g + x) * NB16 + 2 * nb + hf) * KS) * 64 + lane) * 16;
+  float4 u[XPW];
   auto load_u = [&](int x, int s) {
-    const int so = min(s, KS - 1) * 2 * 64 * 16;
-    u[x][0] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x], so, 0));
-    u[x][1] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x] + 64 * 16, so, 0));
+#ifdef W4_NO_ULOAD
+    if (s > 0) return;
+#endif
+    const int so = min(s, KS - 1) * 64 * 16;
+    u[x] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x], so, 0));
   };
-  const int m = lane & 31, h = lane >> 5;
-  const int rq = (m >> 2) & 3;
-  const float* vrd0 = lds + (XPW * wid) * VPLANE + m * KC + (((2 * h) ^ rq) << 2);
-  const float* vrd1 = lds + (XPW * wid) * VPLANE + m * KC + (((2 * h + 1) ^ rq) << 2);
+  const int fm = lane & 15, fk = lane >> 4;
+  // A fragment of M-block mblk: tile 16*mblk + fm, channel quad fk
+  const float* vrd[2];
+#pragma unroll
+  for (int mblk = 0; mblk < 2; ++mblk) {
+    const int tile = 16 * mblk + fm;
+    vrd[mblk] = lds + (XPW * g) * VPLANE + tile * KC + ((fk ^ vswz(tile)) << 2);
+  }
 
-  floatx16 acc[XPW];
+  floatx4 acc[XPW][2];
 #pragma unroll
   for (int x = 0; x < XPW; ++x)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[x][e] = 0.f;
+    for (int mblk = 0; mblk < 2; ++mblk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[x][mblk][e] = 0.f;
 
   load_patch(0);
 #pragma unroll
@@ -214,91 +255,84 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
   store_v(0);
   __syncthreads();
 
-  // One K-step: MFMAs of xi 0..4 (fragment reads one xi ahead, U of the next step behind),
-  // then -- with the patch loads of step s+1, issued at the top, now 40 MFMAs old -- the
-  // transform of that patch in 12 pieces (6 column passes, 6 row passes + V stores),
-  // pinned between the 32 MFMAs of xi 5..8 so it runs in their shadow; one barrier.
-  auto col_piece = [&](int j) {
-    f2 c[6], o[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) c[i] = d[i][j];
-    bt6(c, o);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) d[i][j] = o[i];
-  };
-  auto row_piece = [&](int a, int buf) {
-    float* dst = lds + buf * VBUF + tl * KC + vslot + 6 * a * VPLANE;
-    f2 v[6];
-    bt6(d[a], v);
-#pragma unroll
-    for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(dst + b * VPLANE) = v[b];
-  };
-  for (int s = 0; s < KS; ++s) {
+  // The two waves of a SIMD (cout halves) run the transform at different points of the
+  // step -- hf 0 after xi block 4, hf 1 after its last block -- so one wave's transform
+  // VALU issues while the other wave keeps the SIMD's MFMA pipe busy.
+  auto step = [&](int s, auto split_c) {
+    constexpr int SPLIT = decltype(split_c)::value;
     const int vb = (s & 1) * VBUF;
     load_patch(s + 1);
+    // the patch loads go out first: the transform that consumes them runs >= 32 MFMAs later
+    __builtin_amdgcn_sched_barrier(0);
     float4 fa[2][2];
-    fa[0][0] = *reinterpret_cast<const float4*>(vrd0 + vb);
-    fa[0][1] = *reinterpret_cast<const float4*>(vrd1 + vb);
-    auto frag_next = [&](int x) {
+    fa[0][0] = *reinterpret_cast<const float4*>(vrd[0] + vb);
+    fa[0][1] = *reinterpret_cast<const float4*>(vrd[1] + vb);
+    auto block = [&](int x) {
       if (x + 1 < XPW) {
-        fa[(x + 1) & 1][0] = *reinterpret_cast<const float4*>(vrd0 + vb + (x + 1) * VPLANE);
-        fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd1 + vb + (x + 1) * VPLANE);
+        fa[(x + 1) & 1][0] = *reinterpret_cast<const float4*>(vrd[0] + vb + (x + 1) * VPLANE);
+        fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd[1] + vb + (x + 1) * VPLANE);
       }
-    };
-    auto mfma = [&](int x, int j) {
-      const float4 q = fa[x & 1][j >> 2];
-      const float4 r = u[x][j >> 2];
-      const float av = (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
-      const float bv = (j & 3) == 0 ? r.x : (j & 3) == 1 ? r.y : (j & 3) == 2 ? r.z : r.w;
-      acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[x], 0, 0, 0);
-    };
+      const float4 b = u[x];
+      const float bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int x = 0; x < 5; ++x) {
-      frag_next(x);
+      for (int mblk = 0; mblk < 2; ++mblk) {
+        const float4 a = fa[x & 1][mblk];
+        const float av[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) mfma(x, j);
+        for (int j = 0; j < 4; ++j)
+          acc[x][mblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc[x][mblk], 0, 0, 0);
+      }
       load_u(x, s + 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int nbuf = (s & 1) ^ 1;
+    };
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int x = 5 + (k >> 3), j = k & 7;
-      if (j == 0) frag_next(x);
-      mfma(x, j);
-      if (j == 7) load_u(x, s + 1);
-      // piece i after MFMA floor(8i/3): 0,2,5,8,10,13,16,18,21,24,26,29
-      if ((3 * k) % 8 < 3) {
-        const int piece = (3 * k) / 8;
-        if (piece < 6)
-          col_piece(piece);
-        else
-          row_piece(piece - 6, nbuf);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
+    for (int x = 0; x < SPLIT; ++x) block(x);
     __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int x = SPLIT; x < XPW; ++x) block(x);
+    store_v((s & 1) ^ 1);
+#ifndef W4_NO_BARRIER
+    __syncthreads();
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if (hf == 0) {
+    for (int s = 0; s < KS; ++s) step(s, std::integral_constant<int, W4_SPLIT0>{});
+  } else {
+    for (int s = 0; s < KS; ++s) step(s, std::integral_constant<int, W4_SPLIT1>{});
   }
 
   // ---- epilogue: inverse transform (+ pre-BN correction) + BN (+PReLU | +residual) ---
+#ifdef W4_NO_EPILOGUE
+  {
+    float sum = 0.f;
 #pragma unroll
-  for (int x = 0; x < XPW; ++x) {
-    float* dst = lds + (XPW * wid + x) * MPLANE + m;
+    for (int x = 0; x < XPW; ++x)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2) + 4 * h) * 32] = acc[x][r];
+      for (int mblk = 0; mblk < 2; ++mblk) sum += acc[x][mblk][0] + acc[x][mblk][1] + acc[x][mblk][2] + acc[x][mblk][3];
+    if (sum == 12345.f) p.y[tid] = sum;
+    return;
   }
-  __syncthreads();
+#endif
+#pragma unroll
+  for (int x = 0; x < XPW; ++x)
+#pragma unroll
+    for (int mblk = 0; mblk < 2; ++mblk) {
+      float* dst = lds + (XPW * g + x) * MPLANE + (16 * mblk + 4 * fk) * MROW + 16 * hf + fm;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[r * MROW] = acc[x][mblk][r];
+    }
+  // per (tile slot q, output pixel): element offset into y / res (-1 outside the images) and
+  // border class; residuals are loaded before the staging barrier so their latency overlaps it
   const int ec = tid & 31;
   const int cout = nb * 32 + ec;
-  const float sc = p.post_scale[cout], sh = p.post_shift[cout];
-  float al = 0.f;
-  if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) al = p.prelu[cout];
-#pragma unroll 1
-  for (int q = 0; q < 4; ++q) {
-    const int tile = (tid >> 5) + 8 * q;
-    const int T = mb * WT + tile;
-    if (T >= p.ntiles) continue;
+  int opix[2][4][4];
+  int ocls[2][4][4];
+  float rv[2][4][4];
+  const __amdgpu_buffer_rsrc_t rr = uniform_rsrc4(p.res, (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
+                                                             ? p.B * H * W * p.Cout * 4 : 0);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int T = mb * WT + (tid >> 5) + 16 * q;
     const int tr = T / p.TWc, tc = T - tr * p.TWc;
     const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
     int orow[4], ocol[4], rcls[4], ccls[4];
@@ -307,17 +341,37 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
       int slot;
       const int y = canvas_coord(4 * tr + i, ir0, p.Pr, H, sep_r, slot);
       const int nimg = slot * p.NC;
-      orow[i] = (y >= 0 && nimg < p.B) ? (nimg * H + y) * W : -1;
+      orow[i] = (y >= 0 && nimg < p.B && T < p.ntiles) ? (nimg * H + y) * W : -1;
       rcls[i] = ((y == 0) ? 1 : 0) | ((y == H - 1) ? 2 : 0);
       const int xx = canvas_coord(4 * tc + i, ic0, p.Pc, W, sep_c, slot);
       ocol[i] = (xx >= 0 && slot < p.NC) ? slot * H * W + xx : -1;
       ccls[i] = ((xx == 0) ? 1 : 0) | ((xx == W - 1) ? 2 : 0);
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int pix = orow[r] + ocol[c];
+        const bool ok = orow[r] >= 0 && ocol[c] >= 0 && pix < p.B * H * W;
+        opix[q][r][c] = ok ? pix * p.Cout + cout : -1;
+        ocls[q][r][c] = rcls[r] * 4 + ccls[c];
+        rv[q][r][c] = 0.f;
+        if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
+          rv[q][r][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ok ? opix[q][r][c] * 4 : BIGOFF, 0, 0));
+      }
+  }
+  __syncthreads();
+  const float sc = p.post_scale[cout], sh = p.post_shift[cout];
+  float al = 0.f;
+  if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) al = p.prelu[cout];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int tile = (tid >> 5) + 16 * q;
     float mv[6][6];
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int b = 0; b < 6; ++b) mv[a][b] = lds[(6 * a + b) * MPLANE + tile * 32 + ec];
+      for (int b = 0; b < 6; ++b) mv[a][b] = lds[(6 * a + b) * MPLANE + tile * MROW + ec];
     float z[6][4];
 #pragma unroll
     for (int a = 0; a < 6; ++a) at6(mv[a], z[a]);
@@ -329,17 +383,15 @@ __global__ __launch_bounds__(256, 1) void wino4_kernel(Wino4Params p) {
       at6(col, o);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (orow[r] < 0 || ocol[c] < 0) continue;
-        const int pix = orow[r] + ocol[c];
-        if (pix >= p.B * H * W) continue;
-        const long long oo = (long long)pix * p.Cout + cout;
+        const int oo = opix[q][r][c];
+        if (oo < 0) continue;
         float v = o[r];
-        if constexpr (CORR) v += p.corr[(rcls[r] * 4 + ccls[c]) * p.Cout + cout];
+        if constexpr (CORR) v += p.corr[ocls[q][r][c] * p.Cout + cout];
         v = v * sc + sh;
         if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
-        if constexpr (EPI == EPI_AFFINE_RES) v += p.res[oo];
+        if constexpr (EPI == EPI_AFFINE_RES) v += rv[q][r][c];
         if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
-          v += p.res[oo];
+          v += rv[q][r][c];
           v = v > 0.f ? v : v * al;
         }
         p.y[oo] = v;
@@ -372,8 +424,8 @@ __global__ void wino4_corr_kernel(const float* __restrict__ w, const float* __re
 }
 
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into
-// the fragment order wino4_kernel reads: [xi][Cout/32][Cin/16][q][lane][4] with
-// lane = 32*(c/8) + cout%32, q = (c%8)/4, element = c%4 for c = cin%16.
+// the fragment order wino4_kernel reads: [xi][Cout/16][Cin/16][lane][4] with
+// lane = 16*(c/4) + cout%16, element = c%4 for c = cin%16.
 __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __restrict__ pre_scale,
                                     float* __restrict__ u, int Cout, int Cin) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -402,17 +454,17 @@ __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __
   for (int a = 0; a < 6; ++a)
 #pragma unroll
     for (int x = 0; x < 3; ++x) tg[a][x] = G[a][0] * g[0][x] + G[a][1] * g[1][x] + G[a][2] * g[2][x];
-  const int NB32 = Cout / 32, KS = Cin / KC;
-  const int nb32 = o >> 5, n = o & 31;
+  const int NB16 = Cout / 16, KS = Cin / KC;
+  const int nb16 = o >> 4, n = o & 15;
   const int s = i / KC, c = i % KC;
-  const int ln = 32 * (c >> 3) + n, q = (c & 7) >> 2, e = c & 3;
+  const int ln = 16 * (c >> 2) + n, e = c & 3;
 #pragma unroll
   for (int a = 0; a < 6; ++a)
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
       const double v = tg[a][0] * G[b][0] + tg[a][1] * G[b][1] + tg[a][2] * G[b][2];
       const int xi = 6 * a + b;
-      u[((((long long)(xi * NB32 + nb32) * KS + s) * 2 + q) * 64 + ln) * 4 + e] = (float)v;
+      u[(((long long)(xi * NB16 + nb16) * KS + s) * 64 + ln) * 4 + e] = (float)v;
     }
 }
 
@@ -461,7 +513,7 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   wino4_canvas(p);
   p.mblocks = (p.ntiles + WT - 1) / WT;
   p.nblocks = p.Cout / 32;
-  const dim3 grid(p.mblocks * p.nblocks), block(256);
+  const dim3 grid(p.mblocks * p.nblocks), block(512);
 #define FR_WINO4_CASE(PRE_, EPI_)                                            \
   if (pre == PRE_ && epi == EPI_) {                                          \
     hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_>), grid, block, 0, s, p);    \

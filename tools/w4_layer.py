@@ -26,7 +26,11 @@ def main():
     ap.add_argument("--cout", type=int, default=256)
     ap.add_argument("--epi", type=int, default=2)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib", default=None, help="alternative libfrhip.so (tools/w4_variants.sh)")
     a = ap.parse_args()
+    if a.lib:
+        from facerecognitionpipeline_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     dev = "cuda"
     g = torch.Generator(device="cpu").manual_seed(1)
     x = torch.randn(a.B, a.H, a.H, a.cin, generator=g).to(dev)
