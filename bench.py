@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--topk", type=int, default=5)
     ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32",
                     help="conv arithmetic: exact f32 MFMA (default, parity path) or opt-in split bf16x3")
-    ap.add_argument("--conv-algorithm", choices=["winograd4", "winograd", "direct"], default="winograd",
+    ap.add_argument("--conv-algorithm", choices=["winograd4", "winograd", "direct"], default="winograd4",
                     help="stride-1 3x3 convs: Winograd F(4x4,3x3), F(2x2,3x3) or the direct implicit GEMM (all f32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")

@@ -1,4 +1,4 @@
-// Winograd F(4x4, 3x3) convolution in f32 on gfx950 MFMA (v_mfma_f32_16x16x4_f32).
+// Winograd F(4x4, 3x3) convolution in f32 on gfx950 MFMA (v_mfma_f32_32x32x2_f32).
 //
 // Replaces the stride-1 3x3 Conv2d of net.BasicBlockIR (res_layer[1] and the stride-1
 // res_layer[4]; reached through `self.model(batch)`, face_embedder.py:157) with the same
@@ -21,41 +21,33 @@
 //
 // Per transform element xi = 6a + b (36 of them) the layer is one GEMM
 //   M_xi[tile][cout] = sum_cin V_xi[tile][cin] * U_xi[cin][cout]
-// and one workgroup owns WT = 32 tiles x 32 couts for all 36.
-//   * 8 waves, two per SIMD: wave w owns xi = 9(w%4) .. 9(w%4)+8 and couts 16(w/4) .. +15,
-//     i.e. 9 x 2 16x16 MFMA blocks (v_mfma_f32_16x16x4_f32), 72 accumulator registers; the
-//     two waves of a SIMD run the same schedule on different couts, so one's transform and
-//     memory waits hide under the other's MFMAs.
-//   * K-step = 16 input channels.  Thread (tile, channel) loads its 6x6 patch as 36 4-byte
-//     buffer loads (OOB offset -> 0 = zero padding), transforms it in registers and writes
-//     36 floats of V to LDS V[xi][tile][16 ch], rows XOR-swizzled by 16-B slot so that the
-//     ds_read_b128 fragment reads are conflict-free (the stores are by construction).
+// and one workgroup owns WT = 32 tiles x 32 couts for all 36.  Its 8 waves are specialised,
+// one of each kind per SIMD:
+//   * 4 MFMA waves: wave c owns xi = 9c .. 9c+8, i.e. 9 32x32 accumulator blocks
+//     (v_mfma_f32_32x32x2_f32, 144 registers), 72 MFMAs per K-step, and nothing else to do
+//     but read its A fragments from LDS and its B fragments (U, one K-step ahead) from L2.
+//   * 4 transform waves: thread (tile, channel pair) loads its 6x6 patch as 36 8-byte buffer
+//     loads (OOB offset -> 0 = zero padding) two K-steps ahead, transforms it with packed
+//     f32 math and writes 36 float2 of V to LDS V[xi][tile][16 ch] (rows XOR-swizzled by
+//     16-B slot: conflict-free ds_read_b128 fragment reads and ds_write_b64 stores).  Its
+//     VALU issues in the gaps of the MFMA wave on the same SIMD.
+//   * K-step = 16 input channels; V is double-buffered, one barrier per K-step.
 //   * U (transformed filters, built once per model by wino4_weight_kernel) never touches
-//     LDS: it is stored in MFMA-fragment order, so each wave fetches its B fragments with
-//     fully coalesced 1 KiB buffer loads, one K-step ahead.
-//   * One barrier per K-step: the patch of step s+1 is loaded at the top of step s and
-//     transformed into the other LDS buffer after the first 40 of step s's 72 MFMAs.
+//     LDS: it is stored in MFMA-fragment order (1 KiB coalesced loads).
 //   * The pre-activation BatchNorm of conv1 is folded out of the K loop: its scale into the
 //     filters (U = G (g*sc) G^T), its shift into a per-(border class, cout) constant added
 //     in the epilogue (wino4_corr_kernel), so the transform is pure adds and fmas.
-//   * Epilogue: accumulators go through LDS as M[xi][tile][cout], each thread
+//   * Epilogue: accumulators go through LDS as M[xi][tile][cout], every thread
 //     inverse-transforms 2 (tile, cout) pairs and applies BN (+PReLU | + residual) at the
-//     in-image pixels of each tile.
+//     in-image pixels of each tile (residuals prefetched before the staging barrier).
 //
-// Lane map of 16x16x4 MFMA: A operand lane l = A[m = l%16][k = l/16], B operand lane l =
-// B[k = l/16][n = l%16], C/D lane l register r = D[4(l/16) + r][l%16].  MFMA j (0..3) of a
-// K-step multiplies channel 4k + j, so lane (m, k) reads V[xi][tile][4k .. 4k+3] with one
-// ds_read_b128 and U[xi][4k .. 4k+3][cout] with one 16-B load.
+// Lane map of 32x32x2 MFMA: A operand lane (m = l%32, h = l/32) = A[m][k=h], B operand lane
+// (n = l%32, h) = B[k=h][n], C/D register r = D[8(r/4) + 4h + r%4][n].  MFMA j (0..7) of a
+// K-step multiplies channel 8h + j: lane (m, h) reads V[xi][m][8h .. 8h+7] with two
+// ds_read_b128 and the matching 8 U values with two 16-B loads.
 #include "frhip_kernels.h"
 
-#include <type_traits>
 
-#ifndef W4_SPLIT0
-#define W4_SPLIT0 4  // xi blocks before the transform, cout half 0
-#endif
-#ifndef W4_SPLIT1
-#define W4_SPLIT1 9  // ... cout half 1 (9 = after the last block)
-#endif
 
 #ifdef W4_MFMA_ONLY  // ablation (tools/w4_variants.sh): K loop of MFMAs + fragment reads only
 #define W4_NO_PATCH
@@ -67,7 +59,9 @@
 namespace frhip {
 namespace {
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NXI = 36;              // transform elements
@@ -82,12 +76,9 @@ constexpr int LDS_FLOATS = (2 * VBUF > NXI * MPLANE) ? 2 * VBUF : NXI * MPLANE;
 constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum with it is past the range
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
 
-// XOR of the 16-B slot of a V row, by tile: every ds_read_b128 lane group of the 16x16x4 A
-// fragment (tiles t..t+15, channel quad k) then hits 16 distinct slots
-__device__ __forceinline__ int vswz(int tile) {
-  const int q = (tile >> 2) & 3;
-  return (0x1320 >> (4 * q)) & 3;  // [0, 2, 3, 1][q]
-}
+// XOR of the 16-B slot of a V row, by tile: every ds_read_b128 lane group of the 32x32x2 A
+// fragment (tiles m, slot 2h + r) then hits 16 distinct slots
+__device__ __forceinline__ int vswz(int tile) { return (tile >> 2) & 3; }
 
 __device__ __forceinline__ int wino4_xcd_remap(int bid, int n) {
   const int xcd = bid & 7, loc = bid >> 3;
@@ -117,11 +108,11 @@ __device__ __forceinline__ int canvas_coord(int v, int base, int P, int H, bool 
   return -1;
 }
 
-// 1-D input transform B^T d (6 -> 6)
-__device__ __forceinline__ void bt6(const float (&d)[6], float (&t)[6]) {
-  const float s1 = d[3] + d[4], s2 = d[1] + d[2];
-  const float s3 = d[4] - d[3], s4 = d[1] - d[2];
-  const float s5 = d[4] - d[2], s6 = d[3] - d[1];
+// 1-D input transform B^T d (6 -> 6), two channels at once (packed f32)
+__device__ __forceinline__ void bt6(const f2 (&d)[6], f2 (&t)[6]) {
+  const f2 s1 = d[3] + d[4], s2 = d[1] + d[2];
+  const f2 s3 = d[4] - d[3], s4 = d[1] - d[2];
+  const f2 s5 = d[4] - d[2], s6 = d[3] - d[1];
   t[0] = 4.f * d[0] - 5.f * d[2] + d[4];
   t[1] = s1 - 4.f * s2;
   t[2] = s3 + 4.f * s4;
@@ -151,154 +142,144 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   const int mb = t % p.mblocks, nb = t / p.mblocks;
   const int H = p.H, W = p.W, Cin = p.Cin;
   const int KS = Cin / KC;
-  const int NB16 = p.Cout / 16;
+  const int NB32 = p.Cout / 32;
   const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
+  const bool mfma_wave = wid < 4;  // waves 0-3 MFMA, 4-7 transform (one of each per SIMD)
 
-  // ---- transform role: thread (tile tl, channel ch) -----------------------------------
-  // byte offset of patch pixel (i, j) = roff[i] + coff[j]; an out-of-image row or column
-  // carries BIGOFF, which puts the sum past the buffer range (load returns 0)
-  const int tl = tid >> 4, ch = tid & 15;
-  int roff[6], coff[6];
-  {
-    const int T = mb * WT + tl;
-    const int tr = T / p.TWc, tc = T - tr * p.TWc;
-    const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      int slot;
-      const int y = canvas_coord(4 * tr - 1 + i, ir0, p.Pr, H, sep_r, slot);
-      roff[i] = (y >= 0 && T < p.ntiles) ? (slot * p.NC * H + y) * W * Cin * 4 : BIGOFF;
-      const int x = canvas_coord(4 * tc - 1 + i, ic0, p.Pc, W, sep_c, slot);
-      coff[i] = (x >= 0 && slot < p.NC) ? ((slot * H * W + x) * Cin + ch) * 4 : BIGOFF;
-    }
-  }
-  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc4(p.x, p.B * H * W * Cin * 4);
-  const __amdgpu_buffer_rsrc_t ur = uniform_rsrc4(p.u, NXI * p.Cout * Cin * 4);
-  auto f4u = [](u32x4 v) {
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-  };
-
-  float d[6][6];
-  auto load_patch = [&](int s) {
-#ifdef W4_NO_PATCH
-    if (s > 0) return;
-#endif
-    const int so = min(s, KS - 1) * KC * 4;
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j)
-        d[i][j] = __uint_as_float(
-            __builtin_amdgcn_raw_buffer_load_b32(xr, (int)((unsigned)roff[i] + (unsigned)coff[j]), so, 0));
-  };
-  // physical float offset of this thread's channel inside its V row (16-B slot XOR)
-  float* const vdst = lds + tl * KC + ((((ch >> 2) ^ vswz(tl)) << 2) | (ch & 3));
-  auto store_v = [&](int buf) {
-#ifdef W4_NO_TRANSFORM
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-      for (int b = 0; b < 6; ++b) vdst[buf * VBUF + (6 * a + b) * VPLANE] = d[a][b];
-    return;
-#endif
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {  // columns: d[.][j] <- (B^T d)[.][j], in place
-      float c[6], o[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) c[i] = d[i][j];
-      bt6(c, o);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) d[i][j] = o[i];
-    }
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      float v[6];
-      bt6(d[a], v);
-#pragma unroll
-      for (int b = 0; b < 6; ++b) vdst[buf * VBUF + (6 * a + b) * VPLANE] = v[b];
-    }
-  };
-
-  // ---- GEMM role: wave (xi group g, cout half hf) ----------------------------------------
-  const int g = wid & 3, hf = wid >> 2;
-  int ubase[XPW];
-#pragma unroll
-  for (int x = 0; x < XPW; ++x) ubase[x] = ((((XPW * g + x) * NB16 + 2 * nb + hf) * KS) * 64 + lane) * 16;
-  float4 u[XPW];
-  auto load_u = [&](int x, int s) {
-#ifdef W4_NO_ULOAD
-    if (s > 0) return;
-#endif
-    const int so = min(s, KS - 1) * 64 * 16;
-    u[x] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x], so, 0));
-  };
-  const int fm = lane & 15, fk = lane >> 4;
-  // A fragment of M-block mblk: tile 16*mblk + fm, channel quad fk
-  const float* vrd[2];
-#pragma unroll
-  for (int mblk = 0; mblk < 2; ++mblk) {
-    const int tile = 16 * mblk + fm;
-    vrd[mblk] = lds + (XPW * g) * VPLANE + tile * KC + ((fk ^ vswz(tile)) << 2);
-  }
-
-  floatx4 acc[XPW][2];
+  floatx16 acc[XPW];
 #pragma unroll
   for (int x = 0; x < XPW; ++x)
 #pragma unroll
-    for (int mblk = 0; mblk < 2; ++mblk)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[x][mblk][e] = 0.f;
+    for (int e = 0; e < 16; ++e) acc[x][e] = 0.f;
 
-  load_patch(0);
+  if (!mfma_wave) {
+    // ---- transform waves: thread (tile tl, channel pair cp) -----------------------------
+    // byte offset of patch pixel (i, j) = roff[i] + coff[j]; an out-of-image row or column
+    // carries BIGOFF, which puts the sum past the buffer range (load returns 0)
+    const int pt = tid - 256;
+    const int tl = pt >> 3, cp = pt & 7;
+    int roff[6], coff[6];
+    {
+      const int T = mb * WT + tl;
+      const int tr = T / p.TWc, tc = T - tr * p.TWc;
+      const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
 #pragma unroll
-  for (int x = 0; x < XPW; ++x) load_u(x, 0);
-  store_v(0);
-  __syncthreads();
-
-  // The two waves of a SIMD (cout halves) run the transform at different points of the
-  // step -- hf 0 after xi block 4, hf 1 after its last block -- so one wave's transform
-  // VALU issues while the other wave keeps the SIMD's MFMA pipe busy.
-  auto step = [&](int s, auto split_c) {
-    constexpr int SPLIT = decltype(split_c)::value;
-    const int vb = (s & 1) * VBUF;
-    load_patch(s + 1);
-    // the patch loads go out first: the transform that consumes them runs >= 32 MFMAs later
-    __builtin_amdgcn_sched_barrier(0);
-    float4 fa[2][2];
-    fa[0][0] = *reinterpret_cast<const float4*>(vrd[0] + vb);
-    fa[0][1] = *reinterpret_cast<const float4*>(vrd[1] + vb);
-    auto block = [&](int x) {
-      if (x + 1 < XPW) {
-        fa[(x + 1) & 1][0] = *reinterpret_cast<const float4*>(vrd[0] + vb + (x + 1) * VPLANE);
-        fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd[1] + vb + (x + 1) * VPLANE);
+      for (int i = 0; i < 6; ++i) {
+        int slot;
+        const int y = canvas_coord(4 * tr - 1 + i, ir0, p.Pr, H, sep_r, slot);
+        roff[i] = (y >= 0 && T < p.ntiles) ? (slot * p.NC * H + y) * W * Cin * 4 : BIGOFF;
+        const int x = canvas_coord(4 * tc - 1 + i, ic0, p.Pc, W, sep_c, slot);
+        coff[i] = (x >= 0 && slot < p.NC) ? ((slot * H * W + x) * Cin + 2 * cp) * 4 : BIGOFF;
       }
-      const float4 b = u[x];
-      const float bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int mblk = 0; mblk < 2; ++mblk) {
-        const float4 a = fa[x & 1][mblk];
-        const float av[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[x][mblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc[x][mblk], 0, 0, 0);
-      }
-      load_u(x, s + 1);
-    };
-#pragma unroll
-    for (int x = 0; x < SPLIT; ++x) block(x);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int x = SPLIT; x < XPW; ++x) block(x);
-    store_v((s & 1) ^ 1);
-#ifndef W4_NO_BARRIER
-    __syncthreads();
+    }
+    const __amdgpu_buffer_rsrc_t xr = uniform_rsrc4(p.x, p.B * H * W * Cin * 4);
+    auto f2u = [](u32x2 v) { return f2{__uint_as_float(v.x), __uint_as_float(v.y)}; };
+    f2 dA[6][6], dB[6][6];
+    auto load_patch = [&](f2 (&d)[6][6], int s) {
+#ifdef W4_NO_PATCH
+      if (s > 1) return;
 #endif
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  if (hf == 0) {
-    for (int s = 0; s < KS; ++s) step(s, std::integral_constant<int, W4_SPLIT0>{});
+      const int so = min(s, KS - 1) * KC * 4;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          d[i][j] = f2u(__builtin_amdgcn_raw_buffer_load_b64(xr, (int)((unsigned)roff[i] + (unsigned)coff[j]), so, 0));
+    };
+    // physical float offset of this thread's channel pair inside its V row (16-B slot XOR)
+    float* const vdst = lds + tl * KC + ((((cp >> 1) ^ vswz(tl)) << 2) | ((cp & 1) << 1));
+    auto store_v = [&](f2 (&d)[6][6], int buf) {
+#ifdef W4_NO_TRANSFORM
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(vdst + buf * VBUF + (6 * a + b) * VPLANE) = d[a][b];
+      return;
+#endif
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {  // columns: d[.][j] <- (B^T d)[.][j], in place
+        f2 c[6], o[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c[i] = d[i][j];
+        bt6(c, o);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) d[i][j] = o[i];
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        f2 v[6];
+        bt6(d[a], v);
+#pragma unroll
+        for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(vdst + buf * VBUF + (6 * a + b) * VPLANE) = v[b];
+      }
+    };
+    // prologue: V(0) into buffer 0, patch 1 in flight; step s: issue patch s+2, transform
+    // patch s+1 (loaded a whole step ago) into buffer (s+1)&1, barrier
+    load_patch(dA, 0);
+    load_patch(dB, 1);
+    store_v(dA, 0);
+    __syncthreads();
+    for (int s = 0; s < KS; s += 2) {  // KS even or not: the tail step's extra work is harmless
+      load_patch(dA, s + 2);
+      store_v(dB, 1);
+#ifndef W4_NO_BARRIER
+      __syncthreads();
+#endif
+      if (s + 1 >= KS) break;
+      load_patch(dB, s + 3);
+      store_v(dA, 0);
+#ifndef W4_NO_BARRIER
+      __syncthreads();
+#endif
+    }
   } else {
-    for (int s = 0; s < KS; ++s) step(s, std::integral_constant<int, W4_SPLIT1>{});
+    // ---- MFMA waves: wave wid owns xi = 9*wid + x ---------------------------------------
+    const __amdgpu_buffer_rsrc_t ur = uniform_rsrc4(p.u, NXI * p.Cout * Cin * 4);
+    auto f4u = [](u32x4 v) {
+      return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+    };
+    int ubase[XPW];
+#pragma unroll
+    for (int x = 0; x < XPW; ++x) ubase[x] = ((((XPW * wid + x) * NB32 + nb) * KS) * 2 * 64 + lane) * 16;
+    float4 u[XPW][2];
+    auto load_u = [&](int x, int s) {
+#ifdef W4_NO_ULOAD
+      if (s > 0) return;
+#endif
+      const int so = min(s, KS - 1) * 2 * 64 * 16;
+      u[x][0] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x], so, 0));
+      u[x][1] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x] + 64 * 16, so, 0));
+    };
+    const int m = lane & 31, h = lane >> 5;
+    const int rq = vswz(m);
+    const float* vrd0 = lds + (XPW * wid) * VPLANE + m * KC + (((2 * h) ^ rq) << 2);
+    const float* vrd1 = lds + (XPW * wid) * VPLANE + m * KC + (((2 * h + 1) ^ rq) << 2);
+#pragma unroll
+    for (int x = 0; x < XPW; ++x) load_u(x, 0);
+    __syncthreads();
+    for (int s = 0; s < KS; ++s) {
+      const int vb = (s & 1) * VBUF;
+      float4 fa[2][2];
+      fa[0][0] = *reinterpret_cast<const float4*>(vrd0 + vb);
+      fa[0][1] = *reinterpret_cast<const float4*>(vrd1 + vb);
+#pragma unroll
+      for (int x = 0; x < XPW; ++x) {
+        if (x + 1 < XPW) {
+          fa[(x + 1) & 1][0] = *reinterpret_cast<const float4*>(vrd0 + vb + (x + 1) * VPLANE);
+          fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd1 + vb + (x + 1) * VPLANE);
+        }
+        const float4 a0 = fa[x & 1][0], a1 = fa[x & 1][1];
+        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float bv[8] = {u[x][0].x, u[x][0].y, u[x][0].z, u[x][0].w,
+                             u[x][1].x, u[x][1].y, u[x][1].z, u[x][1].w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc[x], 0, 0, 0);
+        load_u(x, s + 1);
+      }
+#ifndef W4_NO_BARRIER
+      __syncthreads();
+#endif
+    }
   }
 
   // ---- epilogue: inverse transform (+ pre-BN correction) + BN (+PReLU | +residual) ---
@@ -306,21 +287,11 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   {
     float sum = 0.f;
 #pragma unroll
-    for (int x = 0; x < XPW; ++x)
-#pragma unroll
-      for (int mblk = 0; mblk < 2; ++mblk) sum += acc[x][mblk][0] + acc[x][mblk][1] + acc[x][mblk][2] + acc[x][mblk][3];
+    for (int x = 0; x < XPW; ++x) sum += acc[x][0] + acc[x][5] + acc[x][10] + acc[x][15];
     if (sum == 12345.f) p.y[tid] = sum;
     return;
   }
 #endif
-#pragma unroll
-  for (int x = 0; x < XPW; ++x)
-#pragma unroll
-    for (int mblk = 0; mblk < 2; ++mblk) {
-      float* dst = lds + (XPW * g + x) * MPLANE + (16 * mblk + 4 * fk) * MROW + 16 * hf + fm;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dst[r * MROW] = acc[x][mblk][r];
-    }
   // per (tile slot q, output pixel): element offset into y / res (-1 outside the images) and
   // border class; residuals are loaded before the staging barrier so their latency overlaps it
   const int ec = tid & 31;
@@ -359,6 +330,18 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
           rv[q][r][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ok ? opix[q][r][c] * 4 : BIGOFF, 0, 0));
       }
+  }
+#ifdef W4_NO_BARRIER
+  __syncthreads();
+#endif
+  if (mfma_wave) {
+    const int m = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int x = 0; x < XPW; ++x) {
+      float* dst = lds + (XPW * wid + x) * MPLANE + m;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2) + 4 * h) * MROW] = acc[x][r];
+    }
   }
   __syncthreads();
   const float sc = p.post_scale[cout], sh = p.post_shift[cout];
@@ -424,8 +407,8 @@ __global__ void wino4_corr_kernel(const float* __restrict__ w, const float* __re
 }
 
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into
-// the fragment order wino4_kernel reads: [xi][Cout/16][Cin/16][lane][4] with
-// lane = 16*(c/4) + cout%16, element = c%4 for c = cin%16.
+// the fragment order wino4_kernel reads: [xi][Cout/32][Cin/16][q][lane][4] with
+// lane = 32*(c/8) + cout%32, q = (c%8)/4, element = c%4 for c = cin%16.
 __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __restrict__ pre_scale,
                                     float* __restrict__ u, int Cout, int Cin) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -454,17 +437,17 @@ __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __
   for (int a = 0; a < 6; ++a)
 #pragma unroll
     for (int x = 0; x < 3; ++x) tg[a][x] = G[a][0] * g[0][x] + G[a][1] * g[1][x] + G[a][2] * g[2][x];
-  const int NB16 = Cout / 16, KS = Cin / KC;
-  const int nb16 = o >> 4, n = o & 15;
+  const int NB32 = Cout / 32, KS = Cin / KC;
+  const int nb32 = o >> 5, n = o & 31;
   const int s = i / KC, c = i % KC;
-  const int ln = 16 * (c >> 2) + n, e = c & 3;
+  const int ln = 32 * (c >> 3) + n, q = (c & 7) >> 2, e = c & 3;
 #pragma unroll
   for (int a = 0; a < 6; ++a)
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
       const double v = tg[a][0] * G[b][0] + tg[a][1] * G[b][1] + tg[a][2] * G[b][2];
       const int xi = 6 * a + b;
-      u[(((long long)(xi * NB16 + nb16) * KS + s) * 64 + ln) * 4 + e] = (float)v;
+      u[((((long long)(xi * NB32 + nb32) * KS + s) * 2 + q) * 64 + ln) * 4 + e] = (float)v;
     }
 }
 

@@ -624,6 +624,32 @@ int fr_set_param(fr_handle* h, const char* name, const float* host_data, int64_t
   return FR_OK;
 }
 
+// F(2x2,3x3) filters G g G^T of every eligible conv, built on the device from the arena the
+// first time the algorithm is selected after fr_finalize (16/9 of the 3x3 weights).
+static int ensure_wino2(fr_handle* h) {
+  if (h->wino_arena) return FR_OK;
+  std::vector<ConvW*> wconvs;
+  size_t wfloats = 0;
+  for (auto& b : h->blocks)
+    for (ConvW* c : {&b.conv1, &b.conv2}) {
+      c->wino = nullptr;
+      if (c->w && wino_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
+        wconvs.push_back(c);
+        wfloats += wino_weight_floats(c->cout, c->cin);
+      }
+    }
+  if (!wfloats) return FR_OK;
+  FR_HIP(h, hipMalloc((void**)&h->wino_arena, wfloats * sizeof(float)));
+  size_t off = 0;
+  for (ConvW* c : wconvs) {
+    c->wino = h->wino_arena + off;
+    FR_HIP(h, launch_wino_weights(c->w, c->wino, c->cout, c->cin, nullptr));
+    off += wino_weight_floats(c->cout, c->cin);
+  }
+  FR_HIP(h, hipDeviceSynchronize());
+  return FR_OK;
+}
+
 // F(4x4,3x3) filters of every eligible conv, built on the device from the arena the first
 // time the algorithm is selected after fr_finalize (36/9 = 4x the 3x3 weights).
 static int ensure_wino4(fr_handle* h) {
@@ -762,32 +788,18 @@ int fr_finalize(fr_handle* h) {
   h->arena_floats = pk.buf.size();
   for (auto& f : pk.fix) *f.first = h->arena + f.second;
 
-  // Winograd filters G g G^T of every stride-1 3x3 conv, built on the device from the arena
-  std::vector<ConvW*> wconvs;
-  size_t wfloats = 0;
-  for (auto& b : h->blocks) {
-    for (ConvW* c : {&b.conv1, &b.conv2}) {
-      c->wino = nullptr;
-      if (wino_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
-        wconvs.push_back(c);
-        wfloats += wino_weight_floats(c->cout, c->cin);
-      }
-    }
-  }
+  // Winograd filters are built from the arena on the device for the selected algorithm only
+  // (ensure_wino2 / ensure_wino4); a later fr_set_conv_algorithm builds the other set
   if (h->wino_arena) FR_HIP(h, hipFree(h->wino_arena));
   h->wino_arena = nullptr;
   if (h->wino4_arena) FR_HIP(h, hipFree(h->wino4_arena));
   h->wino4_arena = nullptr;
-  if (wfloats) {
-    FR_HIP(h, hipMalloc((void**)&h->wino_arena, wfloats * sizeof(float)));
-    size_t off = 0;
-    for (ConvW* c : wconvs) {
-      c->wino = h->wino_arena + off;
-      FR_HIP(h, launch_wino_weights(c->w, c->wino, c->cout, c->cin, nullptr));
-      off += wino_weight_floats(c->cout, c->cin);
+  for (auto& b : h->blocks)
+    for (ConvW* c : {&b.conv1, &b.conv2}) {
+      c->wino = nullptr;
+      c->wino4 = nullptr;
+      c->wino4_corr = nullptr;
     }
-    FR_HIP(h, hipDeviceSynchronize());
-  }
 
   // workspace for max_batch crops
   const size_t mb = h->max_batch;
@@ -802,9 +814,12 @@ int fr_finalize(fr_handle* h) {
   if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
   h->finalized = true;
-  if (h->winograd && h->wino_m == 4 && ensure_wino4(h) != FR_OK) {
-    h->finalized = false;
-    return FR_ERR_HIP;
+  if (h->winograd) {
+    const int rc = h->wino_m == 4 ? ensure_wino4(h) : ensure_wino2(h);
+    if (rc != FR_OK) {
+      h->finalized = false;
+      return rc;
+    }
   }
   return FR_OK;
 }
@@ -1119,8 +1134,8 @@ int fr_set_conv_algorithm(fr_handle* h, int algo) {
   if (algo != FR_CONV_DIRECT && algo != FR_CONV_WINOGRAD && algo != FR_CONV_WINOGRAD4)
     return fail(h, FR_ERR_INVALID_ARGUMENT, "algorithm must be FR_CONV_DIRECT, FR_CONV_WINOGRAD or FR_CONV_WINOGRAD4");
   h->winograd = algo != FR_CONV_DIRECT;
-  h->wino_m = algo == FR_CONV_WINOGRAD4 ? 4 : 2;
-  if (h->wino_m == 4 && h->finalized) return ensure_wino4(h);
+  h->wino_m = algo == FR_CONV_WINOGRAD ? 2 : 4;
+  if (h->winograd && h->finalized) return h->wino_m == 4 ? ensure_wino4(h) : ensure_wino2(h);
   return FR_OK;
 }
 

@@ -108,9 +108,9 @@ struct fr_handle {
   bool stream_k = true;
   frhip::Precision prec = frhip::PREC_F32;
   bool winograd = true;          // FR_CONV_WINOGRAD / _WINOGRAD4 for stride-1 3x3 convs
-  int wino_m = 2;                // output tile of the Winograd algorithm: 2 = F(2x2,3x3), 4 = F(4x4,3x3)
-  float* wino_arena = nullptr;   // transformed filters of every eligible conv
-  float* wino4_arena = nullptr;  // F(4x4) filters, built when that algorithm is selected
+  int wino_m = 4;                // output tile of the Winograd algorithm: 4 = F(4x4,3x3) (default), 2 = F(2x2,3x3)
+  float* wino_arena = nullptr;   // F(2x2) filters, built when that algorithm is selected
+  float* wino4_arena = nullptr;  // F(4x4) filters (+ pre-BN corrections), likewise
 
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
   frhip_rt::Detector* det = nullptr;

@@ -52,7 +52,7 @@ class FaceEmbedder:
     def __init__(self, architecture: str = "ir_101", model_path: Optional[str] = None,
                  model_type: str = "adaface", device=None, max_batch: int = 256,
                  state_dict=None, weight_seed: Optional[int] = None, precision: str = "fp32",
-                 conv_algorithm: str = "winograd"):
+                 conv_algorithm: str = "winograd4"):
         self.device = _as_device(device)
         self.model_type = model_type
         self.architecture = architecture

@@ -148,14 +148,15 @@ int fr_detect(fr_handle* h, const uint8_t* frames, int n, int height, int width,
 #define FR_PRECISION_BF16X3 1
 int fr_set_precision(fr_handle* h, int mode);
 
-/* Algorithm of the stride-1 3x3 convs (the bulk of the network's MACs).  Both compute in f32.
- * FR_CONV_WINOGRAD (default): Winograd F(2x2,3x3) -- filters transformed once at
- * fr_finalize, 16 f32-MFMA products per 2x2 tile instead of 36; embeddings within 1e-5 of the
- * CPU reference (tests).  FR_CONV_DIRECT: the implicit-GEMM kernel for every conv.
- * Ignored under FR_PRECISION_BF16X3 (direct split-bf16 everywhere). */
+/* Algorithm of the stride-1 3x3 convs (the bulk of the network's MACs).  All compute in f32.
+ * FR_CONV_WINOGRAD4 (default): Winograd F(4x4,3x3) -- 36 f32-MFMA products per 4x4 tile
+ * instead of 144, filters transformed once (on selection / at fr_finalize), pre-BN folded
+ * into them; embeddings within 1e-5 of the CPU reference (tests).  FR_CONV_WINOGRAD:
+ * F(2x2,3x3), 16 products per 2x2 tile instead of 36.  FR_CONV_DIRECT: the implicit-GEMM
+ * kernel for every conv.  Ignored under FR_PRECISION_BF16X3 (direct split-bf16 everywhere). */
 #define FR_CONV_DIRECT 0
 #define FR_CONV_WINOGRAD 1
-#define FR_CONV_WINOGRAD4 2  /* F(4x4,3x3): 36 products per 4x4 tile (4x fewer than direct); filters built on selection */
+#define FR_CONV_WINOGRAD4 2
 int fr_set_conv_algorithm(fr_handle* h, int algo);
 
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).
