@@ -68,6 +68,15 @@ def test_winograd_non_square_map(m):
     _close(got, ref, rel=REL[m])
 
 
+@pytest.mark.parametrize("B,H,cin,cout", [
+    (96, 14, 256, 256),  # 344 workgroups > CUs: a full round plus a partial one
+    (32, 112, 64, 64),   # 1568 workgroups, Cin = 64 (4 K-steps)
+])
+def test_winograd4_multi_round(B, H, cin, cout):
+    got, ref = _wino_case(B, H, cin, cout, 2, seed=500 + H, m=4)
+    _close(got, ref, rel=REL[4])
+
+
 def test_winograd4_small_cin():
     """F(4x4) K-step is 16 channels: Cin = 16 runs one step (F(2x2) needs Cin % 32)."""
     got, ref = _wino_case(2, 12, 16, 32, 1, seed=420, m=4)
