@@ -113,12 +113,13 @@ __device__ __forceinline__ void bt6(const f2 (&d)[6], f2 (&t)[6]) {
   const f2 s1 = d[3] + d[4], s2 = d[1] + d[2];
   const f2 s3 = d[4] - d[3], s4 = d[1] - d[2];
   const f2 s5 = d[4] - d[2], s6 = d[3] - d[1];
-  t[0] = 4.f * d[0] - 5.f * d[2] + d[4];
-  t[1] = s1 - 4.f * s2;
-  t[2] = s3 + 4.f * s4;
-  t[3] = s5 + 2.f * s6;
-  t[4] = s5 - 2.f * s6;
-  t[5] = 4.f * d[1] - 5.f * d[3] + d[5];
+  // 14 ops (8 adds, 6 fmas); the nesting keeps t0/t5 at two fmas each
+  t[0] = 4.f * d[0] + (-5.f * d[2] + d[4]);
+  t[1] = -4.f * s2 + s1;
+  t[2] = 4.f * s4 + s3;
+  t[3] = 2.f * s6 + s5;
+  t[4] = -2.f * s6 + s5;
+  t[5] = 4.f * d[1] + (-5.f * d[3] + d[5]);
 }
 
 // 1-D output transform A^T m (6 -> 4)
@@ -503,8 +504,11 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
     return hipGetLastError();                                                \
   }
   if (pre && !p.corr) return hipErrorInvalidValue;
-  FR_WINO4_CASE(true, EPI_AFFINE_PRELU)
-  FR_WINO4_CASE(false, EPI_AFFINE_RES)
+  FR_WINO4_CASE(true, EPI_AFFINE_PRELU)   // IR conv1: pre-BN, BN, PReLU
+  FR_WINO4_CASE(false, EPI_AFFINE_RES)    // IR conv2: BN + identity shortcut
+  FR_WINO4_CASE(false, EPI_AFFINE_PRELU)  // SCRFD conv + BN + ReLU (zero slopes)
+  FR_WINO4_CASE(false, EPI_AFFINE)        // SCRFD conv + BN / bias
+  FR_WINO4_CASE(false, EPI_AFFINE_RES_PRELU)  // SCRFD BasicBlock conv2 + BN + add + ReLU
 #undef FR_WINO4_CASE
   return hipErrorInvalidValue;
 }

@@ -72,6 +72,28 @@ struct Detector {
 
 void detector_destroy(Detector* d) { delete d; }
 
+void detector_convs(Detector* d, std::vector<ConvW*>& out) {
+  if (!d) return;
+  out.push_back(&d->stem1);
+  out.push_back(&d->stem2);
+  for (auto& st : d->blocks)
+    for (auto& b : st) {
+      out.push_back(&b.conv1);
+      out.push_back(&b.conv2);
+      out.push_back(&b.down);
+    }
+  for (int i = 0; i < 3; ++i) {
+    out.push_back(&d->lateral[i]);
+    out.push_back(&d->fpn[i]);
+    out.push_back(&d->head[i]);
+    for (auto& t : d->tower[i]) out.push_back(&t);
+  }
+  for (int i = 0; i < 2; ++i) {
+    out.push_back(&d->down[i]);
+    out.push_back(&d->pafpn[i]);
+  }
+}
+
 std::map<std::string, size_t> detector_schema() {
   std::map<std::string, size_t> m;
   auto conv = [&](const std::string& k, int o, int i, int kh) { m[k] = (size_t)o * i * kh * kh; };

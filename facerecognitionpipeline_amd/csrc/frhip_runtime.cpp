@@ -304,8 +304,12 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // stage and the 128-channel residual convs, 8-wave 128x128 for the 1x1 shortcuts,
   // 8-wave 256x128 for every other 3x3 conv and the FC.
   const bool wino_epi = (epi == EPI_AFFINE_PRELU && cw.pre_scale) || (epi == EPI_AFFINE_RES && !cw.pre_scale && res_H == p.Ho);
+  // F(4x4) also takes the detector's epilogues (no pre-BN; residual of the output's shape)
+  const bool wino4_epi = wino_epi || (!cw.pre_scale && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE ||
+                                                        ((epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU) &&
+                                                         (res_H == 0 || res_H == p.Ho) && (res_W == 0 || res_W == p.Wo))));
   // Winograd F(4x4,3x3) for the stride-1 3x3 convs (f32 parity path only)
-  if (h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 && wino_epi) {
+  if (h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 && wino4_epi) {
     Wino4Params wp{};
     wp.x = x;
     wp.u = cw.wino4;
@@ -656,8 +660,11 @@ static int ensure_wino4(fr_handle* h) {
   if (h->wino4_arena) return FR_OK;
   std::vector<ConvW*> wconvs;
   size_t wfloats = 0;
+  std::vector<ConvW*> all;
   for (auto& b : h->blocks)
-    for (ConvW* c : {&b.conv1, &b.conv2}) {
+    for (ConvW* c : {&b.conv1, &b.conv2}) all.push_back(c);
+  detector_convs(h->det, all);
+  for (ConvW* c : all) {
       c->wino4 = nullptr;
       c->wino4_corr = nullptr;
       if (c->w && wino4_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
@@ -695,6 +702,10 @@ int fr_finalize(fr_handle* h) {
   if (h->detector) {
     int rc = detector_finalize(h);
     if (rc) return rc;
+    // the detector's stride-1 3x3 convs run on the F(4x4) kernel as well (run_conv)
+    if (h->wino4_arena) FR_HIP(h, hipFree(h->wino4_arena));
+    h->wino4_arena = nullptr;
+    if (h->winograd && h->wino_m == 4 && (rc = ensure_wino4(h)) != FR_OK) return rc;
     h->finalized = true;
     return FR_OK;
   }

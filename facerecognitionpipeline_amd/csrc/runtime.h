@@ -47,6 +47,8 @@ struct ProfEvent {
 
 struct Detector;  // detector.cpp
 void detector_destroy(Detector* d);
+// every conv of the detector (for the Winograd filter builds); no-op for d == nullptr
+void detector_convs(Detector* d, std::vector<ConvW*>& out);
 
 }  // namespace frhip_rt
 
