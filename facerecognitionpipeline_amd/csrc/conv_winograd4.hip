@@ -276,6 +276,15 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc[x], 0, 0, 0);
         load_u(x, s + 1);
+#ifdef W4_PIN_U
+        // keep the next step's U loads here, a whole step ahead of their use (the scheduler
+        // otherwise sinks them to the end of the step, right before the barrier)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+#ifdef W4_PIN_U2
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+#endif
       }
 #ifndef W4_NO_BARRIER
       __syncthreads();
@@ -328,8 +337,10 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         opix[q][r][c] = ok ? pix * p.Cout + cout : -1;
         ocls[q][r][c] = rcls[r] * 4 + ccls[c];
         rv[q][r][c] = 0.f;
+#ifndef W4_EPI_NORES
         if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
           rv[q][r][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ok ? opix[q][r][c] * 4 : BIGOFF, 0, 0));
+#endif
       }
   }
 #ifdef W4_NO_BARRIER
@@ -378,7 +389,11 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
           v += rv[q][r][c];
           v = v > 0.f ? v : v * al;
         }
+#ifdef W4_EPI_NOSTORE
+        if (v == 12345.f) p.y[oo] = v;
+#else
         p.y[oo] = v;
+#endif
       }
     }
   }

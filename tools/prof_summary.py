@@ -45,6 +45,14 @@ def layers(arch, B):
     return out
 
 
+def wino4_tiles(h, B):
+    """4x4 canvas tiles of an h x h layer at batch B (mirrors wino4_canvas in conv_winograd4.hip)."""
+    P = h if h % 4 == 0 else h + 1
+    NC = 1 if P % 4 == 0 else min(4 if P % 2 else 2, B)
+    crow = (B + NC - 1) // NC
+    return ((NC * P + 3) // 4) * ((crow * P + 3) // 4)
+
+
 def align(rows, L, B):
     """[(layer name, row)] for every B-image forward found in a sorted kernel-trace."""
     stem_grid = B * 112 * 256
@@ -126,9 +134,12 @@ def main():
         kn = kname.get(name, "")
         family = "winograd" if "wino" in kn else ("direct" if is_conv else "other")
         exec_flop = flop
-        if family == "winograd":  # 16 products per (padded) 2x2 tile instead of 36 per 4 pixels
+        if family == "winograd":
             hw = int(name.split("@")[1].split("/")[0])
-            exec_flop = flop * 16.0 / 36.0 * (2 * ((hw + 1) // 2)) ** 2 / hw ** 2
+            if "wino4" in kn:  # 36 products per 4x4 canvas tile (launch_wino4's canvas) instead of 144
+                exec_flop = flop * 36.0 / 144.0 * wino4_tiles(hw, a.batch) * 16 / (a.batch * hw * hw)
+            else:  # F(2x2): 16 products per (padded) 2x2 tile instead of 36 per 4 pixels
+                exec_flop = flop * 16.0 / 36.0 * (2 * ((hw + 1) // 2)) ** 2 / hw ** 2
         row["kernel"] = kn.split("(")[0][:60]
         row["family"] = family
         row["exec_tflops"] = exec_flop / (avg_ns * 1e-9) / 1e12 if avg_ns else 0.0
