@@ -98,14 +98,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc4(const void* ptr,
 // Canvas coordinate v (a row or a column) of a tile whose origin lies in image slot `base`:
 // returns the in-image coordinate and sets `slot` (base or base + 1), or -1 for padding.
 __device__ __forceinline__ int canvas_coord(int v, int base, int P, int H, bool sep, int& slot) {
-  const int y = v - base * P;
-  slot = base;
-  if (y >= 0 && y < H) return y;
-  if (sep && y >= P && y - P < H) {
-    slot = base + 1;
-    return y - P;
-  }
-  return -1;
+  const int y = v - base * P, y1 = y - P;  // branch-free: selects only
+  const bool in0 = (unsigned)y < (unsigned)H;
+  const bool in1 = sep && (unsigned)y1 < (unsigned)H;
+  slot = base + (in1 ? 1 : 0);
+  return in0 ? y : (in1 ? y1 : -1);
 }
 
 // 1-D input transform B^T d (6 -> 6), two channels at once (packed f32)
@@ -309,6 +306,8 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   int opix[2][4][4];
   int ocls[2][4][4];
   float rv[2][4][4];
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc4(p.y, p.B * H * W * p.Cout * 4);
+  const __amdgpu_buffer_rsrc_t cr = uniform_rsrc4(p.corr, CORR ? 16 * p.Cout * 4 : 0);
   const __amdgpu_buffer_rsrc_t rr = uniform_rsrc4(p.res, (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
                                                              ? p.B * H * W * p.Cout * 4 : 0);
 #pragma unroll
@@ -334,12 +333,12 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       for (int c = 0; c < 4; ++c) {
         const int pix = orow[r] + ocol[c];
         const bool ok = orow[r] >= 0 && ocol[c] >= 0 && pix < p.B * H * W;
-        opix[q][r][c] = ok ? pix * p.Cout + cout : -1;
+        opix[q][r][c] = ok ? (pix * p.Cout + cout) * 4 : BIGOFF;  // byte offset; BIGOFF = dropped
         ocls[q][r][c] = rcls[r] * 4 + ccls[c];
         rv[q][r][c] = 0.f;
 #ifndef W4_EPI_NORES
         if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
-          rv[q][r][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ok ? opix[q][r][c] * 4 : BIGOFF, 0, 0));
+          rv[q][r][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, opix[q][r][c], 0, 0));
 #endif
       }
   }
@@ -379,9 +378,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int oo = opix[q][r][c];
-        if (oo < 0) continue;
         float v = o[r];
-        if constexpr (CORR) v += p.corr[ocls[q][r][c] * p.Cout + cout];
+        if constexpr (CORR)
+          v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(cr, (ocls[q][r][c] * p.Cout + cout) * 4, 0, 0));
         v = v * sc + sh;
         if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
         if constexpr (EPI == EPI_AFFINE_RES) v += rv[q][r][c];
@@ -390,10 +389,10 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
           v = v > 0.f ? v : v * al;
         }
 #ifdef W4_EPI_NOSTORE
-        if (v == 12345.f) p.y[oo] = v;
-#else
-        p.y[oo] = v;
+        if (v == 12345.f)
 #endif
+        // branch-free: stores of pixels outside the images carry BIGOFF and are dropped
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), yr, oo, 0, 0);
       }
     }
   }
