@@ -61,6 +61,7 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -70,6 +71,9 @@ constexpr int KC = 16;               // input channels per K-step
 constexpr int XPW = 9;               // transform elements per wave
 constexpr int VPLANE = WT * KC;      // one xi plane of V: 512 floats
 constexpr int VBUF = NXI * VPLANE;   // one K-step of V: 18432 floats (72 KiB)
+constexpr int BF_PLANE = WT * 8;     // BF: one xi plane of V hi (or lo): 32 tiles x 16 bf16 = 256 words
+constexpr int BF_LO = NXI * BF_PLANE;  // BF: words from a hi plane to its lo plane
+static_assert(2 * BF_LO <= VBUF, "BF V buffer must fit the f32 one");
 constexpr int MROW = 33;             // epilogue staging row (32 couts + 1: conflict-free stores)
 constexpr int MPLANE = WT * MROW;    // epilogue: one xi plane of M[tile][cout]
 constexpr int LDS_FLOATS = (2 * VBUF > NXI * MPLANE) ? 2 * VBUF : NXI * MPLANE;
@@ -129,7 +133,12 @@ __device__ __forceinline__ void at6(const float (&m)[6], float (&o)[4]) {
   o[3] = m12 + 8.f * m34 + m[5];
 }
 
-template <bool CORR, int EPI>
+// BF (opt-in FR_PRECISION_BF16X3): V and U are split into bf16 hi + lo (x = hi + lo to ~2^-16),
+// the MFMA waves run v_mfma_f32_32x32x16_bf16 on lo*hi + hi*lo + hi*hi with f32 accumulation
+// (the lo*lo term, ~2^-16 relative, is dropped): 3 MFMAs of 32 cycles per transform element
+// and K-step instead of 8 of 64.  V in LDS: per xi plane hi [32 tiles][16 ch] bf16 then the lo
+// planes; 32-B rows, 16-B slot XOR (m >> 3) & 1.
+template <bool CORR, int EPI, bool BF>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
 
@@ -186,12 +195,25 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     };
     // physical float offset of this thread's channel pair inside its V row (16-B slot XOR)
     float* const vdst = lds + tl * KC + ((((cp >> 1) ^ vswz(tl)) << 2) | ((cp & 1) << 1));
+    // BF: the pair as one word of 2 bf16 in the hi plane (lo plane BF_LO words later)
+    unsigned* const vdst_bf = reinterpret_cast<unsigned*>(lds) + tl * 8 + ((((cp >> 2) ^ ((tl >> 3) & 1)) << 2) | (cp & 3));
+    auto put_v = [&](int buf, int xi, f2 v) {
+      if constexpr (BF) {
+        const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y;
+        const __bf16 l0 = (__bf16)(v.x - (float)h0), l1 = (__bf16)(v.y - (float)h1);
+        unsigned* d0 = vdst_bf + buf * VBUF + xi * BF_PLANE;
+        d0[0] = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+        d0[BF_LO] = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+      } else {
+        *reinterpret_cast<f2*>(vdst + buf * VBUF + xi * VPLANE) = v;
+      }
+    };
     auto store_v = [&](f2 (&d)[6][6], int buf) {
 #ifdef W4_NO_TRANSFORM
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
-        for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(vdst + buf * VBUF + (6 * a + b) * VPLANE) = d[a][b];
+        for (int b = 0; b < 6; ++b) put_v(buf, 6 * a + b, d[a][b]);
       return;
 #endif
 #pragma unroll
@@ -208,7 +230,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         f2 v[6];
         bt6(d[a], v);
 #pragma unroll
-        for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(vdst + buf * VBUF + (6 * a + b) * VPLANE) = v[b];
+        for (int b = 0; b < 6; ++b) put_v(buf, 6 * a + b, v[b]);
       }
     };
     // prologue: V(0) into buffer 0, patch 1 in flight; step s: issue patch s+2, transform
@@ -250,8 +272,11 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     };
     const int m = lane & 31, h = lane >> 5;
     const int rq = vswz(m);
-    const float* vrd0 = lds + (XPW * wid) * VPLANE + m * KC + (((2 * h) ^ rq) << 2);
-    const float* vrd1 = lds + (XPW * wid) * VPLANE + m * KC + (((2 * h + 1) ^ rq) << 2);
+    // f32: the two 16-B slots of channels 8h..8h+7; BF: the hi and the lo slot of those channels
+    const float* vrd0 = BF ? lds + (XPW * wid) * BF_PLANE + m * 8 + ((h ^ ((m >> 3) & 1)) << 2)
+                           : lds + (XPW * wid) * VPLANE + m * KC + (((2 * h) ^ rq) << 2);
+    const float* vrd1 = BF ? vrd0 + BF_LO : lds + (XPW * wid) * VPLANE + m * KC + (((2 * h + 1) ^ rq) << 2);
+    constexpr int XPL = BF ? BF_PLANE : VPLANE;  // floats between consecutive xi planes
 #pragma unroll
     for (int x = 0; x < XPW; ++x) load_u(x, 0);
     __syncthreads();
@@ -263,15 +288,23 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
       for (int x = 0; x < XPW; ++x) {
         if (x + 1 < XPW) {
-          fa[(x + 1) & 1][0] = *reinterpret_cast<const float4*>(vrd0 + vb + (x + 1) * VPLANE);
-          fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd1 + vb + (x + 1) * VPLANE);
+          fa[(x + 1) & 1][0] = *reinterpret_cast<const float4*>(vrd0 + vb + (x + 1) * XPL);
+          fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd1 + vb + (x + 1) * XPL);
         }
         const float4 a0 = fa[x & 1][0], a1 = fa[x & 1][1];
-        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const float bv[8] = {u[x][0].x, u[x][0].y, u[x][0].z, u[x][0].w,
-                             u[x][1].x, u[x][1].y, u[x][1].z, u[x][1].w};
+        if constexpr (BF) {
+          const bf16x8 ah = __builtin_bit_cast(bf16x8, a0), al = __builtin_bit_cast(bf16x8, a1);
+          const bf16x8 bh = __builtin_bit_cast(bf16x8, u[x][0]), bl = __builtin_bit_cast(bf16x8, u[x][1]);
+          acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[x], 0, 0, 0);
+          acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[x], 0, 0, 0);
+          acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[x], 0, 0, 0);
+        } else {
+          const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          const float bv[8] = {u[x][0].x, u[x][0].y, u[x][0].z, u[x][0].w,
+                               u[x][1].x, u[x][1].y, u[x][1].z, u[x][1].w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc[x], 0, 0, 0);
+          for (int j = 0; j < 8; ++j) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc[x], 0, 0, 0);
+        }
         load_u(x, s + 1);
 #ifdef W4_PIN_U
         // keep the next step's U loads here, a whole step ahead of their use (the scheduler
@@ -466,7 +499,35 @@ __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __
     }
 }
 
+// bf16 hi/lo split of the transformed filters, fragment order of the BF kernel:
+// [xi][Cout/32][Cin/16][hl][lane][8] bf16 with lane = 32*(c/8) + cout%32, element c%8.
+__global__ void wino4_weight_bf_kernel(const float* __restrict__ u32, unsigned short* __restrict__ ubf, int Cout,
+                                       int Cin) {
+  // u32 is the f32 fragment-ordered U ([xi][Cout/32][Cin/16][q][lane][4], q = (c%8)/4)
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = (long long)NXI * Cout * Cin;
+  if (idx >= n) return;
+  const int e4 = (int)(idx & 3);
+  const int ln = (int)((idx >> 2) & 63);
+  const int q = (int)((idx >> 8) & 1);
+  const long long blk = idx >> 9;  // (xi, nb32, s)
+  const float v = u32[idx];
+  const __bf16 hi = (__bf16)v;
+  const __bf16 lo = (__bf16)(v - (float)hi);
+  const long long o = ((blk * 2) * 64 + ln) * 8 + 4 * q + e4;  // hi; lo is 64*8 later
+  ubf[o] = __builtin_bit_cast(unsigned short, hi);
+  ubf[o + 64 * 8] = __builtin_bit_cast(unsigned short, lo);
+}
+
 }  // namespace
+
+hipError_t launch_wino4_weights_bf(const float* u32, void* ubf, int Cout, int Cin, hipStream_t s) {
+  if (Cout % 32 || Cin % KC) return hipErrorInvalidValue;
+  const long long n = (long long)NXI * Cout * Cin;
+  hipLaunchKernelGGL(wino4_weight_bf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u32,
+                     static_cast<unsigned short*>(ubf), Cout, Cin);
+  return hipGetLastError();
+}
 
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
   return kh == 3 && kw == 3 && stride == 1 && pad == 1 && Cin % KC == 0 && Cin >= KC && Cout % 32 == 0 && Cout >= 32;
@@ -502,7 +563,7 @@ void wino4_canvas(Wino4Params& p) {
   p.ntiles = TRc * p.TWc;
 }
 
-hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
+hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s, bool bf) {
   Wino4Params p = p0;
   if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
       (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF ||
@@ -512,10 +573,13 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   p.mblocks = (p.ntiles + WT - 1) / WT;
   p.nblocks = p.Cout / 32;
   const dim3 grid(p.mblocks * p.nblocks), block(512);
-#define FR_WINO4_CASE(PRE_, EPI_)                                            \
-  if (pre == PRE_ && epi == EPI_) {                                          \
-    hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_>), grid, block, 0, s, p);    \
-    return hipGetLastError();                                                \
+#define FR_WINO4_CASE(PRE_, EPI_)                                                 \
+  if (pre == PRE_ && epi == EPI_) {                                               \
+    if (bf)                                                                       \
+      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, true>), grid, block, 0, s, p);  \
+    else                                                                          \
+      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, false>), grid, block, 0, s, p); \
+    return hipGetLastError();                                                     \
   }
   if (pre && !p.corr) return hipErrorInvalidValue;
   FR_WINO4_CASE(true, EPI_AFFINE_PRELU)   // IR conv1: pre-BN, BN, PReLU

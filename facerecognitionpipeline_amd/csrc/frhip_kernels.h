@@ -117,7 +117,10 @@ void wino4_canvas(Wino4Params& p);
 // corr[16][Cout] (pre_shift through the in-image taps of each border class).
 hipError_t launch_wino4_weights(const float* w, const float* pre_scale, const float* pre_shift, float* u,
                                 float* corr, int Cout, int Cin, hipStream_t s);
-hipError_t launch_wino4(const Wino4Params& p, bool pre, Epi epi, hipStream_t s);
+// bf = true: the opt-in split-bf16 arithmetic; p.u then points at launch_wino4_weights_bf output
+hipError_t launch_wino4(const Wino4Params& p, bool pre, Epi epi, hipStream_t s, bool bf = false);
+// bf16 hi/lo split of an f32 launch_wino4_weights filter set (same byte size)
+hipError_t launch_wino4_weights_bf(const float* u32, void* ubf, int Cout, int Cin, hipStream_t s);
 
 // uint8 RGB HWC 112x112 -> (BGR, LUT normalise) -> conv3x3 3->64 -> BN -> PReLU, NHWC f32.
 hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64,

@@ -309,10 +309,11 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
                                                         ((epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU) &&
                                                          (res_H == 0 || res_H == p.Ho) && (res_W == 0 || res_W == p.Wo))));
   // Winograd F(4x4,3x3) for the stride-1 3x3 convs (f32 parity path only)
-  if (h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 && wino4_epi) {
+  const bool w4bf = h->prec == PREC_BF16X3 && cw.wino4_bf;
+  if (h->winograd && h->wino_m == 4 && (h->prec == PREC_F32 || w4bf) && cw.wino4 && wino4_epi) {
     Wino4Params wp{};
     wp.x = x;
-    wp.u = cw.wino4;
+    wp.u = w4bf ? static_cast<const float*>(cw.wino4_bf) : cw.wino4;
     wp.corr = cw.wino4_corr;
     wp.y = y;
     wp.pre_scale = cw.pre_scale;
@@ -328,10 +329,11 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.Cout = cw.cout;
     Wino4Params cv = wp;
     wino4_canvas(cv);
-    // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
-    const double exec = 2.0 * 36.0 * cv.ntiles * (double)cw.cin * cw.cout;
+    // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair (bf16x3: 3 bf16 MFMA
+    // products each)
+    const double exec = (w4bf ? 3.0 : 1.0) * 2.0 * 36.0 * cv.ntiles * (double)cw.cin * cw.cout;
     ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
-    hipError_t e = launch_wino4(wp, cw.pre_scale != nullptr, epi, s);
+    hipError_t e = launch_wino4(wp, cw.pre_scale != nullptr, epi, s, w4bf);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
     return FR_OK;
   }
@@ -689,6 +691,54 @@ static int ensure_wino4(fr_handle* h) {
   return FR_OK;
 }
 
+// bf16 hi/lo split of every F(4x4) filter set (FR_PRECISION_BF16X3 with FR_CONV_WINOGRAD4)
+static int ensure_wino4_bf(fr_handle* h) {
+  if (h->wino4_bf_arena || !h->wino4_arena) return FR_OK;
+  std::vector<ConvW*> all;
+  for (auto& b : h->blocks)
+    for (ConvW* c : {&b.conv1, &b.conv2}) all.push_back(c);
+  detector_convs(h->det, all);
+  size_t bytes = 0;
+  for (ConvW* c : all)
+    if (c->wino4) bytes += wino4_weight_floats(c->cout, c->cin) * sizeof(float);
+  if (!bytes) return FR_OK;
+  FR_HIP(h, hipMalloc(&h->wino4_bf_arena, bytes));
+  size_t off = 0;
+  for (ConvW* c : all) {
+    c->wino4_bf = nullptr;
+    if (!c->wino4) continue;
+    c->wino4_bf = static_cast<char*>(h->wino4_bf_arena) + off;
+    FR_HIP(h, launch_wino4_weights_bf(c->wino4, c->wino4_bf, c->cout, c->cin, nullptr));
+    off += wino4_weight_floats(c->cout, c->cin) * sizeof(float);
+  }
+  FR_HIP(h, hipDeviceSynchronize());
+  return FR_OK;
+}
+
+static void drop_wino4(fr_handle* h) {
+  (void)hipFree(h->wino4_arena);
+  (void)hipFree(h->wino4_bf_arena);
+  h->wino4_arena = nullptr;
+  h->wino4_bf_arena = nullptr;
+  std::vector<ConvW*> all;
+  for (auto& b : h->blocks)
+    for (ConvW* c : {&b.conv1, &b.conv2}) all.push_back(c);
+  detector_convs(h->det, all);
+  for (ConvW* c : all) {
+    c->wino4 = nullptr;
+    c->wino4_corr = nullptr;
+    c->wino4_bf = nullptr;
+  }
+}
+
+static int ensure_winograd(fr_handle* h) {
+  if (!h->winograd) return FR_OK;
+  if (h->wino_m == 2) return ensure_wino2(h);
+  int rc = ensure_wino4(h);
+  if (rc == FR_OK && h->prec == PREC_BF16X3) rc = ensure_wino4_bf(h);
+  return rc;
+}
+
 int fr_finalize(fr_handle* h) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -703,9 +753,8 @@ int fr_finalize(fr_handle* h) {
     int rc = detector_finalize(h);
     if (rc) return rc;
     // the detector's stride-1 3x3 convs run on the F(4x4) kernel as well (run_conv)
-    if (h->wino4_arena) FR_HIP(h, hipFree(h->wino4_arena));
-    h->wino4_arena = nullptr;
-    if (h->winograd && h->wino_m == 4 && (rc = ensure_wino4(h)) != FR_OK) return rc;
+    drop_wino4(h);
+    if (h->wino_m == 4 && (rc = ensure_winograd(h)) != FR_OK) return rc;
     h->finalized = true;
     return FR_OK;
   }
@@ -803,14 +852,11 @@ int fr_finalize(fr_handle* h) {
   // (ensure_wino2 / ensure_wino4); a later fr_set_conv_algorithm builds the other set
   if (h->wino_arena) FR_HIP(h, hipFree(h->wino_arena));
   h->wino_arena = nullptr;
-  if (h->wino4_arena) FR_HIP(h, hipFree(h->wino4_arena));
-  h->wino4_arena = nullptr;
-  for (auto& b : h->blocks)
-    for (ConvW* c : {&b.conv1, &b.conv2}) {
-      c->wino = nullptr;
-      c->wino4 = nullptr;
-      c->wino4_corr = nullptr;
-    }
+  drop_wino4(h);
+  for (auto& b : h->blocks) {
+    b.conv1.wino = nullptr;
+    b.conv2.wino = nullptr;
+  }
 
   // workspace for max_batch crops
   const size_t mb = h->max_batch;
@@ -826,7 +872,7 @@ int fr_finalize(fr_handle* h) {
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
   h->finalized = true;
   if (h->winograd) {
-    const int rc = h->wino_m == 4 ? ensure_wino4(h) : ensure_wino2(h);
+    const int rc = ensure_winograd(h);
     if (rc != FR_OK) {
       h->finalized = false;
       return rc;
@@ -1136,6 +1182,7 @@ int fr_set_precision(fr_handle* h, int mode) {
   if (mode != FR_PRECISION_F32 && mode != FR_PRECISION_BF16X3)
     return fail(h, FR_ERR_INVALID_ARGUMENT, "precision must be FR_PRECISION_F32 or FR_PRECISION_BF16X3");
   h->prec = mode == FR_PRECISION_BF16X3 ? PREC_BF16X3 : PREC_F32;
+  if (h->finalized) return ensure_winograd(h);
   return FR_OK;
 }
 
@@ -1146,7 +1193,7 @@ int fr_set_conv_algorithm(fr_handle* h, int algo) {
     return fail(h, FR_ERR_INVALID_ARGUMENT, "algorithm must be FR_CONV_DIRECT, FR_CONV_WINOGRAD or FR_CONV_WINOGRAD4");
   h->winograd = algo != FR_CONV_DIRECT;
   h->wino_m = algo == FR_CONV_WINOGRAD ? 2 : 4;
-  if (h->winograd && h->finalized) return h->wino_m == 4 ? ensure_wino4(h) : ensure_wino2(h);
+  if (h->finalized) return ensure_winograd(h);
   return FR_OK;
 }
 
@@ -1330,6 +1377,53 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
   (void)hipFree(u);
   if (e == hipSuccess) e = se;
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd4: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+int frt_conv2d_winograd4_bf(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
+                        const float* pre_scale, const float* pre_shift, const float* post_scale,
+                        const float* post_shift, const float* prelu, const float* res, int epi, void* stream) {
+  if (!wino4_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
+      (epi == EPI_AFFINE_PRELU && (!pre_scale || !pre_shift || !prelu)) || (epi == EPI_AFFINE_RES && (pre_scale || !res)) ||
+      !post_scale || !post_shift || B < 1 || H < 1 || W < 1)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4_bf: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  float* u = nullptr;
+  if (hipMalloc((void**)&u, (wino4_weight_floats(cout, cin) + 16 * (size_t)cout) * sizeof(float)) != hipSuccess)
+    return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4_bf: allocation failed");
+  float* corr = pre_scale ? u + wino4_weight_floats(cout, cin) : nullptr;
+  hipError_t e = launch_wino4_weights(w, pre_scale, pre_shift, u, corr, cout, cin, s);
+  if (e == hipSuccess) {
+    Wino4Params p{};
+    p.x = x;
+    p.u = u;
+    p.corr = corr;
+    p.y = y;
+    p.pre_scale = pre_scale;
+    p.pre_shift = pre_shift;
+    p.post_scale = post_scale;
+    p.post_shift = post_shift;
+    p.prelu = prelu;
+    p.res = res;
+    p.B = B;
+    p.H = H;
+    p.W = W;
+    p.Cin = cin;
+    p.Cout = cout;
+    void* ubf = nullptr;
+    e = hipMalloc(&ubf, wino4_weight_floats(cout, cin) * sizeof(float));
+    if (e == hipSuccess) e = launch_wino4_weights_bf(u, ubf, cout, cin, s);
+    if (e == hipSuccess) {
+      p.u = static_cast<const float*>(ubf);
+      e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s, true);
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(ubf);
+  }
+  const hipError_t se = hipStreamSynchronize(s);
+  (void)hipFree(u);
+  if (e == hipSuccess) e = se;
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd4_bf: ") + hipGetErrorString(e));
   return FR_OK;
 }
 

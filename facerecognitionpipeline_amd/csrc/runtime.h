@@ -28,6 +28,7 @@ struct ConvW {
   float* wino = nullptr;  // Winograd-transformed filters (stride-1 3x3 only), or null
   float* wino4 = nullptr; // F(4x4,3x3) transformed filters (built on demand), or null
   float* wino4_corr = nullptr;  // [16][Cout] pre-BN shift correction of the F(4x4) path (conv1 only)
+  void* wino4_bf = nullptr;     // bf16 hi/lo split of wino4 (FR_PRECISION_BF16X3), built on demand
   int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
 };
 
@@ -113,6 +114,7 @@ struct fr_handle {
   int wino_m = 4;                // output tile of the Winograd algorithm: 4 = F(4x4,3x3) (default), 2 = F(2x2,3x3)
   float* wino_arena = nullptr;   // F(2x2) filters, built when that algorithm is selected
   float* wino4_arena = nullptr;  // F(4x4) filters (+ pre-BN corrections), likewise
+  void* wino4_bf_arena = nullptr;  // their bf16 hi/lo split, built when bf16x3 is selected
 
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
   frhip_rt::Detector* det = nullptr;
@@ -134,6 +136,7 @@ struct fr_handle {
     (void)hipFree(arena);
     (void)hipFree(wino_arena);
     (void)hipFree(wino4_arena);
+    (void)hipFree(wino4_bf_arena);
     for (auto p : act) (void)hipFree(p);
     (void)hipFree(sc_buf);
     (void)hipFree(partial);

@@ -35,7 +35,11 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
 int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                         const float* pre_scale, const float* pre_shift, const float* post_scale,
                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
-/* Winograd F(4x4,3x3) (the FR_CONV_WINOGRAD4 path), same arguments; cin % 16 == 0, cout % 32 == 0. */
+/* Winograd F(4x4,3x3) (the FR_CONV_WINOGRAD4 path), same arguments; cin % 16 == 0, cout % 32 == 0.
+ * The _bf variant runs the opt-in bf16x3 arithmetic of that kernel (FR_PRECISION_BF16X3). */
+int frt_conv2d_winograd4_bf(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
+                            const float* pre_scale, const float* pre_shift, const float* post_scale,
+                            const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                          const float* pre_scale, const float* pre_shift, const float* post_scale,
                          const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
