@@ -161,6 +161,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 
   if (!mfma_wave) {
     // ---- transform waves: thread (tile tl, channel pair cp) -----------------------------
+#ifdef W4_TPRIO
+    __builtin_amdgcn_s_setprio(W4_TPRIO);
+#endif
     // byte offset of patch pixel (i, j) = roff[i] + coff[j]; an out-of-image row or column
     // carries BIGOFF, which puts the sum past the buffer range (load returns 0)
     const int pt = tid - 256;
@@ -254,6 +257,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     }
   } else {
     // ---- MFMA waves: wave wid owns xi = 9*wid + x ---------------------------------------
+#ifdef W4_PRIO
+    __builtin_amdgcn_s_setprio(W4_PRIO);  // MFMA waves win issue arbitration on their SIMD
+#endif
     const __amdgpu_buffer_rsrc_t ur = uniform_rsrc4(p.u, NXI * p.Cout * Cin * 4);
     auto f4u = [](u32x4 v) {
       return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
@@ -281,6 +287,10 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     for (int x = 0; x < XPW; ++x) load_u(x, 0);
     __syncthreads();
     for (int s = 0; s < KS; ++s) {
+#ifdef W4_MFMA_IDLE  // ablation: MFMA waves only keep the barrier cadence
+      __syncthreads();
+      continue;
+#endif
       const int vb = (s & 1) * VBUF;
       float4 fa[2][2];
       fa[0][0] = *reinterpret_cast<const float4*>(vrd0 + vb);
@@ -292,7 +302,12 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
           fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd1 + vb + (x + 1) * XPL);
         }
         const float4 a0 = fa[x & 1][0], a1 = fa[x & 1][1];
+#ifdef W4_NO_MFMA
+        acc[x][0] += a0.x + a1.y + u[x][0].x;
+        if constexpr (false) {
+#else
         if constexpr (BF) {
+#endif
           const bf16x8 ah = __builtin_bit_cast(bf16x8, a0), al = __builtin_bit_cast(bf16x8, a1);
           const bf16x8 bh = __builtin_bit_cast(bf16x8, u[x][0]), bl = __builtin_bit_cast(bf16x8, u[x][1]);
           acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[x], 0, 0, 0);

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -23,6 +24,8 @@
 #include "../../include/frhip_testing.h"
 #include "frhip_kernels.h"
 #include "runtime.h"
+
+#include <cstdlib>
 
 using namespace frhip;
 using namespace frhip_rt;
@@ -735,7 +738,12 @@ static int ensure_winograd(fr_handle* h) {
   if (!h->winograd) return FR_OK;
   if (h->wino_m == 2) return ensure_wino2(h);
   int rc = ensure_wino4(h);
-  if (rc == FR_OK && h->prec == PREC_BF16X3) rc = ensure_wino4_bf(h);
+  // bf16x3 on the F(4x4) kernel is measured slower than the direct split-bf16 kernel (the
+  // Winograd kernel is bound by its transform and load paths, not by the MFMA pipe, and the
+  // hi/lo split adds to the former: DESIGN.md §4), so bf16x3 runs the direct kernel unless
+  // FRHIP_WINO4_BF=1 asks for the Winograd variant
+  const char* ev = getenv("FRHIP_WINO4_BF");
+  if (rc == FR_OK && h->prec == PREC_BF16X3 && ev && ev[0] == '1') rc = ensure_wino4_bf(h);
   return rc;
 }
 

@@ -153,8 +153,8 @@ int fr_set_precision(fr_handle* h, int mode);
  * instead of 144, filters transformed once (on selection / at fr_finalize), pre-BN folded
  * into them; embeddings within 1e-5 of the CPU reference (tests).  FR_CONV_WINOGRAD:
  * F(2x2,3x3), 16 products per 2x2 tile instead of 36.  FR_CONV_DIRECT: the implicit-GEMM
- * kernel for every conv.  Under FR_PRECISION_BF16X3 the F(4x4) kernel runs split-bf16 too (its
- * filters split into bf16 hi/lo on selection); F(2x2) is not used there (direct split-bf16). */
+ * kernel for every conv.  FR_PRECISION_BF16X3 runs the direct split-bf16 kernel (faster there than
+ * the split-bf16 F(4x4) variant, which FRHIP_WINO4_BF=1 selects for experiments). */
 #define FR_CONV_DIRECT 0
 #define FR_CONV_WINOGRAD 1
 #define FR_CONV_WINOGRAD4 2
