@@ -25,8 +25,6 @@
 #include "frhip_kernels.h"
 #include "runtime.h"
 
-#include <cstdlib>
-
 using namespace frhip;
 using namespace frhip_rt;
 
