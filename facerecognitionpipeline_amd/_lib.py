@@ -48,6 +48,8 @@ _SIGNATURES = {
     "fr_detect": (_I, [_P, _P, _I, _I, _I, ctypes.c_float, _I, _P, _P, _P]),
     "fr_set_precision": (_I, [_P, _I]),
     "fr_set_conv_algorithm": (_I, [_P, _I]),
+    "fr_set_graph_batch": (_I, [_P, _I]),
+    "fr_graph_count": (_I, [_P, ctypes.POINTER(ctypes.c_int)]),
     "fr_profile_enable": (_I, [_P, _I]),
     "fr_profile_kernel": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
@@ -251,6 +253,15 @@ class Handle:
         if algo not in algos:
             raise ValueError(f"conv_algorithm must be one of {sorted(algos)}")
         check(self._lib.fr_set_conv_algorithm(self.h, algos[algo]), self.h)
+
+    def set_graph_batch(self, max_n: int) -> None:
+        """Replay forwards of n <= max_n crops as captured hipGraphs (0 disables)."""
+        check(self._lib.fr_set_graph_batch(self.h, int(max_n)), self.h)
+
+    def graph_count(self) -> int:
+        c = ctypes.c_int()
+        check(self._lib.fr_graph_count(self.h, ctypes.byref(c)), self.h)
+        return c.value
 
     # -- profiling ---------------------------------------------------------
     def profile_enable(self, on: bool = True) -> None:

@@ -416,7 +416,56 @@ int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int norma
   return FR_OK;
 }
 
+void clear_graphs(fr_handle* h) {
+  for (auto& g : h->graphs) (void)hipGraphExecDestroy(g.exec);
+  h->graphs.clear();
+}
+
+// Capture forward_chunk(in_stage -> emb_stage) for n crops as a hipGraph.  Every pointer and
+// size a launch takes is fixed for (n, normalize) once the handle is finalised, and the
+// stream-K tickets re-arm themselves, so the graph replays without updates.
+int capture_graph(fr_handle* h, int n, int normalize) {
+  if (!h->cap_stream) FR_HIP(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+  FR_HIP(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+  const int rc = forward_chunk(h, h->in_stage, n, h->emb_stage, normalize, h->cap_stream);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(h->cap_stream, &g);
+  if (rc != FR_OK || e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc != FR_OK ? rc : fail(h, FR_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+  }
+  hipGraphExec_t ex = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (ei != hipSuccess) return fail(h, FR_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(ei));
+  h->graphs.push_back({n, normalize, ex});
+  return FR_OK;
+}
+
+// One forward of n <= max_batch crops from in_stage to emb_stage.  Small n (the serving
+// pattern: a frame's faces, or batch 1) is launch-bound, so with fr_set_graph_batch those
+// forwards replay a captured graph: the first call for an n runs eagerly (loading every
+// kernel), then captures; later calls are one hipGraphLaunch.
+int forward_staged(fr_handle* h, int n, int normalize, hipStream_t s) {
+  if (n > h->graph_max_n || h->prof) return forward_chunk(h, h->in_stage, n, h->emb_stage, normalize, s);
+  for (const auto& g : h->graphs)
+    if (g.n == n && g.normalize == normalize) {
+      FR_HIP(h, hipGraphLaunch(g.exec, s));
+      return FR_OK;
+    }
+  const int rc = forward_chunk(h, h->in_stage, n, h->emb_stage, normalize, s);
+  if (rc != FR_OK) return rc;
+  return capture_graph(h, n, normalize);
+}
+
 int embed_device(fr_handle* h, const uint8_t* rgb, int n, float* out, int normalize, hipStream_t s) {
+  if (n > 0 && n <= h->graph_max_n && !h->prof) {
+    FR_HIP(h, hipMemcpyAsync(h->in_stage, rgb, (size_t)n * 112 * 112 * 3, hipMemcpyDeviceToDevice, s));
+    const int rc = forward_staged(h, n, normalize, s);
+    if (rc != FR_OK) return rc;
+    FR_HIP(h, hipMemcpyAsync(out, h->emb_stage, (size_t)n * 512 * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return FR_OK;
+  }
   for (int off = 0; off < n; off += h->max_batch) {
     const int bn = std::min(h->max_batch, n - off);
     int rc = forward_chunk(h, rgb + (size_t)off * 112 * 112 * 3, bn, out + (size_t)off * 512, normalize, s);
@@ -755,6 +804,7 @@ int fr_finalize(fr_handle* h) {
   }
   if (!missing.empty()) return fail(h, FR_ERR_MISSING_PARAM, "Missing key(s) in state_dict: " + missing);
   DeviceGuard dg(h->device);
+  clear_graphs(h);
   if (h->detector) {
     int rc = detector_finalize(h);
     if (rc) return rc;
@@ -914,7 +964,7 @@ int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width
     const int bn = std::min(h->max_batch, n - off);
     FR_HIP(h, hipMemcpyAsync(h->in_stage, rgb + (size_t)off * 112 * 112 * 3, (size_t)bn * 112 * 112 * 3,
                              hipMemcpyHostToDevice, s));
-    int rc = forward_chunk(h, h->in_stage, bn, h->emb_stage, normalize, s);
+    int rc = forward_staged(h, bn, normalize, s);
     if (rc) return rc;
     FR_HIP(h, hipMemcpyAsync(out + (size_t)off * 512, h->emb_stage, (size_t)bn * 512 * sizeof(float),
                              hipMemcpyDeviceToHost, s));
@@ -1188,6 +1238,7 @@ int fr_set_precision(fr_handle* h, int mode) {
   if (mode != FR_PRECISION_F32 && mode != FR_PRECISION_BF16X3)
     return fail(h, FR_ERR_INVALID_ARGUMENT, "precision must be FR_PRECISION_F32 or FR_PRECISION_BF16X3");
   h->prec = mode == FR_PRECISION_BF16X3 ? PREC_BF16X3 : PREC_F32;
+  clear_graphs(h);
   if (h->finalized) return ensure_winograd(h);
   return FR_OK;
 }
@@ -1199,7 +1250,26 @@ int fr_set_conv_algorithm(fr_handle* h, int algo) {
     return fail(h, FR_ERR_INVALID_ARGUMENT, "algorithm must be FR_CONV_DIRECT, FR_CONV_WINOGRAD or FR_CONV_WINOGRAD4");
   h->winograd = algo != FR_CONV_DIRECT;
   h->wino_m = algo == FR_CONV_WINOGRAD ? 2 : 4;
+  clear_graphs(h);
   if (h->finalized) return ensure_winograd(h);
+  return FR_OK;
+}
+
+int fr_set_graph_batch(fr_handle* h, int max_n) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (h->detector) return fail(h, FR_ERR_STATE, "this handle is a detector (scrfd_10g)");
+  if (max_n < 0 || max_n > h->max_batch) return fail(h, FR_ERR_INVALID_ARGUMENT, "max_n must be in [0, max_batch]");
+  DeviceGuard dg(h->device);
+  h->graph_max_n = max_n;
+  clear_graphs(h);
+  return FR_OK;
+}
+
+int fr_graph_count(fr_handle* h, int* count) {
+  if (!h || !count) return fail(h, FR_ERR_INVALID_ARGUMENT, "NULL argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  *count = (int)h->graphs.size();
   return FR_OK;
 }
 

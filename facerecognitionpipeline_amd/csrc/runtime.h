@@ -119,6 +119,16 @@ struct fr_handle {
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
   frhip_rt::Detector* det = nullptr;
 
+  // hipGraph replay of small forwards (fr_set_graph_batch): one executable graph per
+  // (n, normalize), captured on cap_stream from in_stage to emb_stage
+  struct GraphEntry {
+    int n, normalize;
+    hipGraphExec_t exec;
+  };
+  int graph_max_n = 0;
+  hipStream_t cap_stream = nullptr;
+  std::vector<GraphEntry> graphs;
+
   // profiling
   bool prof = false;
   std::vector<frhip_rt::ProfEvent> events;
@@ -133,6 +143,8 @@ struct fr_handle {
       (void)hipEventDestroy(e.b);
     }
     for (auto e : pool) (void)hipEventDestroy(e);
+    for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
+    if (cap_stream) (void)hipStreamDestroy(cap_stream);
     (void)hipFree(arena);
     (void)hipFree(wino_arena);
     (void)hipFree(wino4_arena);

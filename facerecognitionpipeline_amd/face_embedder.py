@@ -52,7 +52,7 @@ class FaceEmbedder:
     def __init__(self, architecture: str = "ir_101", model_path: Optional[str] = None,
                  model_type: str = "adaface", device=None, max_batch: int = 256,
                  state_dict=None, weight_seed: Optional[int] = None, precision: str = "fp32",
-                 conv_algorithm: str = "winograd4"):
+                 conv_algorithm: str = "winograd4", graph_batch: int = 16):
         self.device = _as_device(device)
         self.model_type = model_type
         self.architecture = architecture
@@ -81,6 +81,10 @@ class FaceEmbedder:
         self.model.set_precision(precision)
         self.conv_algorithm = conv_algorithm
         self.model.set_conv_algorithm(conv_algorithm)
+        # serving-sized forwards (n <= graph_batch: batch 1, one frame's faces) replay a
+        # captured hipGraph instead of ~100 individual launches (bit-identical results)
+        self.graph_batch = min(int(graph_batch), max_batch)
+        self.model.set_graph_batch(self.graph_batch)
         self.input_size = INPUT_SIZE
         # face_embedder.py:60-61 (AdaFace) and :86-87 (ArcFace)
         self.mean, self.std = (0.5, 0.5) if model_type == "adaface" else (127.5, 127.5)

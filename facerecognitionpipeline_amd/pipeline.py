@@ -10,11 +10,16 @@ frame uploaded once:
     embed + match every valid face in one fr_embed_match  ->  top-k per face
 
 Detections come from any detector with the reference ``FaceDetector.detect``
-contract (``face_recognition.py:31-48``); SCRFD itself is not rebuilt yet.
+contract (``face_recognition.py:31-48``), the GPU SCRFD ``FaceDetector`` included.
+``MatchBatcher`` batches concurrent single-face requests the same way.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Sequence
+import queue
+import threading
+import time
+from concurrent.futures import Future
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -73,3 +78,100 @@ class RecognitionPipeline:
             out[i]["matches"] = m
             out[i]["recognized"] = bool(m) and m[0][2] >= self.similarity_threshold
         return out
+
+
+class MatchBatcher:
+    """Dynamic batching of concurrent ``match_single_face`` calls.
+
+    The reference server handles each request on its own Flask thread
+    (``threaded=True``, ``face_recognition_server.py:1102``) and every one of them
+    runs a batch-1 embed + search (``:321-323`` -> ``face_matcher.py:52-58``).  Here
+    those threads call :meth:`match_single_face` (or :meth:`submit`) and one worker
+    thread gathers whatever is pending -- up to ``max_batch`` crops, waiting at most
+    ``max_wait_ms`` after the first -- into ONE ``FaceMatcher.match_faces`` call, i.e.
+    one ``fr_embed_match`` (a replayed hipGraph when the batch is small).  Each
+    caller gets exactly what ``match_single_face`` would return: the embedder is
+    batch-invariant and the top-k kernel is exact with the same tie order, so the
+    first ``top_k`` of a larger k are the top-``top_k``.
+
+    Errors keep the reference behaviour per request: a crop of the wrong shape raises
+    ``ValueError`` in the calling thread before it is queued; a failure of the batched
+    call is raised in every caller of that batch.
+    """
+
+    def __init__(self, matcher, max_batch: int = 64, max_wait_ms: float = 2.0):
+        if max_batch < 1:
+            raise ValueError("max_batch must be >= 1")
+        self.matcher = matcher
+        self.max_batch = int(max_batch)
+        self.max_wait = max(0.0, float(max_wait_ms)) / 1000.0
+        self.batches: List[int] = []  # size of every batch run (for tests and monitoring)
+        self._q: "queue.Queue[Optional[Tuple[np.ndarray, int, Future]]]" = queue.Queue()
+        self._closed = False
+        self._lock = threading.Lock()
+        self._worker = threading.Thread(target=self._run, name="frhip-match-batcher", daemon=True)
+        self._worker.start()
+
+    def submit(self, face_image: np.ndarray, top_k: int = 5) -> Future:
+        self.matcher.embedder._check_shape(face_image)
+        fut: Future = Future()
+        item = (np.ascontiguousarray(face_image, dtype=np.uint8), int(top_k), fut)
+        with self._lock:
+            if self._closed:
+                raise RuntimeError("MatchBatcher is closed")
+            self._q.put(item)
+        return fut
+
+    def match_single_face(self, face_image: np.ndarray, top_k: int = 5) -> List[Tuple[str, str, float]]:
+        return self.submit(face_image, top_k).result()
+
+    def close(self) -> None:
+        """Finish every queued request, then stop the worker."""
+        with self._lock:
+            if self._closed:
+                return
+            self._closed = True
+            self._q.put(None)
+        self._worker.join()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _run(self) -> None:
+        stop = False
+        while not stop:
+            item = self._q.get()
+            if item is None:
+                break
+            batch = [item]
+            deadline = time.monotonic() + self.max_wait
+            while len(batch) < self.max_batch:
+                try:
+                    nxt = self._q.get(timeout=max(0.0, deadline - time.monotonic()))
+                except queue.Empty:
+                    break
+                if nxt is None:
+                    stop = True
+                    break
+                batch.append(nxt)
+            self._serve(batch)
+
+    def _serve(self, batch) -> None:
+        self.batches.append(len(batch))
+        try:
+            n_rows = len(self.matcher.gallery.students)
+            ks = [_slice_len(n_rows, k) for _, k, _ in batch]
+            kmax = max(ks)
+            if kmax == 0:
+                res = [[] for _ in batch]
+            else:
+                res = self.matcher.match_faces([f for f, _, _ in batch], top_k=kmax)
+        except BaseException as e:  # every caller of this batch sees the failure
+            for _, _, fut in batch:
+                fut.set_exception(e)
+            return
+        for (_, _, fut), r, k in zip(batch, res, ks):
+            fut.set_result(r[:k])

@@ -160,6 +160,14 @@ int fr_set_precision(fr_handle* h, int mode);
 #define FR_CONV_WINOGRAD4 2
 int fr_set_conv_algorithm(fr_handle* h, int algo);
 
+/* hipGraph replay of small forwards.  With max_n > 0 (<= max_batch), every embed of n <= max_n
+ * crops (fr_embed, fr_embed_host, fr_embed_match) runs its ~100 kernel launches as one captured
+ * graph: the first call for an n runs eagerly and captures, later calls replay (same kernels and
+ * arguments, so bit-identical results).  0 (default) disables; changing the precision, the conv
+ * algorithm or the weights drops the captured graphs.  fr_graph_count reports how many exist. */
+int fr_set_graph_batch(fr_handle* h, int max_n);
+int fr_graph_count(fr_handle* h, int* count);
+
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).
  * enable=1 starts recording; fr_profile_read synchronises and returns, since the
  * last read: summed milliseconds and algorithmic FLOPs of the conv_mfma launches,

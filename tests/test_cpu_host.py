@@ -172,3 +172,51 @@ def test_gallery_delta_replays_random_mutations(tmp_path):
         gm._mark_synced(new_ids)
     gm._touch()  # a bulk change (load / load_backup) always falls back to a full upload
     assert gm.pending_delta() is None
+
+
+def test_match_batcher_routes_concurrent_requests():
+    """MatchBatcher (pipeline.py) on a stand-in matcher: every concurrent caller gets its own
+    result, cut to its own top_k with slice semantics; requests are batched; a wrong-shape
+    crop raises ValueError in the caller; a failing batch fails each of its callers."""
+    import threading
+    import types
+
+    from facerecognitionpipeline_amd.pipeline import MatchBatcher
+
+    class FakeMatcher:
+        def __init__(self):
+            self.gallery = types.SimpleNamespace(students={f"S{i}": None for i in range(6)})
+            self.embedder = types.SimpleNamespace(_check_shape=self._check)
+            self.fail = False
+            self.gate = threading.Event()
+
+        @staticmethod
+        def _check(f):
+            if f.shape != (112, 112, 3):
+                raise ValueError("bad shape")
+
+        def match_faces(self, faces, top_k=5):
+            self.gate.wait(5)
+            if self.fail:
+                raise RuntimeError("device failure")
+            # "match" = the crop's tag pixel, repeated top_k times with descending scores
+            return [[(f"S{int(f[0, 0, 0])}", "n", 1.0 - j / 10) for j in range(top_k)] for f in faces]
+
+    fm = FakeMatcher()
+    with MatchBatcher(fm, max_batch=8, max_wait_ms=20) as mb:
+        crops = [np.full((112, 112, 3), i % 6, np.uint8) for i in range(24)]
+        ks = [1 + i % 4 for i in range(23)] + [-2]  # -2: slice semantics -> 4 of 6 rows
+        futs = [mb.submit(c, k) for c, k in zip(crops, ks)]
+        fm.gate.set()
+        for i, (f, k) in enumerate(zip(futs, ks)):
+            r = f.result(timeout=10)
+            assert len(r) == len(range(6)[:k])
+            assert all(x[0] == f"S{i % 6}" for x in r)
+        assert sum(mb.batches) == 24 and max(mb.batches) <= 8 and len(mb.batches) < 24
+        with pytest.raises(ValueError):
+            mb.submit(np.zeros((50, 50, 3), np.uint8))
+        fm.fail = True
+        with pytest.raises(RuntimeError, match="device failure"):
+            mb.match_single_face(crops[0], 3)
+    with pytest.raises(RuntimeError, match="closed"):
+        mb.submit(crops[0])

@@ -1,0 +1,117 @@
+"""Serving-sized forwards: hipGraph replay (fr_set_graph_batch) and MatchBatcher.
+
+Graph replay runs the same kernels with the same arguments as the eager path, so the
+bar is bit-identical embeddings and match results.  MatchBatcher must give each
+concurrent caller exactly what FaceMatcher.match_single_face gives it.
+"""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from facerecognitionpipeline_amd import weights as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def embedder():
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    return FaceEmbedder(architecture="ir_101", model_path="synthetic", max_batch=64, graph_batch=0)
+
+
+def test_graph_replay_is_bit_identical_to_eager(embedder):
+    h = embedder.model
+    crops = torch.from_numpy(W.synthetic_crops(20, seed=W.CROP_SEED_GALLERY)).cuda()
+    eager = {}
+    for n in (1, 3, 8, 20):
+        eager[n] = embedder.embed_tensor(crops[:n]).clone()
+    h.set_graph_batch(8)
+    try:
+        assert h.graph_count() == 0
+        for rep in range(3):  # rep 0 runs eagerly and captures; reps 1-2 replay
+            for n in (1, 3, 8, 20):
+                got = embedder.embed_tensor(crops[:n])
+                assert torch.equal(got, eager[n]), (n, rep, (got - eager[n]).abs().max().item())
+        assert h.graph_count() == 3  # n = 1, 3, 8; n = 20 > max_n stays eager
+        # un-normalised embeddings are a separate graph
+        raw = embedder.embed_tensor(crops[:3], normalize=False)
+        assert h.graph_count() == 4
+        assert torch.equal(embedder.embed_tensor(crops[:3], normalize=False), raw)
+        assert torch.allclose(raw / raw.norm(dim=1, keepdim=True), eager[3], atol=1e-6)
+        # different inputs through the same graph (a crop's row in the batch can move the
+        # last bits, as it does eagerly: the batch-invariance bar elsewhere is 1e-6)
+        other = torch.flip(crops[:3], dims=[0]).contiguous()
+        assert (embedder.embed_tensor(other) - eager[3].flip(0)).abs().max().item() < 1e-6
+        h.set_graph_batch(0)
+        other_eager = embedder.embed_tensor(other).clone()
+        h.set_graph_batch(8)
+        assert torch.equal(embedder.embed_tensor(other), other_eager)
+        # switching the conv algorithm drops the graphs; results stay within the parity bar
+        h.set_conv_algorithm("winograd")
+        assert h.graph_count() == 0
+        w2 = embedder.embed_tensor(crops[:3])
+        assert (w2 - eager[3]).abs().max().item() < 1e-5
+        h.set_conv_algorithm("winograd4")
+        assert torch.equal(embedder.embed_tensor(crops[:3]), eager[3])
+    finally:
+        h.set_graph_batch(0)
+        h.set_conv_algorithm("winograd4")
+
+
+def test_graph_replay_embed_match_and_host_path(embedder, tmp_path):
+    from facerecognitionpipeline_amd.face_matcher import FaceMatcher
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+
+    base = W.synthetic_crops(16, seed=W.CROP_SEED_GALLERY)
+    gm = GalleryManager(gallery_path=str(tmp_path / "g.npz"), device="cuda:0", verbose=False)
+    ref = embedder.extract_embeddings_batch(list(base))
+    for i in range(16):
+        gm.add_student(f"S{i}", f"N{i}", ref[i])
+    fm = FaceMatcher(embedder=embedder, gallery=gm)
+    probes = W.probe_crops(base, 6)
+    eager = fm.match_faces(list(probes), top_k=3)
+    single_eager = [fm.match_single_face(p, top_k=3) for p in probes[:2]]
+    embedder.model.set_graph_batch(8)
+    try:
+        for _ in range(2):
+            assert fm.match_faces(list(probes), top_k=3) == eager
+            assert [fm.match_single_face(p, top_k=3) for p in probes[:2]] == single_eager
+        assert [r[0][0] for r in eager] == [f"S{i}" for i in range(6)]
+    finally:
+        embedder.model.set_graph_batch(0)
+
+
+def test_match_batcher_equals_match_single_face(embedder, tmp_path):
+    from facerecognitionpipeline_amd.face_matcher import FaceMatcher
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    from facerecognitionpipeline_amd.pipeline import MatchBatcher
+
+    base = W.synthetic_crops(32, seed=W.CROP_SEED_GALLERY)
+    gm = GalleryManager(gallery_path=str(tmp_path / "g.npz"), device="cuda:0", verbose=False)
+    ref = embedder.extract_embeddings_batch(list(base))
+    for i in range(32):
+        gm.add_student(f"S{i}", f"N{i}", ref[i])
+    fm = FaceMatcher(embedder=embedder, gallery=gm)
+    probes = W.probe_crops(base, 48)
+    ks = [1 + i % 5 for i in range(48)]
+    want = [fm.match_single_face(p, top_k=k) for p, k in zip(probes, ks)]
+    embedder.model.set_graph_batch(16)
+    got = [None] * 48
+    try:
+        with MatchBatcher(fm, max_batch=16, max_wait_ms=5) as mb:
+            def worker(t):
+                for i in range(t, 48, 12):
+                    got[i] = mb.match_single_face(probes[i], top_k=ks[i])
+            ts = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join(60)
+            assert sum(mb.batches) == 48
+        for i in range(48):
+            assert [r[0] for r in got[i]] == [r[0] for r in want[i]], i
+            np.testing.assert_allclose([r[2] for r in got[i]], [r[2] for r in want[i]], atol=1e-6)
+    finally:
+        embedder.model.set_graph_batch(0)
