@@ -45,6 +45,8 @@
 // (n = l%32, h) = B[k=h][n], C/D register r = D[8(r/4) + 4h + r%4][n].  MFMA j (0..7) of a
 // K-step multiplies channel 8h + j: lane (m, h) reads V[xi][m][8h .. 8h+7] with two
 // ds_read_b128 and the matching 8 U values with two 16-B loads.
+#include <algorithm>
+
 #include "frhip_kernels.h"
 
 
@@ -138,17 +140,24 @@ __device__ __forceinline__ void at6(const float (&m)[6], float (&o)[4]) {
 // (the lo*lo term, ~2^-16 relative, is dropped): 3 MFMAs of 32 cycles per transform element
 // and K-step instead of 8 of 64.  V in LDS: per xi plane hi [32 tiles][16 ch] bf16 then the lo
 // planes; 32-B rows, 16-B slot XOR (m >> 3) & 1.
-template <bool CORR, int EPI, bool BF>
+template <bool CORR, int EPI, bool BF, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int t = wino4_xcd_remap(blockIdx.x, p.mblocks * p.nblocks);
+  // SPLIT (small grids): workgroup (t, split) runs K-steps [s0, s0 + KS) of item t and writes
+  // its raw partial output to slab `split`; wino4_split_reduce_kernel finishes the layer
+  const int nT = p.mblocks * p.nblocks;
+  const int tt = wino4_xcd_remap(blockIdx.x, SPLIT ? nT * p.ksplit : nT);
+  const int split = SPLIT ? tt / nT : 0;
+  const int t = SPLIT ? tt - split * nT : tt;
   const int mb = t % p.mblocks, nb = t / p.mblocks;
   const int H = p.H, W = p.W, Cin = p.Cin;
-  const int KS = Cin / KC;
+  const int KST = Cin / KC;  // K-steps of the whole reduction (filter layout stride)
+  const int s0 = SPLIT ? split * p.ks_per : 0;
+  const int KS = SPLIT ? min(p.ks_per, KST - s0) : KST;  // K-steps this workgroup runs
   const int NB32 = p.Cout / 32;
   const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
   const bool mfma_wave = wid < 4;  // waves 0-3 MFMA, 4-7 transform (one of each per SIMD)
@@ -189,7 +198,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #ifdef W4_NO_PATCH
       if (s > 1) return;
 #endif
-      const int so = min(s, KS - 1) * KC * 4;
+      const int so = (s0 + min(s, KS - 1)) * KC * 4;
 #pragma unroll
       for (int i = 0; i < 6; ++i)
 #pragma unroll
@@ -266,13 +275,13 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     };
     int ubase[XPW];
 #pragma unroll
-    for (int x = 0; x < XPW; ++x) ubase[x] = ((((XPW * wid + x) * NB32 + nb) * KS) * 2 * 64 + lane) * 16;
+    for (int x = 0; x < XPW; ++x) ubase[x] = ((((XPW * wid + x) * NB32 + nb) * KST) * 2 * 64 + lane) * 16;
     float4 u[XPW][2];
     auto load_u = [&](int x, int s) {
 #ifdef W4_NO_ULOAD
       if (s > 0) return;
 #endif
-      const int so = min(s, KS - 1) * 2 * 64 * 16;
+      const int so = (s0 + min(s, KS - 1)) * 2 * 64 * 16;
       u[x][0] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x], so, 0));
       u[x][1] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x] + 64 * 16, so, 0));
     };
@@ -354,10 +363,10 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   int opix[2][4][4];
   int ocls[2][4][4];
   float rv[2][4][4];
-  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc4(p.y, p.B * H * W * p.Cout * 4);
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc4(SPLIT ? p.part + split * p.part_stride : p.y, p.B * H * W * p.Cout * 4);
   const __amdgpu_buffer_rsrc_t cr = uniform_rsrc4(p.corr, CORR ? 16 * p.Cout * 4 : 0);
-  const __amdgpu_buffer_rsrc_t rr = uniform_rsrc4(p.res, (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
-                                                             ? p.B * H * W * p.Cout * 4 : 0);
+  constexpr bool RES = !SPLIT && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
+  const __amdgpu_buffer_rsrc_t rr = uniform_rsrc4(p.res, RES ? p.B * H * W * p.Cout * 4 : 0);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int T = mb * WT + (tid >> 5) + 16 * q;
@@ -385,7 +394,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         ocls[q][r][c] = rcls[r] * 4 + ccls[c];
         rv[q][r][c] = 0.f;
 #ifndef W4_EPI_NORES
-        if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
+        if constexpr (RES)
           rv[q][r][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, opix[q][r][c], 0, 0));
 #endif
       }
@@ -403,9 +412,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     }
   }
   __syncthreads();
-  const float sc = p.post_scale[cout], sh = p.post_shift[cout];
+  const float sc = SPLIT ? 1.f : p.post_scale[cout], sh = SPLIT ? 0.f : p.post_shift[cout];
   float al = 0.f;
-  if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) al = p.prelu[cout];
+  if constexpr (!SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU)) al = p.prelu[cout];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int tile = (tid >> 5) + 16 * q;
@@ -427,14 +436,18 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       for (int r = 0; r < 4; ++r) {
         const int oo = opix[q][r][c];
         float v = o[r];
-        if constexpr (CORR)
-          v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(cr, (ocls[q][r][c] * p.Cout + cout) * 4, 0, 0));
-        v = v * sc + sh;
-        if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
-        if constexpr (EPI == EPI_AFFINE_RES) v += rv[q][r][c];
-        if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
-          v += rv[q][r][c];
-          v = v > 0.f ? v : v * al;
+        if constexpr (CORR) {  // the correction is linear: split 0 carries it
+          if (!SPLIT || split == 0)
+            v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(cr, (ocls[q][r][c] * p.Cout + cout) * 4, 0, 0));
+        }
+        if constexpr (!SPLIT) {
+          v = v * sc + sh;
+          if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
+          if constexpr (EPI == EPI_AFFINE_RES) v += rv[q][r][c];
+          if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
+            v += rv[q][r][c];
+            v = v > 0.f ? v : v * al;
+          }
         }
 #ifdef W4_EPI_NOSTORE
         if (v == 12345.f)
@@ -444,6 +457,44 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       }
     }
   }
+}
+
+// Split-K finish: y = epilogue(sum over splits of the raw partial outputs), summed in split
+// order (deterministic).  Pixels outside the images were never stored by any split, and
+// none of them is read here (n covers exactly the B*H*W*Cout outputs).
+template <int EPI>
+__global__ void wino4_split_reduce_kernel(const float* __restrict__ part, int S, long long stride, long long n4,
+                                          int Cout, const float* __restrict__ sc, const float* __restrict__ sh,
+                                          const float* __restrict__ prelu, const float* __restrict__ res,
+                                          float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 v = reinterpret_cast<const float4*>(part)[i];
+  for (int s = 1; s < S; ++s) {
+    const float4 w = reinterpret_cast<const float4*>(part + s * stride)[i];
+    v.x += w.x;
+    v.y += w.y;
+    v.z += w.z;
+    v.w += w.w;
+  }
+  const int c0 = (int)((i * 4) % Cout);
+  float o[4] = {v.x, v.y, v.z, v.w};
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) r = reinterpret_cast<const float4*>(res)[i];
+  const float rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = c0 + j;
+    float t = o[j] * sc[c] + sh[c];
+    if constexpr (EPI == EPI_AFFINE_PRELU) t = t > 0.f ? t : t * prelu[c];
+    if constexpr (EPI == EPI_AFFINE_RES) t += rr[j];
+    if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
+      t += rr[j];
+      t = t > 0.f ? t : t * prelu[c];
+    }
+    o[j] = t;
+  }
+  reinterpret_cast<float4*>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // Pre-activation BatchNorm folded out of the transform (conv1 of every block):
@@ -587,14 +638,40 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s,
   wino4_canvas(p);
   p.mblocks = (p.ntiles + WT - 1) / WT;
   p.nblocks = p.Cout / 32;
-  const dim3 grid(p.mblocks * p.nblocks), block(512);
-#define FR_WINO4_CASE(PRE_, EPI_)                                                 \
-  if (pre == PRE_ && epi == EPI_) {                                               \
-    if (bf)                                                                       \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, true>), grid, block, 0, s, p);  \
-    else                                                                          \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, false>), grid, block, 0, s, p); \
-    return hipGetLastError();                                                     \
+  // split-K when the grid leaves most CUs idle (small batches): as many splits as fill ~256
+  // workgroups, bounded by the K-steps and by the partial-output workspace
+  const int KST = p.Cin / KC;
+  const long long elems = (long long)p.B * p.H * p.W * p.Cout;
+  int S = 1;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(p.y) | reinterpret_cast<uintptr_t>(p.res) |
+                         reinterpret_cast<uintptr_t>(p.part)) & 15) == 0;
+  if (!bf && p.part && aligned && p.mblocks * p.nblocks < 128 && KST > 1) {
+    S = std::min(KST, (256 + p.mblocks * p.nblocks - 1) / (p.mblocks * p.nblocks));
+    S = (int)std::min<long long>(S, p.part_floats / elems);
+    if (S > 1) {
+      p.ks_per = (KST + S - 1) / S;
+      S = (KST + p.ks_per - 1) / p.ks_per;
+    }
+  }
+  p.ksplit = S > 1 ? S : 1;
+  p.part_stride = elems;
+  const dim3 grid(p.mblocks * p.nblocks * p.ksplit), block(512);
+  const bool split = p.ksplit > 1;
+#define FR_WINO4_CASE(PRE_, EPI_)                                                                      \
+  if (pre == PRE_ && epi == EPI_) {                                                                    \
+    if (bf)                                                                                            \
+      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, true, false>), grid, block, 0, s, p);                \
+    else if (split)                                                                                    \
+      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, false, true>), grid, block, 0, s, p);                \
+    else                                                                                               \
+      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, false, false>), grid, block, 0, s, p);               \
+    if (split) {                                                                                       \
+      const long long n4 = elems / 4;                                                                  \
+      hipLaunchKernelGGL((wino4_split_reduce_kernel<EPI_>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), \
+                         0, s, p.part, p.ksplit, p.part_stride, n4, p.Cout, p.post_scale, p.post_shift,  \
+                         p.prelu, p.res, p.y);                                                          \
+    }                                                                                                  \
+    return hipGetLastError();                                                                          \
   }
   if (pre && !p.corr) return hipErrorInvalidValue;
   FR_WINO4_CASE(true, EPI_AFFINE_PRELU)   // IR conv1: pre-BN, BN, PReLU

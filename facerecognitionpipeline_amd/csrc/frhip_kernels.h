@@ -109,6 +109,12 @@ struct Wino4Params {
   const float* corr;  // [16][Cout] pre-BN shift correction (launch_wino4_weights), with pre-BN only
   int B, H, W, Cin, Cout;
   int Pr, Pc, NC, TWc, ntiles, mblocks, nblocks;  // set by launch_wino4 (wino4_canvas)
+  // split-K workspace (optional): raw partial outputs [ksplit][B*H*W*Cout]; launch_wino4 splits
+  // the K loop over workgroups when the grid is small and part_floats holds the slabs
+  float* part;
+  long long part_floats;
+  int ksplit, ks_per;      // set by launch_wino4
+  long long part_stride;   // set by launch_wino4
 };
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);
 size_t wino4_weight_floats(int Cout, int Cin);

@@ -328,6 +328,8 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.W = W;
     wp.Cin = cw.cin;
     wp.Cout = cw.cout;
+    wp.part = h->w4part;
+    wp.part_floats = h->w4part ? fr_handle::W4PART_FLOATS : 0;
     Wino4Params cv = wp;
     wino4_canvas(cv);
     // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair (bf16x3: 3 bf16 MFMA
@@ -923,6 +925,7 @@ int fr_finalize(fr_handle* h) {
     FR_HIP(h, hipMalloc((void**)&h->partial, (size_t)h->head_split * mb * 512 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->in_stage, mb * 112 * 112 * 3));
     FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
+    FR_HIP(h, hipMalloc((void**)&h->w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
   }
   if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
@@ -1417,6 +1420,12 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
   return FR_OK;
 }
 
+static int g_frt_wino4_split = 1;
+int frt_set_wino4_split(int on) {
+  g_frt_wino4_split = on != 0;
+  return FR_OK;
+}
+
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                         const float* pre_scale, const float* pre_shift, const float* post_scale,
                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream) {
@@ -1429,6 +1438,7 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
   if (hipMalloc((void**)&u, (wino4_weight_floats(cout, cin) + 16 * (size_t)cout) * sizeof(float)) != hipSuccess)
     return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4: allocation failed");
   float* corr = pre_scale ? u + wino4_weight_floats(cout, cin) : nullptr;
+  float* part = nullptr;
   hipError_t e = launch_wino4_weights(w, pre_scale, pre_shift, u, corr, cout, cin, s);
   if (e == hipSuccess) {
     Wino4Params p{};
@@ -1447,10 +1457,16 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.W = W;
     p.Cin = cin;
     p.Cout = cout;
-    e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s);
+    if (g_frt_wino4_split) {  // split-K workspace: small grids take the split path
+      p.part_floats = (long long)B * H * W * cout * std::min(cin / 16, 16);
+      if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;
+      p.part = part;
+    }
+    if (e == hipSuccess) e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s);
   }
   const hipError_t se = hipStreamSynchronize(s);
   (void)hipFree(u);
+  (void)hipFree(part);
   if (e == hipSuccess) e = se;
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd4: ") + hipGetErrorString(e));
   return FR_OK;

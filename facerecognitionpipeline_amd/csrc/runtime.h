@@ -115,6 +115,8 @@ struct fr_handle {
   float* wino_arena = nullptr;   // F(2x2) filters, built when that algorithm is selected
   float* wino4_arena = nullptr;  // F(4x4) filters (+ pre-BN corrections), likewise
   void* wino4_bf_arena = nullptr;  // their bf16 hi/lo split, built when bf16x3 is selected
+  float* w4part = nullptr;         // F(4x4) split-K partial outputs (small batches), W4PART_FLOATS
+  static constexpr long long W4PART_FLOATS = 16ll << 20;
 
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
   frhip_rt::Detector* det = nullptr;
@@ -149,6 +151,7 @@ struct fr_handle {
     (void)hipFree(wino_arena);
     (void)hipFree(wino4_arena);
     (void)hipFree(wino4_bf_arena);
+    (void)hipFree(w4part);
     for (auto p : act) (void)hipFree(p);
     (void)hipFree(sc_buf);
     (void)hipFree(partial);

@@ -40,6 +40,9 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 int frt_conv2d_winograd4_bf(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                             const float* pre_scale, const float* pre_shift, const float* post_scale,
                             const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
+/* frt_conv2d_winograd4 gives launch_wino4 a split-K workspace (small grids then split the K
+ * loop over workgroups + a reduce pass) unless frt_set_wino4_split(0). */
+int frt_set_wino4_split(int on);
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                          const float* pre_scale, const float* pre_shift, const float* post_scale,
                          const float* post_shift, const float* prelu, const float* res, int epi, void* stream);

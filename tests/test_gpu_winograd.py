@@ -77,6 +77,34 @@ def test_winograd4_multi_round(B, H, cin, cout):
     _close(got, ref, rel=REL[4])
 
 
+@pytest.mark.parametrize("B,H,cin,cout", [
+    (1, 14, 256, 256),   # 8 workgroups -> 16 splits of 1 K-step
+    (1, 7, 512, 512),    # 16 workgroups -> 16 splits of 2 K-steps
+    (3, 28, 128, 128),   # 20 workgroups -> 8 splits
+    (1, 112, 64, 64),    # 50 workgroups -> 4 splits of 1 K-step
+    (2, 15, 32, 64),     # Cin = 32: 2 K-steps -> 2 splits
+    (7, 14, 224, 512),   # 64 workgroups -> 4 splits of 4, 4, 4, 2 K-steps
+])
+@pytest.mark.parametrize("epi", [1, 2])
+def test_winograd4_split_k_small_grids(B, H, cin, cout, epi):
+    """Small grids split the F(4x4) K loop over workgroups (raw partial outputs, one split
+    carrying the pre-BN correction) and finish in wino4_split_reduce_kernel; both paths
+    match the CPU conv, and each other to the same bar."""
+    L = _frt.lib()
+    outs = {}
+    try:
+        for split in (1, 0):
+            L.frt_set_wino4_split(split)
+            got, ref = _wino_case(B, H, cin, cout, epi, seed=700 + H + cin + epi, m=4)
+            _close(got, ref, rel=REL[4])
+            outs[split] = got
+    finally:
+        L.frt_set_wino4_split(1)
+    _close(outs[1], outs[0], rel=REL[4])
+    again, _ = _wino_case(B, H, cin, cout, epi, seed=700 + H + cin + epi, m=4)
+    assert torch.equal(again, outs[1]), "split-K result is not run-to-run deterministic"
+
+
 @pytest.mark.parametrize("B,H,cin,cout", [(2, 14, 64, 64), (4, 7, 512, 512), (1, 28, 256, 256), (3, 15, 32, 64)])
 @pytest.mark.parametrize("epi", [1, 2])
 def test_winograd4_bf16x3(B, H, cin, cout, epi):
