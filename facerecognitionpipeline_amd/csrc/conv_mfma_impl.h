@@ -506,8 +506,10 @@ static hipError_t launch_tile(const ConvParams& p0, bool pre, Epi epi, int nspli
     }
     const long long ntile = (long long)p.mtiles * p.ntiles;
     const long long P0 = (long long)p.sk_cus * o;
-    // never more blocks than K-steps in the stream-K region (every range non-empty)
-    p.sk_blocks = (int)min(P0, ntile * p.steps_total);
+    // at least ~8 K-steps per block: a tile's last arriver sums one slab per contributor, so
+    // cutting a small grid (batch 1: 2-4 tiles) over every CU would make that fixup the
+    // critical path; large grids are unaffected (ntile * steps / 8 >> CUs)
+    p.sk_blocks = (int)min(P0, ntile * max(1, p.steps_total / 8));
   }
   dim3 grid(p.sk_blocks > 0 ? p.sk_blocks : p.mtiles * p.ntiles, p.sk_blocks > 0 ? 1 : nsplit), block(NTHREADS);
   if (p.sk_blocks > 0) {

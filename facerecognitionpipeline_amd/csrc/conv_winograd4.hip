@@ -469,13 +469,26 @@ __global__ void wino4_split_reduce_kernel(const float* __restrict__ part, int S,
                                           float* __restrict__ y) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  float4 v = reinterpret_cast<const float4*>(part)[i];
-  for (int s = 1; s < S; ++s) {
-    const float4 w = reinterpret_cast<const float4*>(part + s * stride)[i];
-    v.x += w.x;
-    v.y += w.y;
-    v.z += w.z;
-    v.w += w.w;
+  // all slab loads in flight at once (S <= 16 in practice), then summed in split order
+  float4 w[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+    if (s < S) w[s] = reinterpret_cast<const float4*>(part + s * stride)[i];
+  float4 v = w[0];
+#pragma unroll
+  for (int s = 1; s < 16; ++s)
+    if (s < S) {
+      v.x += w[s].x;
+      v.y += w[s].y;
+      v.z += w[s].z;
+      v.w += w[s].w;
+    }
+  for (int s = 16; s < S; ++s) {
+    const float4 u = reinterpret_cast<const float4*>(part + s * stride)[i];
+    v.x += u.x;
+    v.y += u.y;
+    v.z += u.z;
+    v.w += u.w;
   }
   const int c0 = (int)((i * 4) % Cout);
   float o[4] = {v.x, v.y, v.z, v.w};
