@@ -46,6 +46,7 @@
 // K-step multiplies channel 8h + j: lane (m, h) reads V[xi][m][8h .. 8h+7] with two
 // ds_read_b128 and the matching 8 U values with two 16-B loads.
 #include <algorithm>
+#include <cstdlib>
 
 #include "frhip_kernels.h"
 
@@ -651,16 +652,22 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s,
   wino4_canvas(p);
   p.mblocks = (p.ntiles + WT - 1) / WT;
   p.nblocks = p.Cout / 32;
-  // split-K when the grid leaves most CUs idle (small batches): as many splits as fill ~256
-  // workgroups, bounded by the K-steps and by the partial-output workspace
+  // split-K when the grid leaves most CUs idle (small batches): as many splits as fit one
+  // round of 256 workgroups, bounded by the K-steps and by the partial-output workspace
   const int KST = p.Cin / KC;
   const long long elems = (long long)p.B * p.H * p.W * p.Cout;
   int S = 1;
   const bool aligned = ((reinterpret_cast<uintptr_t>(p.y) | reinterpret_cast<uintptr_t>(p.res) |
                          reinterpret_cast<uintptr_t>(p.part)) & 15) == 0;
-  if (!bf && p.part && aligned && p.mblocks * p.nblocks < 128 && KST > 1) {
-    S = std::min(KST, (256 + p.mblocks * p.nblocks - 1) / (p.mblocks * p.nblocks));
-    S = (int)std::min<long long>(S, p.part_floats / elems);
+  // grids of up to 128 workgroups split (>= 2 splits fit one round); FRHIP_W4_SPLIT_WG overrides
+  // that bound for experiments (tools/serve_latency.py sweeps: 96 / 256 / 512 were slower)
+  static const int split_max = [] {
+    const char* e = getenv("FRHIP_W4_SPLIT_WG");
+    return e ? atoi(e) : 128;
+  }();
+  if (!bf && p.part && aligned && p.mblocks * p.nblocks <= split_max && KST > 1) {
+    S = std::min(KST, 256 / (p.mblocks * p.nblocks));  // all splits in one round of 256 CUs
+    S = (int)std::min<long long>(S, std::min<long long>(p.part_floats, (1ll << 29) - 1) / elems);
     if (S > 1) {
       p.ks_per = (KST + S - 1) / S;
       S = (KST + p.ks_per - 1) / p.ks_per;

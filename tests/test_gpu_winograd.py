@@ -88,16 +88,16 @@ def test_winograd4_multi_round(B, H, cin, cout):
 @pytest.mark.parametrize("epi", [1, 2])
 def test_winograd4_split_k_small_grids(B, H, cin, cout, epi):
     """Small grids split the F(4x4) K loop over workgroups (raw partial outputs, one split
-    carrying the pre-BN correction) and finish in wino4_split_reduce_kernel; both paths
-    match the CPU conv, and each other to the same bar."""
+    carrying the pre-BN correction); wino4_split_reduce_kernel sums the slabs in split order
+    and applies the epilogue.  Both paths match the CPU conv, and each other to the same bar."""
     L = _frt.lib()
     outs = {}
     try:
-        for split in (1, 0):
-            L.frt_set_wino4_split(split)
+        for mode in (1, 0):  # split K loop + reduce pass, no split
+            L.frt_set_wino4_split(mode)
             got, ref = _wino_case(B, H, cin, cout, epi, seed=700 + H + cin + epi, m=4)
             _close(got, ref, rel=REL[4])
-            outs[split] = got
+            outs[mode] = got
     finally:
         L.frt_set_wino4_split(1)
     _close(outs[1], outs[0], rel=REL[4])
