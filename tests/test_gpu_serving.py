@@ -115,3 +115,20 @@ def test_match_batcher_equals_match_single_face(embedder, tmp_path):
             np.testing.assert_allclose([r[2] for r in got[i]], [r[2] for r in want[i]], atol=1e-6)
     finally:
         embedder.model.set_graph_batch(0)
+
+
+def test_small_batches_match_oracle(embedder):
+    """Serving batch sizes take the split-K F(4x4) path and small stream-K grids: every
+    embedding stays within the pipeline's 1e-5 bar of the CPU oracle."""
+    import os
+
+    from oracle import reference_path as rp
+    from oracle.adaface_net import load_oracle
+
+    crops = W.synthetic_crops(5, seed=4242)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref = rp.extract_embeddings_batch(load_oracle("ir_101", W.synthetic_state_dict("ir_101")), list(crops))
+    dev = torch.from_numpy(crops).cuda()
+    for n in (1, 2, 5):
+        got = embedder.embed_tensor(dev[:n].contiguous()).cpu().numpy()
+        assert np.abs(got - ref[:n]).max() <= 1e-5, n
