@@ -154,7 +154,11 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   const int tt = wino4_xcd_remap(blockIdx.x, SPLIT ? nT * p.ksplit : nT);
   const int split = SPLIT ? tt / nT : 0;
   const int t = SPLIT ? tt - split * nT : tt;
-  const int mb = t % p.mblocks, nb = t / p.mblocks;
+  // item t -> (tile block mb, cout block nb): consecutive items (one XCD's contiguous run)
+  // cycle through p.nbg cout blocks of a tile block before moving on, so those workgroups
+  // share the tile block's input in the XCD's L2 (nbg = 1: one cout block per run)
+  const int gsz = p.mblocks * p.nbg, g = t / gsz, rem = t - g * gsz;
+  const int mb = rem / p.nbg, nb = g * p.nbg + (rem - (rem / p.nbg) * p.nbg);
   const int H = p.H, W = p.W, Cin = p.Cin;
   const int KST = Cin / KC;  // K-steps of the whole reduction (filter layout stride)
   const int s0 = SPLIT ? split * p.ks_per : 0;
@@ -652,6 +656,14 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s,
   wino4_canvas(p);
   p.mblocks = (p.ntiles + WT - 1) / WT;
   p.nblocks = p.Cout / 32;
+  // 4 cout blocks per tile block (C3: 9,515 -> 9,707 faces/s; 2: 9,673, 8: 9,704);
+  // FRHIP_W4_NBG overrides for experiments
+  static const int nbg_env = [] {
+    const char* e = getenv("FRHIP_W4_NBG");
+    return e ? atoi(e) : 4;
+  }();
+  p.nbg = 1;
+  while (p.nbg * 2 <= nbg_env && p.nblocks % (p.nbg * 2) == 0) p.nbg *= 2;
   // split-K when the grid leaves most CUs idle (small batches): as many splits as fit one
   // round of 256 workgroups, bounded by the K-steps and by the partial-output workspace
   const int KST = p.Cin / KC;

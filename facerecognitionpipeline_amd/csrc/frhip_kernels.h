@@ -109,6 +109,7 @@ struct Wino4Params {
   const float* corr;  // [16][Cout] pre-BN shift correction (launch_wino4_weights), with pre-BN only
   int B, H, W, Cin, Cout;
   int Pr, Pc, NC, TWc, ntiles, mblocks, nblocks;  // set by launch_wino4 (wino4_canvas)
+  int nbg;  // cout blocks interleaved per tile block in the item order (set by launch_wino4)
   // split-K workspace (optional): raw partial outputs [ksplit][B*H*W*Cout]; launch_wino4 splits
   // the K loop over workgroups when the grid is small and part_floats holds the slabs
   float* part;
