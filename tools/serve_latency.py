@@ -42,8 +42,9 @@ def main():
     ap.add_argument("--gallery", type=int, default=1000)
     ap.add_argument("--algos", default="", help="only sweep these conv algorithms (comma list) x --ns")
     ap.add_argument("--ns", default="1,4,16,64")
+    ap.add_argument("--graph", type=int, default=0, help="--algos: fr_set_graph_batch value")
     args = ap.parse_args()
-    emb = FaceEmbedder(architecture="ir_101", model_path="synthetic", max_batch=64, graph_batch=0)
+    emb = FaceEmbedder(architecture="ir_101", model_path="synthetic", max_batch=256, graph_batch=0)
     G = args.gallery
     base = W.synthetic_crops(G, seed=W.CROP_SEED_GALLERY)
     E = emb.extract_embeddings_batch(list(base))
@@ -58,11 +59,22 @@ def main():
     if args.algos:
         for algo in args.algos.split(","):
             h.set_conv_algorithm(algo)
+            h.set_graph_batch(args.graph)
             for n in [int(x) for x in args.ns.split(",")]:
                 rgb = torch.from_numpy(probes[:n]).to(dev)
                 o = torch.empty((n, 512), dtype=torch.float32, device=dev)
                 ms = timed(lambda: h.embed(rgb, o, True), 20)
-                print(f"{algo:10s} n={n:3d} embed {ms:.3f} ms", flush=True)
+                hh = gm._sync_device()
+                idx = torch.empty((n, 5), dtype=torch.int32, device=dev)
+                sc = torch.empty((n, 5), dtype=torch.float32, device=dev)
+                ms2 = timed(lambda: hh.embed_match(rgb, 5, idx, sc), 20)
+                h.profile_enable(True)
+                h.profile_read()
+                ms3 = timed(lambda: hh.embed_match(rgb, 5, idx, sc), 20)
+                h.profile_read()
+                h.profile_enable(False)
+                print(f"{algo:10s} n={n:3d} embed {ms:.3f} ms, embed+match {ms2:.3f} ms, "
+                      f"with HIP-event profiling {ms3:.3f} ms", flush=True)
         return
     out = {"arch": "ir_101", "gallery": G, "top_k": k, "embed_match_ms": {}}
     for n in (1, 2, 4, 8, 16, 32):
