@@ -18,14 +18,16 @@
 namespace frhip {
 
 // One thread per output pixel (all channels); blockIdx.y = face.
+// Maps come from device memory (minv) or, for up to WARP_MAPS_BY_VALUE faces, by value in the
+// kernel arguments (no H2D copy, so the caller needs no stream sync to keep a host buffer alive).
 __global__ __launch_bounds__(256) void warp_affine_kernel(const uint8_t* __restrict__ frame, int H, int W,
-                                                          const double* __restrict__ minv, int S,
-                                                          uint8_t* __restrict__ out) {
+                                                          const double* __restrict__ minv, WarpMaps maps,
+                                                          int S, uint8_t* __restrict__ out) {
   const int face = blockIdx.y;
   const int pix = blockIdx.x * 256 + threadIdx.x;
   if (pix >= S * S) return;
   const int oy = pix / S, ox = pix - oy * S;
-  const double* m = minv + face * 6;
+  const double* m = minv ? minv + face * 6 : maps.m[face];
   const long long X0 = (long long)__builtin_rint((m[1] * oy + m[2]) * 1024.0) + 16;
   const long long Y0 = (long long)__builtin_rint((m[4] * oy + m[5]) * 1024.0) + 16;
   const long long adx = (long long)__builtin_rint(m[0] * ox * 1024.0);
@@ -52,7 +54,20 @@ __global__ __launch_bounds__(256) void warp_affine_kernel(const uint8_t* __restr
 hipError_t launch_warp_affine(const uint8_t* frame, int H, int W, const double* minv, int n, int S, uint8_t* out,
                               hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(warp_affine_kernel, dim3((S * S + 255) / 256, n), dim3(256), 0, s, frame, H, W, minv, S, out);
+  hipLaunchKernelGGL(warp_affine_kernel, dim3((S * S + 255) / 256, n), dim3(256), 0, s, frame, H, W, minv,
+                     WarpMaps{}, S, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_warp_affine_by_value(const uint8_t* frame, int H, int W, const double* host_minv, int n, int S,
+                                       uint8_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n > WARP_MAPS_BY_VALUE) return hipErrorInvalidValue;
+  WarpMaps maps{};
+  for (int f = 0; f < n; ++f)
+    for (int j = 0; j < 6; ++j) maps.m[f][j] = host_minv[f * 6 + j];
+  hipLaunchKernelGGL(warp_affine_kernel, dim3((S * S + 255) / 256, n), dim3(256), 0, s, frame, H, W,
+                     (const double*)nullptr, maps, S, out);
   return hipGetLastError();
 }
 

@@ -149,6 +149,14 @@ hipError_t launch_topk(const float* scores, int n, int G, int k, int32_t* idx, f
 // minv: device [n][6] inverse maps (double), out: [n][S][S][3].
 hipError_t launch_warp_affine(const uint8_t* frame, int H, int W, const double* minv, int n, int S, uint8_t* out,
                               hipStream_t s);
+// The same with up to WARP_MAPS_BY_VALUE host maps passed by value in the kernel arguments
+// (2.3 KB of the 4 KB limit): nothing to copy, so nothing for the caller to wait on.
+constexpr int WARP_MAPS_BY_VALUE = 48;
+struct WarpMaps {
+  double m[WARP_MAPS_BY_VALUE][6];
+};
+hipError_t launch_warp_affine_by_value(const uint8_t* frame, int H, int W, const double* host_minv, int n, int S,
+                                       uint8_t* out, hipStream_t s);
 
 // Laplacian variance of the gray image of n uint8 RGB crops [n][S][S][3] -> var[n] (double).
 hipError_t launch_blur(const uint8_t* crops, int n, int S, double* var, hipStream_t s);

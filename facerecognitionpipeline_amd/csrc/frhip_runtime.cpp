@@ -1176,9 +1176,14 @@ int fr_align_faces(fr_handle* h, const uint8_t* frame, int height, int width, co
     if (tforms) memcpy(tforms + (size_t)f * 6, Mf, sizeof(Mf));
     invert_affine(Mf, &minv[(size_t)f * 6]);
   }
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= WARP_MAPS_BY_VALUE) {  // maps in the kernel arguments: no copy, no sync
+    const hipError_t e = launch_warp_affine_by_value(frame, height, width, minv.data(), n, out_size, out, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("warp launch: ") + hipGetErrorString(e));
+    return FR_OK;
+  }
   int rc = ensure_buf(h, &h->align_m, &h->align_m_cap, minv.size() * sizeof(double));
   if (rc) return rc;
-  hipStream_t s = (hipStream_t)stream;
   FR_HIP(h, hipMemcpyAsync(h->align_m, minv.data(), minv.size() * sizeof(double), hipMemcpyHostToDevice, s));
   hipError_t e = launch_warp_affine(frame, height, width, (const double*)h->align_m, n, out_size, out, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("warp launch: ") + hipGetErrorString(e));
@@ -1198,9 +1203,14 @@ int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, co
   DeviceGuard dg(h->device);
   std::vector<double> minv((size_t)n * 6);
   for (int f = 0; f < n; ++f) invert_affine(tforms + (size_t)f * 6, &minv[(size_t)f * 6]);
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= WARP_MAPS_BY_VALUE) {  // maps in the kernel arguments: no copy, no sync
+    const hipError_t e = launch_warp_affine_by_value(frame, height, width, minv.data(), n, out_size, out, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("warp launch: ") + hipGetErrorString(e));
+    return FR_OK;
+  }
   int rc = ensure_buf(h, &h->align_m, &h->align_m_cap, minv.size() * sizeof(double));
   if (rc) return rc;
-  hipStream_t s = (hipStream_t)stream;
   FR_HIP(h, hipMemcpyAsync(h->align_m, minv.data(), minv.size() * sizeof(double), hipMemcpyHostToDevice, s));
   hipError_t e = launch_warp_affine(frame, height, width, (const double*)h->align_m, n, out_size, out, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("warp launch: ") + hipGetErrorString(e));
