@@ -423,6 +423,8 @@ int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int norma
 }
 
 void clear_graphs(fr_handle* h) {
+  if (h->graphs.empty()) return;
+  (void)hipDeviceSynchronize();  // no replay of these graphs may still be in flight
   for (auto& g : h->graphs) (void)hipGraphExecDestroy(g.exec);
   h->graphs.clear();
 }
@@ -1255,6 +1257,7 @@ int fr_set_precision(fr_handle* h, int mode) {
   if (mode != FR_PRECISION_F32 && mode != FR_PRECISION_BF16X3)
     return fail(h, FR_ERR_INVALID_ARGUMENT, "precision must be FR_PRECISION_F32 or FR_PRECISION_BF16X3");
   h->prec = mode == FR_PRECISION_BF16X3 ? PREC_BF16X3 : PREC_F32;
+  DeviceGuard dg(h->device);
   clear_graphs(h);
   if (h->finalized) return ensure_winograd(h);
   return FR_OK;
@@ -1267,6 +1270,7 @@ int fr_set_conv_algorithm(fr_handle* h, int algo) {
     return fail(h, FR_ERR_INVALID_ARGUMENT, "algorithm must be FR_CONV_DIRECT, FR_CONV_WINOGRAD or FR_CONV_WINOGRAD4");
   h->winograd = algo != FR_CONV_DIRECT;
   h->wino_m = algo == FR_CONV_WINOGRAD ? 2 : 4;
+  DeviceGuard dg(h->device);
   clear_graphs(h);
   if (h->finalized) return ensure_winograd(h);
   return FR_OK;
