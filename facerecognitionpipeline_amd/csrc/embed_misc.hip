@@ -18,10 +18,13 @@ namespace frhip {
 constexpr int IMG = 112;
 constexpr int STEM_C = 64;
 
-// One block per (image, output row).  LDS: three LUT-normalised input rows with
-// a zero halo ([3][IMG+2][3] floats) and the [27][64] weights.  Thread t owns 4
-// output channels (t&15) of pixels (t>>4) + 16j: a wave writes 4 pixels x 256 B
-// contiguous, and the weight float4 reads of a wave cover all 64 banks once.
+// One block per (image, STEM_ROWS output rows).  LDS: STEM_ROWS+2 LUT-normalised input rows
+// with a zero halo ([STEM_ROWS+2][IMG+2][3] floats) and the [27][64] weights.  Thread t owns 4
+// output channels (t&15) of pixels (t>>4) + 16j of every row; its 27x4 weights live in
+// registers for the whole block.  A wave writes 4 pixels x 256 B contiguous.  Per output the
+// 27 FMAs run in (ky, kx, c) order, as before the row blocking.
+constexpr int STEM_ROWS = 4;
+static_assert(IMG % STEM_ROWS == 0, "rows per block must divide the image height");
 __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, const float* __restrict__ lut,
                                                    const float* __restrict__ w27x64,
                                                    const float* __restrict__ bn_scale,
@@ -29,60 +32,67 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
                                                    const float* __restrict__ prelu, float* __restrict__ y) {
   __shared__ float s_lut[256];
   __shared__ __attribute__((aligned(16))) float s_w[27 * STEM_C];
-  __shared__ float s_in[3][IMG + 2][3];
-  const int b = blockIdx.x / IMG;
-  const int oy = blockIdx.x - b * IMG;
+  __shared__ float s_in[STEM_ROWS + 2][IMG + 2][3];
+  constexpr int RB = IMG / STEM_ROWS;  // row blocks per image
+  const int b = blockIdx.x / RB;
+  const int oy0 = (blockIdx.x - b * RB) * STEM_ROWS;
   const int tid = threadIdx.x;
   s_lut[tid] = lut[tid];
   for (int i = tid; i < 27 * STEM_C; i += 256) s_w[i] = w27x64[i];
   __syncthreads();
-  for (int i = tid; i < 3 * (IMG + 2) * 3; i += 256) {
+  for (int i = tid; i < (STEM_ROWS + 2) * (IMG + 2) * 3; i += 256) {
     const int r = i / ((IMG + 2) * 3);
     const int rem = i - r * (IMG + 2) * 3;
     const int xx = rem / 3;
     const int c = rem - xx * 3;
-    const int iy = oy + r - 1, ix = xx - 1;
+    const int iy = oy0 + r - 1, ix = xx - 1;
     float v = 0.f;
     if ((unsigned)iy < IMG && (unsigned)ix < IMG) v = s_lut[img[(((long long)b * IMG + iy) * IMG + ix) * 3 + c]];
     s_in[r][xx][c] = v;
   }
   __syncthreads();
   const int cg = tid & 15;
+  float4 w[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) w[t] = *reinterpret_cast<const float4*>(s_w + t * STEM_C + 4 * cg);
   const float4 sc = *reinterpret_cast<const float4*>(bn_scale + 4 * cg);
   const float4 sh = *reinterpret_cast<const float4*>(bn_shift + 4 * cg);
   const float4 al = *reinterpret_cast<const float4*>(prelu + 4 * cg);
-  for (int px = tid >> 4; px < IMG; px += 16) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < STEM_ROWS; ++r) {
+    for (int px = tid >> 4; px < IMG; px += 16) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+      for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx)
+        for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const float v = s_in[ky][px + kx][c];
-          const float4 w = *reinterpret_cast<const float4*>(s_w + ((ky * 3 + kx) * 3 + c) * STEM_C + 4 * cg);
-          acc.x = fmaf(v, w.x, acc.x);
-          acc.y = fmaf(v, w.y, acc.y);
-          acc.z = fmaf(v, w.z, acc.z);
-          acc.w = fmaf(v, w.w, acc.w);
-        }
-    float4 o;
-    o.x = acc.x * sc.x + sh.x;
-    o.y = acc.y * sc.y + sh.y;
-    o.z = acc.z * sc.z + sh.z;
-    o.w = acc.w * sc.w + sh.w;
-    o.x = o.x > 0.f ? o.x : o.x * al.x;
-    o.y = o.y > 0.f ? o.y : o.y * al.y;
-    o.z = o.z > 0.f ? o.z : o.z * al.z;
-    o.w = o.w > 0.f ? o.w : o.w * al.w;
-    *reinterpret_cast<float4*>(y + (((long long)b * IMG + oy) * IMG + px) * STEM_C + 4 * cg) = o;
+          for (int c = 0; c < 3; ++c) {
+            const float v = s_in[r + ky][px + kx][c];
+            const float4 wt = w[(ky * 3 + kx) * 3 + c];
+            acc.x = fmaf(v, wt.x, acc.x);
+            acc.y = fmaf(v, wt.y, acc.y);
+            acc.z = fmaf(v, wt.z, acc.z);
+            acc.w = fmaf(v, wt.w, acc.w);
+          }
+      float4 o;
+      o.x = acc.x * sc.x + sh.x;
+      o.y = acc.y * sc.y + sh.y;
+      o.z = acc.z * sc.z + sh.z;
+      o.w = acc.w * sc.w + sh.w;
+      o.x = o.x > 0.f ? o.x : o.x * al.x;
+      o.y = o.y > 0.f ? o.y : o.y * al.y;
+      o.z = o.z > 0.f ? o.z : o.z * al.z;
+      o.w = o.w > 0.f ? o.w : o.w * al.w;
+      *reinterpret_cast<float4*>(y + (((long long)b * IMG + oy0 + r) * IMG + px) * STEM_C + 4 * cg) = o;
+    }
   }
 }
 
 hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, const float* bn_scale,
                        const float* bn_shift, const float* prelu, float* y, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(stem_kernel, dim3(B * IMG), dim3(256), 0, s, img, lut, w27x64, bn_scale, bn_shift, prelu, y);
+  hipLaunchKernelGGL(stem_kernel, dim3(B * (IMG / STEM_ROWS)), dim3(256), 0, s, img, lut, w27x64, bn_scale, bn_shift,
+                     prelu, y);
   return hipGetLastError();
 }
 
