@@ -55,12 +55,12 @@ def wino4_tiles(h, B):
 
 def align(rows, L, B):
     """[(layer name, row)] for every B-image forward found in a sorted kernel-trace."""
-    stem_grid = B * 112 * 256
+    stem_grids = (B * 28 * 256, B * 112 * 256)  # 4 rows per workgroup (1 before the row blocking)
     found = []
     i = 0
     while i < len(rows):
         r = rows[i]
-        if "stem_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == stem_grid and i + len(L) <= len(rows):
+        if "stem_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) in stem_grids and i + len(L) <= len(rows):
             seq = rows[i:i + len(L)]
             if "head_reduce" in seq[-1]["Kernel_Name"]:
                 found.append([(n[0], d) for n, d in zip(L, seq)])
