@@ -33,6 +33,7 @@ _SIGNATURES = {
     "fr_finalize": (_I, [_P]),
     "fr_embed": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
     "fr_embed_host": (_I, [_P, _P, _I, _I, _I, _P, _I]),
+    "fr_resize_crops": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "fr_gallery_set": (_I, [_P, _P, _I, _I, _I, _P]),
     "fr_gallery_size": (_I, [_P, ctypes.POINTER(_I)]),
     "fr_gallery_write_rows": (_I, [_P, _I, _I, _P, _I, _P]),
@@ -151,12 +152,24 @@ class Handle:
         check(self._lib.fr_embed(self.h, ptr(rgb), n, rgb.shape[1], rgb.shape[2], ptr(out), int(normalize),
                                  stream_of(self.device)), self.h)
 
+    def resize_crops(self, src: torch.Tensor, out: torch.Tensor) -> None:
+        """cv2.resize(INTER_LINEAR) of uint8 [n,H,W,3] device crops into out [n,112,112,3]."""
+        check(self._lib.fr_resize_crops(self.h, ptr(src), src.shape[0], src.shape[1], src.shape[2], ptr(out),
+                                        stream_of(self.device)), self.h)
+
     # -- gallery -----------------------------------------------------------
     def gallery_set(self, E: torch.Tensor, tag=None) -> None:
         G = E.shape[0] if E.numel() else 0
         D = E.shape[1] if E.dim() == 2 else 512
         check(self._lib.fr_gallery_set(self.h, ptr(E) if G else None, G, D, 1, stream_of(self.device)), self.h)
         self.gallery_tag = tag
+
+    def gallery_replace(self, E: torch.Tensor) -> None:
+        """Replace the rows with a device [G,512] matrix built from the current ones (a delta
+        replay's compaction; the gallery tag is left to the caller)."""
+        E = E.contiguous()
+        G = E.shape[0]
+        check(self._lib.fr_gallery_set(self.h, ptr(E) if G else None, G, 512, 1, stream_of(self.device)), self.h)
 
     def gallery_size(self) -> int:
         g = ctypes.c_int()

@@ -342,11 +342,10 @@ int detector_finalize(fr_handle* h) {
   return FR_OK;
 }
 
-namespace {
-
-// cv::resize INTER_LINEAR coefficient table for one axis: (src0, src1, w0, w1) per output.
+// cv::resize INTER_LINEAR coefficient table for one axis: (src0, src1, w0, w1) per output
+// (also the resize branch of FaceEmbedder.preprocess, frhip_runtime.cpp).
 #pragma clang fp contract(off)
-void axis_table(int dsize, int ssize, int* t) {
+void resize_axis_table(int dsize, int ssize, int* t) {
   const double scale = 1.0 / ((double)dsize / ssize);
   for (int d = 0; d < dsize; ++d) {
     float f = (float)((d + 0.5) * scale - 0.5);
@@ -367,6 +366,16 @@ void axis_table(int dsize, int ssize, int* t) {
   }
 }
 #pragma clang fp contract(on)
+
+int resize_simd_end(int row) {
+  // SSE2 vertical pass: 16-element chunks while x <= row-16, then 8-element chunks while x < row-8
+  int x = 0;
+  while (x <= row - 16) x += 16;
+  while (x < row - 8) x += 8;
+  return x;
+}
+
+namespace {
 
 int dconv(fr_handle* h, const ConvW& c, const float* x, float* y, int B, int H, int W, Epi epi, const float* res,
           hipStream_t s) {
@@ -397,13 +406,9 @@ int setup_geometry(fr_handle* h, int height, int width, Geometry& g, hipStream_t
   if (g.new_w < 1 || g.new_h < 1) return fail(h, FR_ERR_INVALID_ARGUMENT, "frame too small to letterbox");
   g.det_scale = (double)g.new_h / height;
   d->htabs.assign((size_t)(g.new_w + g.new_h) * 4, 0);
-  axis_table(g.new_w, width, d->htabs.data());
-  axis_table(g.new_h, height, d->htabs.data() + 4 * g.new_w);
-  // SSE2 vertical pass: 16-element chunks while x <= width-16, then 8-element chunks while x < width-8
-  const int row = g.new_w * 3;
-  g.simd_end = 0;
-  while (g.simd_end <= row - 16) g.simd_end += 16;
-  while (g.simd_end < row - 8) g.simd_end += 8;
+  resize_axis_table(g.new_w, width, d->htabs.data());
+  resize_axis_table(g.new_h, height, d->htabs.data() + 4 * g.new_w);
+  g.simd_end = resize_simd_end(g.new_w * 3);
   FR_HIP(h, hipMemcpyAsync(d->tabs, d->htabs.data(), d->htabs.size() * sizeof(int), hipMemcpyHostToDevice, s));
   return FR_OK;
 }

@@ -165,9 +165,14 @@ hipError_t launch_l2norm_rows(const float* q, float* out, int n, int d, hipStrea
   return hipGetLastError();
 }
 
-// (score, index) total order: a before b  <=>  a.s > b.s || (a.s == b.s && a.i < b.i).
+// (score, index) total order: a before b  <=>  a.s > b.s || (a.s == b.s && a.i > b.i).
+// Equal scores rank the HIGHER gallery row first: that is np.argsort(s)[::-1] (the reference,
+// gallery_manager.py:197) whenever numpy's sort is stable -- its insertion sort for <= 16
+// elements, or kind="stable" -- i.e. a stable ascending sort, reversed.  (numpy's AVX-512
+// argsort leaves ties in no defined order)  NO_ROW ranks after any real row.
+constexpr int NO_ROW = -1;
 __device__ __forceinline__ bool ranks_before(float sa, int ia, float sb, int ib) {
-  return sa > sb || (sa == sb && ia < ib);
+  return sa > sb || (sa == sb && ia > ib);
 }
 
 // One wave per score row; k selection passes, each a strided scan for the best
@@ -180,10 +185,10 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sco
   const int lane = threadIdx.x & 63;
   const float* r = scores + (long long)row * G;
   float prev_s = INFINITY;
-  int prev_i = -1;
+  int prev_i = 0x7fffffff;  // ranks before every (score, row), +inf included
   for (int t = 0; t < k; ++t) {
     float bs = -INFINITY;
-    int bi = 0x7fffffff;
+    int bi = NO_ROW;
     for (int g = lane; g < G; g += 64) {
       const float s = r[g];
       if (s != s) continue;  // NaN never ranks
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sco
       }
     }
     if (lane == 0) {
-      idx[(long long)row * k + t] = bi == 0x7fffffff ? -1 : bi;
+      idx[(long long)row * k + t] = bi < 0 ? -1 : bi;
       val[(long long)row * k + t] = bs;
     }
     prev_s = bs;
@@ -226,7 +231,7 @@ __global__ __launch_bounds__(256) void topk_small_kernel(const float* __restrict
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) {
     ls[j] = -INFINITY;
-    li[j] = 0x7fffffff;
+    li[j] = NO_ROW;
   }
   auto push = [&](float sv, int iv) {
     if (sv != sv || !ranks_before(sv, iv, ls[KMAX - 1], li[KMAX - 1])) return;
@@ -283,17 +288,17 @@ __global__ __launch_bounds__(256) void topk_small_kernel(const float* __restrict
       }
     __syncthreads();
     if (tid == 0) {
-      idx[(long long)row * k + t] = bi == 0x7fffffff ? -1 : bi;
+      idx[(long long)row * k + t] = bi < 0 ? -1 : bi;
       val[(long long)row * k + t] = bs;
     }
-    if (li[0] == bi && bi != 0x7fffffff) {  // indices are unique: exactly one owner pops
+    if (li[0] == bi && bi >= 0) {  // indices are unique: exactly one owner pops
 #pragma unroll
       for (int j = 0; j < KMAX - 1; ++j) {
         ls[j] = ls[j + 1];
         li[j] = li[j + 1];
       }
       ls[KMAX - 1] = -INFINITY;
-      li[KMAX - 1] = 0x7fffffff;
+      li[KMAX - 1] = NO_ROW;
     }
   }
 }

@@ -482,6 +482,50 @@ int embed_device(fr_handle* h, const uint8_t* rgb, int n, float* out, int normal
   return FR_OK;
 }
 
+// cv2.resize(crop, (112, 112), INTER_LINEAR) of n H x W crops (face_embedder.py:94-96), device to
+// device, in OpenCV's fixed point (the letterbox kernel of the detector with a 112 x 112 canvas).
+// The coefficient tables are built once per source size and kept on the device.
+int resize_device(fr_handle* h, const uint8_t* src, int n, int H, int W, uint8_t* dst, hipStream_t s) {
+  const fr_handle::ResizeTab* t = nullptr;
+  for (const auto& r : h->rs_tabs)
+    if (r.H == H && r.W == W) t = &r;
+  if (!t) {
+    std::vector<int> host(4 * (112 + 112));
+    resize_axis_table(112, W, host.data());
+    resize_axis_table(112, H, host.data() + 4 * 112);
+    int* d = nullptr;
+    FR_HIP(h, hipMalloc((void**)&d, host.size() * sizeof(int)));
+    FR_HIP(h, hipMemcpy(d, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice));
+    h->rs_tabs.push_back({H, W, resize_simd_end(112 * 3), d});
+    t = &h->rs_tabs.back();
+  }
+  ProfScope ps(h, s, 0.0, 0);
+  hipError_t e = launch_letterbox(src, n, H, W, t->tab, t->tab + 4 * 112, 112, 112, t->simd_end, 112, 112, dst, s);
+  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("resize launch: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+int check_crop_size(fr_handle* h, int height, int width) {
+  if (height < 1 || width < 1 || height > 8192 || width > 8192)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "crop height/width must be in [1, 8192]");
+  return FR_OK;
+}
+
+// Embed n crops of any size: 112 x 112 go straight to the forward, others through resize_device
+// one max_batch chunk at a time.
+int embed_any(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize,
+              hipStream_t s) {
+  if (height == 112 && width == 112) return embed_device(h, rgb, n, out, normalize, s);
+  for (int off = 0; off < n; off += h->max_batch) {
+    const int bn = std::min(h->max_batch, n - off);
+    int rc = resize_device(h, rgb + (size_t)off * height * width * 3, bn, height, width, h->rs_stage, s);
+    if (rc) return rc;
+    rc = embed_device(h, h->rs_stage, bn, out + (size_t)off * 512, normalize, s);
+    if (rc) return rc;
+  }
+  return FR_OK;
+}
+
 int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float* score, hipStream_t s) {
   if (h->G <= 0) return fail(h, FR_ERR_STATE, "gallery is empty (fr_gallery_set first)");
   if (k < 1 || k > h->G) return fail(h, FR_ERR_INVALID_ARGUMENT, "k must be in [1, G]");
@@ -930,6 +974,7 @@ int fr_finalize(fr_handle* h) {
     FR_HIP(h, hipMalloc((void**)&h->sc_buf, mb * 56 * 56 * 64 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->partial, (size_t)h->head_split * mb * 512 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->in_stage, mb * 112 * 112 * 3));
+    FR_HIP(h, hipMalloc((void**)&h->rs_stage, mb * 112 * 112 * 3));
     FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
   }
@@ -952,11 +997,20 @@ int fr_embed(fr_handle* h, const uint8_t* rgb, int n, int height, int width, flo
   std::lock_guard<std::mutex> lk(h->mu);
   if (h->detector) return fail(h, FR_ERR_STATE, "this handle is a detector (scrfd_10g); use fr_detect");
   if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
-  if (height != 112 || width != 112)
-    return fail(h, FR_ERR_INVALID_ARGUMENT, "input must be 112x112x3 (resize is done by the caller)");
+  if (int rc = check_crop_size(h, height, width)) return rc;
   if (n < 0 || (n > 0 && (!rgb || !out))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
   DeviceGuard dg(h->device);
-  return embed_device(h, rgb, n, out, normalize, (hipStream_t)stream);
+  return embed_any(h, rgb, n, height, width, out, normalize, (hipStream_t)stream);
+}
+
+int fr_resize_crops(fr_handle* h, const uint8_t* src, int n, int height, int width, uint8_t* dst, void* stream) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_crop_size(h, height, width)) return rc;
+  if (n < 0 || (n > 0 && (!src || !dst))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
+  if (n == 0) return FR_OK;
+  DeviceGuard dg(h->device);
+  return resize_device(h, src, n, height, width, dst, (hipStream_t)stream);
 }
 
 int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize) {
@@ -964,15 +1018,22 @@ int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width
   std::lock_guard<std::mutex> lk(h->mu);
   if (h->detector) return fail(h, FR_ERR_STATE, "this handle is a detector (scrfd_10g); use fr_detect");
   if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
-  if (height != 112 || width != 112)
-    return fail(h, FR_ERR_INVALID_ARGUMENT, "input must be 112x112x3 (resize is done by the caller)");
+  if (int rc = check_crop_size(h, height, width)) return rc;
   if (n < 0 || (n > 0 && (!rgb || !out))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
   DeviceGuard dg(h->device);
   hipStream_t s = nullptr;
+  const size_t crop = (size_t)height * width * 3;
   for (int off = 0; off < n; off += h->max_batch) {
     const int bn = std::min(h->max_batch, n - off);
-    FR_HIP(h, hipMemcpyAsync(h->in_stage, rgb + (size_t)off * 112 * 112 * 3, (size_t)bn * 112 * 112 * 3,
-                             hipMemcpyHostToDevice, s));
+    if (height == 112 && width == 112) {
+      FR_HIP(h, hipMemcpyAsync(h->in_stage, rgb + (size_t)off * crop, (size_t)bn * crop, hipMemcpyHostToDevice, s));
+    } else {  // raw crops to the device, then cv2.resize to 112 x 112 into the forward's input
+      int rc = ensure_buf(h, &h->rs_src, &h->rs_src_cap, (size_t)bn * crop);
+      if (rc) return rc;
+      FR_HIP(h, hipMemcpyAsync(h->rs_src, rgb + (size_t)off * crop, (size_t)bn * crop, hipMemcpyHostToDevice, s));
+      rc = resize_device(h, static_cast<const uint8_t*>(h->rs_src), bn, height, width, h->in_stage, s);
+      if (rc) return rc;
+    }
     int rc = forward_staged(h, bn, normalize, s);
     if (rc) return rc;
     FR_HIP(h, hipMemcpyAsync(out + (size_t)off * 512, h->emb_stage, (size_t)bn * 512 * sizeof(float),

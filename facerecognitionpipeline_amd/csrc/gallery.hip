@@ -87,7 +87,8 @@ __global__ __launch_bounds__(256) void template_kernel(const float* __restrict__
       int c = 0;
       for (int i = 0; i < N; ++i)
         if (avg[i] >= min_sim) keep_idx[c++] = i;
-      if (c < 2) {  // np.argsort(avg)[-2:]: the two largest (higher index on ties, as a stable sort)
+      if (c < 2) {  // np.argsort(avg)[-2:]: the two largest; ties take the higher index, as a stable sort
+        // would (numpy's default argsort leaves tie order unspecified)
         int a = -1, b = -1;
         for (int i = 0; i < N; ++i) {
           if (a < 0 || avg[i] >= avg[a]) {

@@ -81,6 +81,18 @@ struct fr_handle {
   uint8_t* in_stage = nullptr;
   float* emb_stage = nullptr;
 
+  // resize branch of FaceEmbedder.preprocess (face_embedder.py:94-96): cv2.resize INTER_LINEAR
+  // coefficient tables per source size ([112 x][4] then [112 y][4], device), resized crops of one
+  // chunk, and host-API staging of the raw crops
+  struct ResizeTab {
+    int H, W, simd_end;
+    int* tab;
+  };
+  std::vector<ResizeTab> rs_tabs;
+  uint8_t* rs_stage = nullptr;
+  void* rs_src = nullptr;
+  size_t rs_src_cap = 0;
+
   // gallery + match workspace
   float* gallery = nullptr;
   int G = 0;
@@ -157,6 +169,9 @@ struct fr_handle {
     (void)hipFree(partial);
     (void)hipFree(in_stage);
     (void)hipFree(emb_stage);
+    for (auto& t : rs_tabs) (void)hipFree(t.tab);
+    (void)hipFree(rs_stage);
+    (void)hipFree(rs_src);
     (void)hipFree(gallery);
     (void)hipFree(qn);
     (void)hipFree(scores);
@@ -217,6 +232,10 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
 const std::vector<float>* getp(fr_handle* h, const std::string& k);
 
 // detector.cpp
+// cv::resize INTER_LINEAR (uint8) coefficient table of one axis: (src0, src1, w0, w1) per output
+void resize_axis_table(int dsize, int ssize, int* t);
+// end of the SSE2-vectorised part of a resized row of row_elems bytes (the rest rounds as scalar code)
+int resize_simd_end(int row_elems);
 std::map<std::string, size_t> detector_schema();
 int detector_finalize(fr_handle* h);
 int detector_run(fr_handle* h, const uint8_t* frames, int n, int height, int width, float det_thresh, int max_faces,

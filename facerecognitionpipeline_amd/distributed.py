@@ -50,8 +50,11 @@ def gather_topk(idx: torch.Tensor, score: torch.Tensor, n_total: int, group=None
     world = dist.get_world_size(group)
     k = idx.shape[1]
     longest = shard_range(n_total, world, 0)[1]
-    pad_i = torch.full((longest, k), -1, dtype=torch.int32, device=idx.device)
-    pad_s = torch.zeros((longest, k), dtype=torch.float32, device=score.device)
+    # gloo gathers host tensors only: device results go through the host there (RCCL gathers
+    # them in place)
+    dev = idx.device if (idx.device.type == "cpu" or dist.get_backend(group) != "gloo") else torch.device("cpu")
+    pad_i = torch.full((longest, k), -1, dtype=torch.int32, device=dev)
+    pad_s = torch.zeros((longest, k), dtype=torch.float32, device=dev)
     pad_i[: idx.shape[0]] = idx
     pad_s[: score.shape[0]] = score
     all_i = [torch.empty_like(pad_i) for _ in range(world)]
@@ -163,8 +166,11 @@ def sync_gallery(gm, handle, device: torch.device, src: int = 0, group=None,
                  matrix: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """Every rank: bring ``handle`` (this rank's libfrhip handle; on ``src`` the one the
     GalleryManager is attached to) or ``matrix`` up to ``src``'s gallery.  ``gm`` on src only."""
-    mode, payload = broadcast_gallery_update(gm, device, src=src, group=group)
-    out = apply_gallery_update(mode, payload, handle=handle, matrix=matrix)
-    if dist.get_rank(group) == src and mode != SYNC_NONE:
-        gm._mark_synced(list(gm.students.keys()))
+    import contextlib
+    # on src, the gallery lock spans building the delta, applying it and marking it synced
+    with (gm._lock if gm is not None else contextlib.nullcontext()):
+        mode, payload = broadcast_gallery_update(gm, device, src=src, group=group)
+        out = apply_gallery_update(mode, payload, handle=handle, matrix=matrix)
+        if dist.get_rank(group) == src and mode != SYNC_NONE:
+            gm._mark_synced(list(gm.students.keys()))
     return out

@@ -7,9 +7,11 @@ uint8 crops go to HBM once, the stem kernel fuses the BGR flip and the
 ``(x/255-0.5)/0.5`` normalisation, and the embedding comes back already
 L2-normalised the way the reference's ``normalize=True`` path leaves it.
 
-Differences (documented in DESIGN.md): inputs must already be 112x112 (the
-reference would ``cv2.resize`` them, face_embedder.py:94-96; cv2 is absent
-here), ``model_type='arcface'`` runs the same kernels with the insightface
+Crops of any other size go through the device restatement of the reference's
+``cv2.resize(..., (112, 112), INTER_LINEAR)`` (face_embedder.py:94-96; OpenCV's
+fixed-point bilinear, parity vs cv2 itself unpinned: cv2 is absent here).
+
+Differences (documented in DESIGN.md): ``model_type='arcface'`` runs the same kernels with the insightface
 IResNet weights of an ``arcface_torch`` state dict (the ONNX files the reference
 loads need onnxruntime, which is absent), and ``device`` must be a HIP device —
 there is no CPU fallback.
@@ -93,9 +95,14 @@ class FaceEmbedder:
     # -- reference API -------------------------------------------------------
     def preprocess(self, face_image: np.ndarray):
         """Host input exactly as face_embedder.py:93-110 builds it (for API parity; the
-        GPU path does the same arithmetic inside the stem kernel): a float32 torch tensor
-        for AdaFace, a float32 numpy array for ArcFace."""
+        GPU path does the same arithmetic inside the resize and stem kernels): a float32
+        torch tensor for AdaFace, a float32 numpy array for ArcFace."""
         self._check_shape(face_image)
+        if face_image.shape[:2] != self.input_size:
+            x = torch.from_numpy(np.ascontiguousarray(self._as_u8(face_image))[None]).to(self.device)
+            out = torch.empty((1,) + self.input_size + (3,), dtype=torch.uint8, device=self.device)
+            self.model.resize_crops(x, out)
+            face_image = out[0].cpu().numpy()
         bgr = face_image[:, :, ::-1]
         if self.model_type == "arcface":
             bgr = (bgr - self.mean) / self.std
@@ -112,12 +119,34 @@ class FaceEmbedder:
         batch-invariant and chunks by the handle's max_batch instead."""
         if len(face_images) == 0:
             return np.array([])
+        out = self.embed_tensor(self.to_device_crops(face_images), normalize=normalize)
+        return out.cpu().numpy()
+
+    def to_device_crops(self, face_images: List[np.ndarray]) -> torch.Tensor:
+        """Host HxWx3 crops -> uint8 [N,112,112,3] on the device: 112x112 crops uploaded as they
+        are, any other size uploaded and resized there (cv2.resize INTER_LINEAR restatement,
+        face_embedder.py:94-96), one launch per distinct size."""
         for f in face_images:
             self._check_shape(f)
-        host = np.ascontiguousarray(np.stack(face_images).astype(np.uint8, copy=False))
-        rgb = torch.from_numpy(host).to(self.device, non_blocking=False)
-        out = self.embed_tensor(rgb, normalize=normalize)
-        return out.cpu().numpy()
+        if all(f.shape[:2] == self.input_size for f in face_images):
+            host = np.ascontiguousarray(np.stack([self._as_u8(f) for f in face_images]))
+            rgb = torch.from_numpy(host).to(self.device, non_blocking=False)
+        else:
+            # cv2.resize branch (face_embedder.py:94-96) on the device, one launch per crop size
+            rgb = torch.empty((len(face_images),) + self.input_size + (3,), dtype=torch.uint8, device=self.device)
+            by_size = {}
+            for i, f in enumerate(face_images):
+                by_size.setdefault(f.shape[:2], []).append(i)
+            for size, rows in by_size.items():
+                src = torch.from_numpy(np.ascontiguousarray(np.stack([self._as_u8(face_images[i]) for i in rows])))
+                src = src.to(self.device)
+                if size == self.input_size:
+                    rgb[rows] = src
+                else:
+                    tmp = torch.empty((len(rows),) + self.input_size + (3,), dtype=torch.uint8, device=self.device)
+                    self.model.resize_crops(src, tmp)
+                    rgb[rows] = tmp
+        return rgb
 
     def compute_similarity(self, embedding1: np.ndarray, embedding2: np.ndarray) -> float:
         e1 = embedding1 / (np.linalg.norm(embedding1) + 1e-8)
@@ -160,6 +189,20 @@ class FaceEmbedder:
     def _check_shape(self, face_image: np.ndarray) -> None:
         if face_image.ndim != 3 or face_image.shape[2] != 3:
             raise ValueError(f"expected an HxWx3 RGB crop, got shape {face_image.shape}")
-        if face_image.shape[:2] != self.input_size:
-            raise ValueError(f"crop is {face_image.shape[:2]}, expected {self.input_size}: resize to 112x112 first "
-                             "(cv2.resize INTER_LINEAR in the reference, face_embedder.py:94-96)")
+        if min(face_image.shape[:2]) < 1 or max(face_image.shape[:2]) > 8192:
+            raise ValueError(f"crop size {face_image.shape[:2]} out of range [1, 8192]")
+
+    _as_u8 = staticmethod(lambda face_image: as_uint8_crop(face_image))
+
+
+def as_uint8_crop(face_image: np.ndarray) -> np.ndarray:
+    """The device path computes on uint8 pixels (a 256-entry LUT of the reference's float64
+    normalisation, face_embedder.py:99-100).  Non-uint8 crops whose values are integers in
+    [0, 255] convert exactly, so the result is the reference's; any other value (fractional,
+    out of range) would be normalised differently, so it is refused."""
+    a = np.asarray(face_image)
+    if a.dtype == np.uint8:
+        return a
+    if a.dtype.kind in "biuf" and np.all(np.isfinite(a)) and np.all((a >= 0) & (a <= 255) & (a == np.floor(a))):
+        return a.astype(np.uint8)
+    raise ValueError(f"crops must be uint8 (or integer-valued in [0, 255]); got {a.dtype} with other values")

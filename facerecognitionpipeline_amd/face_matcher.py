@@ -37,20 +37,6 @@ class FaceMatcher:
         """Batched match_single_face: one device embed+match for all crops."""
         if len(face_images) == 0:
             return []
-        g = self.gallery
-        if not g.students:
-            return [[] for _ in face_images]
-        k = _slice_len(len(g.students), top_k)
-        if k == 0:
-            return [[] for _ in face_images]
-        for f in face_images:
-            self.embedder._check_shape(f)
-        dev = self.embedder.device
-        rgb = torch.from_numpy(np.ascontiguousarray(np.stack(face_images), dtype=np.uint8)).to(dev)
-        h = g._sync_device()
-        idx = torch.empty((len(face_images), k), dtype=torch.int32, device=dev)
-        score = torch.empty((len(face_images), k), dtype=torch.float32, device=dev)
-        h.embed_match(rgb, k, idx, score)
-        idx, score = idx.cpu().numpy(), score.cpu().numpy()
-        return [[(g._ids[i], g.students[g._ids[i]].name, float(s)) for i, s in zip(ri, rs)]
-                for ri, rs in zip(idx, score)]
+        rgb = self.embedder.to_device_crops(list(face_images))  # validates; resizes non-112 crops
+        return self.gallery.match_resolved(len(face_images), top_k,
+                                           lambda h, k, idx, score: h.embed_match(rgb, k, idx, score))

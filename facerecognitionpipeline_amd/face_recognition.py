@@ -206,10 +206,17 @@ class FaceProcessor:
         faces = self.detector.detect(image_rgb)
         if len(faces) == 0:
             return []
-        frame = torch.from_numpy(np.ascontiguousarray(image_rgb, np.uint8)).to(self.aligner._ops.device)
+        # a grayscale frame is warped as three equal channels: each channel of the warp is the
+        # reference's single-channel warpAffine (face_recognition.py:72-74), and RGB2GRAY of
+        # (g, g, g) is g, so the blur score is the reference's on the 2-D crop (:94-99); the
+        # aligned face is handed back 2-D, as the reference's is
+        gray = np.ndim(image_rgb) == 2
+        frame = torch.from_numpy(FaceDetector._to_rgb(image_rgb)).to(self.aligner._ops.device)
         crops = self.aligner.align_batch(frame, np.stack([f["landmarks"] for f in faces]))
         blur = self.quality_filter.compute_blur_scores(crops) if self.quality_filter.check_blur else None
         host = crops.cpu().numpy()
+        if gray:
+            host = np.ascontiguousarray(host[..., 0])
         results = []
         for i, face in enumerate(faces):
             ok, q = self.quality_filter.is_valid(face, None, None if blur is None else float(blur[i]))

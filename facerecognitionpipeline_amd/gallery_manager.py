@@ -25,6 +25,7 @@ from __future__ import annotations
 import json
 import os
 import shutil
+import threading
 import uuid
 from dataclasses import dataclass, field
 from datetime import datetime
@@ -74,12 +75,47 @@ MAX_PENDING_OPS = 256  # beyond this a full upload is cheaper than replaying row
 OP_PUT, OP_DELETE = 0, 1
 
 
+def _delta_layout(g_old: int, ops) -> List[Tuple[bool, int]]:
+    """Final row order after replaying ``ops`` on ``g_old`` rows: per final row, (True, old
+    row it keeps) or (False, index into the PUT rows)."""
+    src: List[Tuple[bool, int]] = [(True, i) for i in range(g_old)]
+    r = 0
+    for kind, row in ops:
+        if kind == OP_DELETE:
+            src.pop(row)
+        else:
+            if row == len(src):
+                src.append((False, r))
+            else:
+                src[row] = (False, r)
+            r += 1
+    return src
+
+
 def apply_gallery_delta(handle: "_lib.Handle", ops: torch.Tensor, rows: torch.Tensor) -> None:
     """Replay a compiled delta on a handle's HBM gallery.  ``ops`` int32 [n,2] of
-    (OP_PUT, row) / (OP_DELETE, row); PUTs consume ``rows`` [m,512] in order.  Runs of
-    PUTs to consecutive rows become one write."""
+    (OP_PUT, row) / (OP_DELETE, row); PUTs consume ``rows`` [m,512] in order.
+
+    Without deletes, runs of PUTs to consecutive rows become one write each.  With deletes
+    the final layout is computed on the host and the gallery is rebuilt in ONE device pass
+    (gather of the surviving rows + the new ones), instead of one tail compaction per
+    delete (O(G) each)."""
     ops = ops.cpu().tolist()
     rows = rows.to(handle.device, torch.float32)
+    if any(kind == OP_DELETE for kind, _row in ops):
+        layout = _delta_layout(handle.gallery_size(), ops)
+        E = handle.gallery_read()
+        out = torch.empty((len(layout), 512), dtype=torch.float32, device=handle.device)
+        keep = [(j, i) for j, (old, i) in enumerate(layout) if old]
+        new = [(j, i) for j, (old, i) in enumerate(layout) if not old]
+        if keep:
+            dst, srcr = (torch.tensor(c, dtype=torch.long, device=handle.device) for c in zip(*keep))
+            out[dst] = E[srcr]
+        if new:
+            dst, srcr = (torch.tensor(c, dtype=torch.long, device=handle.device) for c in zip(*new))
+            out[dst] = rows[srcr]
+        handle.gallery_replace(out)
+        return
     i, r = 0, 0
     while i < len(ops):
         kind, row = ops[i]
@@ -127,6 +163,10 @@ class GalleryManager:
         self._ids: List[str] = []  # row order of the HBM copy
         self._uid = uuid.uuid4().hex
         self._pending: Optional[List[Tuple[int, str]]] = None  # row ops since the HBM copy; None = full
+        # one lock per manager: mutations, the HBM sync and each search's row -> id resolution
+        # are atomic with respect to each other (the reference server shares one GalleryManager
+        # across Flask request threads, face_recognition_server.py:1102)
+        self._lock = threading.RLock()
         os.makedirs(os.path.dirname(gallery_path) or ".", exist_ok=True)
         if os.path.exists(self._arrays_path(gallery_path)):
             self.load()
@@ -137,67 +177,71 @@ class GalleryManager:
     # -- records -------------------------------------------------------------
     def add_student(self, student_id: str, name: str, embeddings: np.ndarray, metadata: Optional[Dict] = None,
                     overwrite: bool = False) -> bool:
-        if student_id in self.students and not overwrite:
-            self._log(f"Student {student_id} already exists. Use overwrite=True to replace.")
-            return False
-        emb = embeddings.reshape(1, -1) if embeddings.ndim == 1 else embeddings
-        now = datetime.now().isoformat()
-        self.students[student_id] = StudentRecord(student_id, name, emb, self._aggregate_embeddings(emb),
-                                                  len(emb), now, now, metadata or {})
-        self._touch((OP_PUT, student_id))
-        self._log(f"{'Updated' if overwrite else 'Added'} student: {name} ({student_id}) with {len(emb)} embeddings")
-        return True
+        with self._lock:
+            if student_id in self.students and not overwrite:
+                self._log(f"Student {student_id} already exists. Use overwrite=True to replace.")
+                return False
+            emb = embeddings.reshape(1, -1) if embeddings.ndim == 1 else embeddings
+            now = datetime.now().isoformat()
+            self.students[student_id] = StudentRecord(student_id, name, emb, self._aggregate_embeddings(emb),
+                                                      len(emb), now, now, metadata or {})
+            self._touch((OP_PUT, student_id))
+            self._log(f"{'Updated' if overwrite else 'Added'} student: {name} ({student_id}) with {len(emb)} embeddings")
+            return True
 
     def update_embeddings(self, student_id: str, new_embeddings: np.ndarray, mode: str = "append") -> bool:
-        rec = self.students.get(student_id)
-        if rec is None:
-            self._log(f"Student {student_id} not found")
-            return False
-        new = new_embeddings.reshape(1, -1) if new_embeddings.ndim == 1 else new_embeddings
-        if mode == "append":
-            emb = np.vstack([rec.embeddings, new])
-        elif mode == "replace":
-            emb = new
-        elif mode == "merge":
-            emb = self._remove_outliers(np.vstack([rec.embeddings, new]))
-        else:
-            raise ValueError(f"Unknown mode: {mode}")
-        rec.embeddings = emb
-        rec.template_embedding = self._aggregate_embeddings(emb)
-        rec.num_samples = len(emb)
-        rec.last_updated = datetime.now().isoformat()
-        self._touch((OP_PUT, student_id))
-        return True
+        with self._lock:
+            rec = self.students.get(student_id)
+            if rec is None:
+                self._log(f"Student {student_id} not found")
+                return False
+            new = new_embeddings.reshape(1, -1) if new_embeddings.ndim == 1 else new_embeddings
+            if mode == "append":
+                emb = np.vstack([rec.embeddings, new])
+            elif mode == "replace":
+                emb = new
+            elif mode == "merge":
+                emb = self._remove_outliers(np.vstack([rec.embeddings, new]))
+            else:
+                raise ValueError(f"Unknown mode: {mode}")
+            rec.embeddings = emb
+            rec.template_embedding = self._aggregate_embeddings(emb)
+            rec.num_samples = len(emb)
+            rec.last_updated = datetime.now().isoformat()
+            self._touch((OP_PUT, student_id))
+            return True
 
     def delete_student(self, student_id: str) -> bool:
-        if student_id not in self.students:
-            self._log(f"Student {student_id} not found")
-            return False
-        del self.students[student_id]
-        self._touch((OP_DELETE, student_id))
-        return True
+        with self._lock:
+            if student_id not in self.students:
+                self._log(f"Student {student_id} not found")
+                return False
+            del self.students[student_id]
+            self._touch((OP_DELETE, student_id))
+            return True
 
     def add_students_batch(self, entries: Sequence[Tuple[str, str, np.ndarray]], overwrite: bool = False,
                            min_similarity: float = 0.70) -> int:
         """``add_student`` for many students, templates built in one GPU launch
         (``fr_build_templates``).  ``entries``: (student_id, name, embeddings [n_i,512]).
         Returns how many were added (existing ids are skipped unless ``overwrite``)."""
-        todo = [(sid, name, np.asarray(e, np.float32).reshape(-1, 512)) for sid, name, e in entries
-                if overwrite or sid not in self.students]
-        if not todo:
-            return 0
-        h = self._get_handle()
-        offsets = np.zeros(len(todo) + 1, np.int64)
-        offsets[1:] = np.cumsum([len(e) for _s, _n, e in todo])
-        allemb = torch.from_numpy(np.ascontiguousarray(np.concatenate([e for _s, _n, e in todo]))).to(self.device)
-        tpl, _kept = h.build_templates(allemb, offsets, self.aggregation_method, min_similarity)
-        tpl = tpl.cpu().numpy()
-        now = datetime.now().isoformat()
-        for i, (sid, name, e) in enumerate(todo):
-            self.students[sid] = StudentRecord(sid, name, e, tpl[i], len(e), now, now, {})
-            self._touch((OP_PUT, sid))
-        self._log(f"Added {len(todo)} students (templates built on {self.device})")
-        return len(todo)
+        with self._lock:
+            todo = [(sid, name, np.asarray(e, np.float32).reshape(-1, 512)) for sid, name, e in entries
+                    if overwrite or sid not in self.students]
+            if not todo:
+                return 0
+            h = self._get_handle()
+            offsets = np.zeros(len(todo) + 1, np.int64)
+            offsets[1:] = np.cumsum([len(e) for _s, _n, e in todo])
+            allemb = torch.from_numpy(np.ascontiguousarray(np.concatenate([e for _s, _n, e in todo]))).to(self.device)
+            tpl, _kept = h.build_templates(allemb, offsets, self.aggregation_method, min_similarity)
+            tpl = tpl.cpu().numpy()
+            now = datetime.now().isoformat()
+            for i, (sid, name, e) in enumerate(todo):
+                self.students[sid] = StudentRecord(sid, name, e, tpl[i], len(e), now, now, {})
+                self._touch((OP_PUT, sid))
+            self._log(f"Added {len(todo)} students (templates built on {self.device})")
+            return len(todo)
 
     def get_student(self, student_id: str) -> Optional[StudentRecord]:
         return self.students.get(student_id)
@@ -213,32 +257,46 @@ class GalleryManager:
 
     # -- matching (device) ---------------------------------------------------
     def search(self, query_embedding: np.ndarray, top_k: int = 5) -> List[Tuple[str, str, float]]:
-        if not self.students:
-            return []
         return self.search_batch(np.asarray(query_embedding).reshape(1, -1), top_k)[0]
 
     def search_batch(self, queries: np.ndarray, top_k: int = 5) -> List[List[Tuple[str, str, float]]]:
         """search() for every row of ``queries`` [n, 512], one device round trip."""
-        if not self.students:
-            return [[] for _ in range(len(queries))]
-        k = _slice_len(len(self.students), top_k)
-        if k == 0:
-            return [[] for _ in range(len(queries))]
         q = torch.from_numpy(np.ascontiguousarray(queries, dtype=np.float32)).to(self.device)
-        idx, score = self.search_device(q, k)
-        idx, score = idx.cpu().numpy(), score.cpu().numpy()
-        return [[(self._ids[i], self.students[self._ids[i]].name, float(s)) for i, s in zip(ri, rs)]
-                for ri, rs in zip(idx, score)]
+        return self.match_resolved(len(queries), top_k, lambda h, k, idx, score: h.match(q, k, idx, score))
+
+    def match_resolved(self, n: int, top_k: int, launch) -> List[List[Tuple[str, str, float]]]:
+        """Bring the HBM copy up to date, run ``launch(handle, k, idx, score)`` (any kernel
+        sequence that fills idx/score [n,k] with gallery rows), and turn rows into
+        ``(sid, name, score)`` -- all under the gallery lock, so a concurrent mutation can
+        neither change the rows between the match and their resolution nor make two threads
+        replay one delta twice."""
+        with self._lock:
+            if not self.students:
+                return [[] for _ in range(n)]
+            k = _slice_len(len(self.students), top_k)
+            if k == 0 or n == 0:
+                return [[] for _ in range(n)]
+            h = self._sync_device()
+            idx = torch.empty((n, k), dtype=torch.int32, device=self.device)
+            score = torch.empty((n, k), dtype=torch.float32, device=self.device)
+            launch(h, k, idx, score)
+            idx, score = idx.cpu().numpy(), score.cpu().numpy()
+            ids = self._ids
+            return [[(ids[i], self.students[ids[i]].name, float(s)) for i, s in zip(ri, rs)]
+                    for ri, rs in zip(idx, score)]
 
     def search_device(self, queries: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """Device form: float32 [n,512] on the GPU -> (int32 [n,k] gallery rows, float32 [n,k] scores).
-        Row order is ``get_gallery_embeddings()`` order (dict insertion order)."""
-        h = self._sync_device()
-        n = queries.shape[0]
-        idx = torch.empty((n, k), dtype=torch.int32, device=self.device)
-        score = torch.empty((n, k), dtype=torch.float32, device=self.device)
-        h.match(queries.contiguous(), k, idx, score)
-        return idx, score
+        Row order is ``get_gallery_embeddings()`` order (dict insertion order) at the time of the
+        call; a caller that resolves rows while other threads mutate the gallery holds ``_lock``
+        across both (or uses :meth:`match_resolved`)."""
+        with self._lock:
+            h = self._sync_device()
+            n = queries.shape[0]
+            idx = torch.empty((n, k), dtype=torch.int32, device=self.device)
+            score = torch.empty((n, k), dtype=torch.float32, device=self.device)
+            h.match(queries.contiguous(), k, idx, score)
+            return idx, score
 
     @property
     def device(self) -> torch.device:
@@ -302,6 +360,10 @@ class GalleryManager:
         self._handle.gallery_tag = (self._uid, self._version)
 
     def _sync_device(self) -> "_lib.Handle":
+        with self._lock:
+            return self._sync_device_locked()
+
+    def _sync_device_locked(self) -> "_lib.Handle":
         h = self._get_handle()
         if self._device_version == self._version and self._device_current():
             return h
@@ -337,27 +399,29 @@ class GalleryManager:
             json.dump(meta, f, indent=2)
 
     def load(self, path: Optional[str] = None) -> None:
-        path = path or self.gallery_path
-        arr_path = self._arrays_path(path)
-        if not os.path.exists(arr_path):
-            self._log(f"Gallery file not found: {arr_path}")
-            return
-        with open(os.path.splitext(path)[0] + ".json") as f:
-            meta = json.load(f)
-        arrays = np.load(arr_path)
-        self.students = {}
-        for i, s in enumerate(meta["order"]):
-            m = meta["students"][s]
-            self.students[s] = StudentRecord(s, m["name"], arrays[f"e{i}"], arrays[f"t{i}"], m["num_samples"],
-                                             m["enrollment_date"], m["last_updated"], m.get("metadata", {}))
-        self._touch()
+        with self._lock:
+            path = path or self.gallery_path
+            arr_path = self._arrays_path(path)
+            if not os.path.exists(arr_path):
+                self._log(f"Gallery file not found: {arr_path}")
+                return
+            with open(os.path.splitext(path)[0] + ".json") as f:
+                meta = json.load(f)
+            arrays = np.load(arr_path)
+            self.students = {}
+            for i, s in enumerate(meta["order"]):
+                m = meta["students"][s]
+                self.students[s] = StudentRecord(s, m["name"], arrays[f"e{i}"], arrays[f"t{i}"], m["num_samples"],
+                                                 m["enrollment_date"], m["last_updated"], m.get("metadata", {}))
+            self._touch()
 
     def load_backup(self, json_path: str) -> None:
         """Import a reference ``export_for_backup`` JSON (gallery_manager.py:246-270)."""
-        with open(json_path) as f:
-            data = json.load(f)
-        self.students = {sid: StudentRecord.from_dict(d) for sid, d in data["students"].items()}
-        self._touch()
+        with self._lock:
+            with open(json_path) as f:
+                data = json.load(f)
+            self.students = {sid: StudentRecord.from_dict(d) for sid, d in data["students"].items()}
+            self._touch()
 
     def export_for_backup(self, backup_dir: str, backup_name: Optional[str] = None) -> str:
         os.makedirs(backup_dir, exist_ok=True)

@@ -24,7 +24,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from .face_embedder import FaceEmbedder
+from .face_embedder import FaceEmbedder, as_uint8_crop
 from .face_recognition import FaceAligner, FaceQualityFilter
 from .gallery_manager import GalleryManager, _slice_len
 
@@ -63,18 +63,12 @@ class RecognitionPipeline:
                         "is_valid": ok, "matches": [], "recognized": False})
             if ok:
                 valid.append(i)
-        g = self.gallery
-        k = _slice_len(len(g.students), top_k)
-        if not valid or k == 0:
+        if not valid:
             return out
-        h = g._sync_device()
         sel = crops[torch.tensor(valid, device=dev)].contiguous()
-        idx = torch.empty((len(valid), k), dtype=torch.int32, device=dev)
-        score = torch.empty((len(valid), k), dtype=torch.float32, device=dev)
-        h.embed_match(sel, k, idx, score)
-        idx, score = idx.cpu().numpy(), score.cpu().numpy()
+        res = self.gallery.match_resolved(len(valid), top_k, lambda h, k, idx, score: h.embed_match(sel, k, idx, score))
         for row, i in enumerate(valid):
-            m = [(g._ids[j], g.students[g._ids[j]].name, float(s)) for j, s in zip(idx[row], score[row])]
+            m = res[row]
             out[i]["matches"] = m
             out[i]["recognized"] = bool(m) and m[0][2] >= self.similarity_threshold
         return out
@@ -90,9 +84,10 @@ class MatchBatcher:
     thread gathers whatever is pending -- up to ``max_batch`` crops, waiting at most
     ``max_wait_ms`` after the first -- into ONE ``FaceMatcher.match_faces`` call, i.e.
     one ``fr_embed_match`` (a replayed hipGraph when the batch is small).  Each
-    caller gets exactly what ``match_single_face`` would return: the embedder is
-    batch-invariant and the top-k kernel is exact with the same tie order, so the
-    first ``top_k`` of a larger k are the top-``top_k``.
+    caller gets what ``match_single_face`` would return, to fp32 summation order: the
+    forward is batch-invariant within 1e-6 per embedding element (the stream-K schedule
+    cuts a batch-size-dependent set of tiles along K), and the top-k kernel is exact
+    with the same tie order, so the first ``top_k`` of a larger k are the top-``top_k``.
 
     Errors keep the reference behaviour per request: a crop of the wrong shape raises
     ``ValueError`` in the calling thread before it is queued; a failure of the batched
@@ -115,7 +110,7 @@ class MatchBatcher:
     def submit(self, face_image: np.ndarray, top_k: int = 5) -> Future:
         self.matcher.embedder._check_shape(face_image)
         fut: Future = Future()
-        item = (np.ascontiguousarray(face_image, dtype=np.uint8), int(top_k), fut)
+        item = (np.ascontiguousarray(as_uint8_crop(face_image)), int(top_k), fut)
         with self._lock:
             if self._closed:
                 raise RuntimeError("MatchBatcher is closed")

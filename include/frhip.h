@@ -13,12 +13,16 @@
  *  - "device" pointers are HIP device allocations on the handle's device;
  *    "host" pointers are ordinary host memory, borrowed for the call only.
  *  - `stream` is a hipStream_t (NULL = the null stream).  Device-pointer calls
- *    are asynchronous on that stream; host-pointer calls synchronise.
+ *    are asynchronous on that stream; host-pointer calls synchronise.  Every call
+ *    on one handle must use the SAME stream: the handle's workspace (activations,
+ *    stream-K slabs and tickets, staging buffers, captured graphs) is shared by
+ *    all of its calls and only stream order keeps them apart.
  *  - One mutex per handle: a handle may be shared by threads (the reference
  *    server shares one FaceEmbedder/GalleryManager across Flask request
  *    threads, face_recognition_server.py:1102).
- *  - Embeddings are 512-d float32 rows; images are uint8 RGB HWC 112x112x3,
- *    C-contiguous (the reference's aligned crops, face_recognition.py:64-74).
+ *  - Embeddings are 512-d float32 rows; images are uint8 RGB HWC, C-contiguous:
+ *    112x112x3 (the reference's aligned crops, face_recognition.py:64-74), or any
+ *    size for fr_embed / fr_embed_host, which resize it first (face_embedder.py:94-96).
  */
 #ifndef FRHIP_H_
 #define FRHIP_H_
@@ -62,13 +66,18 @@ int fr_set_param(fr_handle* h, const char* name, const float* host_data, int64_t
 int fr_finalize(fr_handle* h);
 
 /* Embed n crops.  Replaces FaceEmbedder.extract_embeddings_batch
- * (face_embedder.py:137-182) and extract_embedding (:112-135): BGR + LUT
- * normalise, IR forward, x/||x||, and with normalize!=0 the extra
- * e/(||e||+1e-8).  rgb: device [n][112][112][3] uint8; out: device [n][512]. */
+ * (face_embedder.py:137-182) and extract_embedding (:112-135): cv2.resize to 112x112
+ * (INTER_LINEAR, OpenCV fixed point) when height x width is not 112x112 (:94-96), BGR + LUT
+ * normalise, IR forward, x/||x||, and with normalize!=0 the extra e/(||e||+1e-8).
+ * rgb: device [n][height][width][3] uint8 (1 <= height, width <= 8192); out: device [n][512]. */
 int fr_embed(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize,
              void* stream);
 /* Same with host buffers (H2D, forward, D2H, synchronise). */
 int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width, float* out, int normalize);
+/* The resize step alone: dst[i] = cv2.resize(src[i], (112, 112), INTER_LINEAR) for n device crops
+ * of height x width (face_embedder.py:94-96).  src: device [n][height][width][3] uint8; dst: device
+ * [n][112][112][3] uint8. */
+int fr_resize_crops(fr_handle* h, const uint8_t* src, int n, int height, int width, uint8_t* dst, void* stream);
 
 /* Replace the gallery matrix (G rows of D=512 float32).  Replaces the per-query
  * `np.vstack` of GalleryManager.get_gallery_embeddings (gallery_manager.py:177-187):

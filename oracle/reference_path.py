@@ -18,12 +18,15 @@ INPUT_SIZE = (112, 112)
 def preprocess(face_image: np.ndarray) -> torch.Tensor:
     """``FaceEmbedder.preprocess`` adaface branch (face_embedder.py:93-104).
 
+    ``cv2.resize(face_image, (112, 112))`` (INTER_LINEAR) when the crop is not
+    112x112 (:94-96; cv2 is absent, so this is the fixed-point restatement
+    ``oracle.scrfd.resize_linear_u8`` -- parity vs cv2 itself unpinned), then
     RGB->BGR view, ``(x/255.0 - 0.5)/0.5`` in float64, CHW, ``.float()``,
-    batch dim.  Only 112x112 input (the ``cv2.resize`` branch at :94-96 is
-    not restated: cv2 is absent here).
+    batch dim.
     """
     if face_image.shape[:2] != INPUT_SIZE:
-        raise ValueError("oracle restates the 112x112 path only")
+        from oracle.scrfd import resize_linear_u8
+        face_image = resize_linear_u8(face_image, INPUT_SIZE[1], INPUT_SIZE[0])
     bgr = face_image[:, :, ::-1]
     bgr = (bgr / 255.0 - 0.5) / 0.5
     return torch.from_numpy(bgr.transpose(2, 0, 1)).float().unsqueeze(0)
@@ -80,11 +83,13 @@ def search(gallery: np.ndarray, ids: List[str], names: Dict[str, str], query: np
 
 
 def topk_policy(scores: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
-    """Deterministic top-k: descending score, ties by ascending index.
+    """Deterministic top-k: descending score, ties by DESCENDING index.
 
-    np.argsort(...)[::-1] has no defined tie order (introsort); the build fixes
-    this policy and parity inputs are designed with margins.
-    Works row-wise on a 2-D score matrix.
+    That is ``np.argsort(s)[::-1][:k]`` (gallery_manager.py:197) whenever numpy's
+    sort is stable (its insertion sort for <= 16 elements, or ``kind="stable"``):
+    a stable ascending sort, reversed.  numpy's AVX-512 argsort (numpy >= 2 on
+    such CPUs) leaves ties in no defined order, so the build fixes this policy;
+    parity inputs are designed with margins.  Row-wise on 2-D.
     """
     s = np.atleast_2d(scores)
     n, g = s.shape
@@ -93,7 +98,7 @@ def topk_policy(scores: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
     val = np.empty((n, k), dtype=np.float32)
     cols = np.arange(g)
     for r in range(n):
-        order = np.lexsort((cols, -s[r].astype(np.float64)))[:k]
+        order = np.lexsort((-cols, -s[r].astype(np.float64)))[:k]
         idx[r] = order
         val[r] = s[r, order]
     return idx, val

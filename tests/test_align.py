@@ -164,6 +164,16 @@ def test_processor_align_embed_match_stays_on_device():
     assert keys == sorted(keys, reverse=True)
     best = fp.process_numpy(frame)
     assert len(best) == 1 and np.array_equal(best[0]["aligned_face"], out[0]["aligned_face"])
+    # grayscale frame: the reference warps the 2-D frame and blur-scores the 2-D crop
+    gray = A.rgb_to_gray(frame)
+    g_out = fp.process_numpy(gray, return_all=True)
+    assert len(g_out) == 6
+    for r in g_out:
+        assert r["aligned_face"].ndim == 2
+        i = [j for j, lm in enumerate(lms) if np.array_equal(lm, r["landmarks"])][0]
+        want = A.warp_affine_linear(gray[:, :, None], A.fit_similarity(lms[i], t), 112)[:, :, 0]
+        assert np.array_equal(r["aligned_face"], want)
+        assert r["quality_metrics"]["blur_score"] == A.laplacian_var(want)
 
 
 @pytest.mark.gpu

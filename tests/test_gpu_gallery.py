@@ -142,3 +142,85 @@ def test_add_students_batch_matches_add_student(tmp_path):
     assert np.abs(Ea - Eb).max() <= 1e-7
     q = np.stack([e[0] for _s, _n, e in entries])
     assert [[r[0] for r in x] for x in a.search_batch(q, 3)] == [[r[0] for r in x] for x in b.search_batch(q, 3)]
+
+
+def test_concurrent_mutation_and_search_stay_consistent(tmp_path):
+    """searches racing enrollment changes on one GalleryManager (the reference's Flask
+    threads share one, face_recognition_server.py:1102).  Every result must be the host search of
+    SOME consistent gallery state: each returned (sid, score) pair equals q . template(sid) of
+    that student at some version, and the HBM copy ends equal to the host matrix."""
+    import threading
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    gm = GalleryManager(gallery_path=str(tmp_path / "c" / "s.npz"), device="cuda:0", verbose=False)
+    rng = np.random.default_rng(17)
+
+    def unit(n):
+        e = rng.normal(size=(n, 512)).astype(np.float32)
+        return e / np.linalg.norm(e, axis=1, keepdims=True)
+
+    base = unit(40)
+    for i in range(40):
+        gm.add_student(f"S{i}", f"N{i}", base[i])
+    history = {f"S{i}": [base[i]] for i in range(40)}  # every template each sid ever had
+    q = base[:8] + 0.05 * unit(8)
+    errors = []
+    stop = threading.Event()
+
+    def searcher():
+        try:
+            while not stop.is_set():
+                for r, row in zip(q, gm.search_batch(q, 3)):
+                    for sid, name, sc in row:
+                        best = min(abs(float(np.dot(r / np.linalg.norm(r), t)) - sc) for t in history[sid])
+                        if best > 1e-5:
+                            errors.append((sid, sc, best))
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=searcher) for _ in range(4)]
+    for t in threads:
+        t.start()
+    nxt = 40
+    for step in range(150):
+        ids = list(gm.students)
+        op = step % 3
+        if op == 0 and len(ids) > 10:
+            gm.delete_student(ids[int(rng.integers(len(ids)))])
+        elif op == 1:
+            e = unit(1)[0]
+            history.setdefault(f"S{nxt}", []).append(e)
+            gm.add_student(f"S{nxt}", "x", e)
+            nxt += 1
+        else:
+            sid = ids[int(rng.integers(len(ids)))]
+            e = unit(1)[0]
+            history[sid].append(e)
+            gm.add_student(sid, "y", e, overwrite=True)
+    stop.set()
+    for t in threads:
+        t.join(30)
+    assert not errors, errors[:5]
+    gm.search_batch(q, 3)
+    dev = gm._get_handle().gallery_read().cpu().numpy()
+    assert np.array_equal(dev, np.asarray(gm.get_gallery_embeddings()[0], np.float32))
+
+
+def test_batched_delete_compaction(tmp_path):
+    """A sync with many deletes rebuilds the rows in one device pass (apply_gallery_delta) and
+    ends equal to the host matrix."""
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    gm = GalleryManager(gallery_path=str(tmp_path / "d" / "s.npz"), device="cuda:0", verbose=False)
+    rng = np.random.default_rng(3)
+    E = rng.normal(size=(300, 512)).astype(np.float32)
+    for i in range(300):
+        gm.add_student(f"S{i}", "n", E[i])
+    gm.search_batch(E[:2], 1)
+    for i in range(0, 300, 3):
+        gm.delete_student(f"S{i}")
+    gm.add_student("S1", "m", E[0], overwrite=True)
+    gm.add_student("NEW", "m", E[5])
+    assert gm.pending_delta() is not None
+    res = gm.search_batch(E[:4], 1)
+    dev = gm._get_handle().gallery_read().cpu().numpy()
+    assert np.array_equal(dev, np.asarray(gm.get_gallery_embeddings()[0], np.float32))
+    assert res[0][0][0] == "S1" and res[2][0][0] == "S2"

@@ -140,7 +140,7 @@ def test_topk_matches_policy(G, k):
     from oracle.reference_path import topk_policy
     g = torch.Generator().manual_seed(G)
     s = torch.rand(9, G, generator=g)
-    s[0, :] = 0.5            # all ties: lowest indices first
+    s[0, :] = 0.5            # all ties: highest indices first
     s[1, 3] = s[1, 7] = 2.0  # a tie at the top
     idx, val = _frt.topk(s.to(DEV), k)
     ri, rv = topk_policy(s.numpy(), k)

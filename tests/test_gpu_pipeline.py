@@ -108,6 +108,53 @@ def test_embed_match_fused_equals_two_step(arch_embedder):
     assert (idx[:, 0].cpu().numpy() == np.arange(48)).all()  # probes are noisy copies of gallery rows
 
 
+def _check_topk_vs_reference(idx, sc, ref_idx, ref_sc, tie=1e-5):
+    """Top-1 ids identical, every rank's score within SCORE_TOL; ranks 2..k identical ids
+    except inside reference near-ties (adjacent scores closer than `tie`), where the id must
+    come from the same tie group (fp32 summation order may swap them)."""
+    assert np.array_equal(idx[:, 0], ref_idx[:, 0]), np.nonzero(idx[:, 0] != ref_idx[:, 0])
+    assert np.abs(sc - ref_sc).max() <= SCORE_TOL
+    n, k = ref_idx.shape
+    swaps = 0
+    for r in range(n):
+        for j in range(1, k):
+            if idx[r, j] == ref_idx[r, j]:
+                continue
+            group = [m for m in range(k) if abs(float(ref_sc[r, m]) - float(ref_sc[r, j])) < tie]
+            assert idx[r, j] in ref_idx[r, group] or abs(float(sc[r, j]) - float(ref_sc[r, k - 1])) < tie, (r, j)
+            swaps += 1
+    return swaps
+
+
+def test_c3_exact_config_vs_reference(golden_dir):
+    """BASELINE.json configs[2] exactly -- IR-101, B = 256 crops, 1,000-row gallery, top-5 --
+    through fr_embed_match, against the REFERENCE's own outputs on the same crops
+    (tests/golden/c3_ir_101.npz: reference FaceEmbedder + GalleryManager.add_student/search).
+    All 256 top-1 ids identical and |d score| <= 1e-4 at every rank, with the gallery embedded
+    on the GPU and with the reference's gallery matrix."""
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    g = np.load(os.path.join(golden_dir, "c3_ir_101.npz"))
+    gal = W.synthetic_crops(1000, int(g["gallery_seed"]))
+    probes = W.probe_crops(gal, 256, seed=int(g["probe_seed"]))
+    assert hashlib.sha256(gal.tobytes()).hexdigest() == str(g["gallery_crops_sha256"])
+    assert hashlib.sha256(probes.tobytes()).hexdigest() == str(g["probe_crops_sha256"])
+    emb = FaceEmbedder(architecture="ir_101", model_path="synthetic", max_batch=256)
+    dev = emb.device
+    ge = emb.embed_tensor(torch.from_numpy(gal).to(dev))
+    assert np.abs(ge.cpu().numpy() - g["gallery_emb"]).max() <= EMB_TOL
+    rgb = torch.from_numpy(probes).to(dev)
+    idx = torch.empty((256, 5), dtype=torch.int32, device=dev)
+    sc = torch.empty((256, 5), dtype=torch.float32, device=dev)
+    e_out = torch.empty((256, 512), dtype=torch.float32, device=dev)
+    for gallery in (ge, torch.from_numpy(g["gallery_emb"]).to(dev)):
+        emb.model.gallery_set(gallery)
+        emb.model.embed_match(rgb, 5, idx, sc, e_out)
+        torch.cuda.synchronize()
+        assert np.abs(e_out.cpu().numpy() - g["probe_emb"]).max() <= EMB_TOL
+        _check_topk_vs_reference(idx.cpu().numpy(), sc.cpu().numpy(), g["search_idx"], g["search_score"])
+    emb.model.gallery_set(torch.empty((0, 512), device=dev))
+
+
 def test_match_large_gallery_vs_numpy():
     """C5-sized gallery (100k rows) against numpy fp32 sgemv + the tie policy."""
     from oracle.reference_path import topk_policy
@@ -131,7 +178,7 @@ def test_match_large_gallery_vs_numpy():
 def test_backup_fixture_search_on_gpu(golden_dir):
     """The reference's committed galleries: GPU search == reference GalleryManager.search."""
     from facerecognitionpipeline_amd.gallery_manager import GalleryManager
-    for name in ("adaface_ir_101", "adaface_ir_50", "arcface_ir_101", "arcface_ir_50"):
+    for name in ("adaface_ir_101", "adaface_ir_50", "arcface_ir_101", "arcface_ir_50", "root_adaface_ir_50"):
         f = np.load(os.path.join(golden_dir, f"backup_{name}.npz"))
         gm = GalleryManager(gallery_path=f"/tmp/_fr_b/{name}/students.npz", device="cuda:0", verbose=False)
         for sid, e in zip(f["student_ids"], f["embeddings"]):
@@ -150,7 +197,9 @@ def test_edge_cases(arch_embedder, tmp_path):
     out = emb.extract_embeddings_batch([])
     assert isinstance(out, np.ndarray) and out.size == 0
     with pytest.raises(ValueError):
-        emb.extract_embedding(np.zeros((224, 224, 3), np.uint8))
+        emb.extract_embedding(np.zeros((112, 112), np.uint8))        # not HxWx3
+    with pytest.raises(ValueError):
+        emb.extract_embedding(np.full((112, 112, 3), 0.5))           # fractional pixels: not LUT-exact
     with pytest.raises(ValueError):
         FaceEmbedder(architecture="ir_7", model_path="synthetic")
     with pytest.raises(ValueError):
@@ -212,3 +261,41 @@ def test_torch_library_ops_match_python_api(arch_embedder):
     finally:
         torch_ops.unregister(hid)
         emb.model.gallery_set(torch.empty((0, 512), device=emb.device))
+
+
+@pytest.mark.parametrize("hw", [(224, 224), (150, 130), (96, 96), (113, 111), (1, 1), (480, 640), (112, 200)])
+def test_resize_crops_bit_exact(hw):
+    """cv2.resize(crop, (112, 112), INTER_LINEAR) on the device (face_embedder.py:94-96) equals the
+    fixed-point restatement oracle/scrfd.resize_linear_u8 byte for byte (parity vs cv2 unpinned)."""
+    from facerecognitionpipeline_amd import _lib
+    from oracle.scrfd import resize_linear_u8
+    h = _lib.Handle("ir_50", "adaface", torch.device("cuda", 0), max_batch=4)
+    r = np.random.default_rng(hw[0] * 1000 + hw[1])
+    crops = r.integers(0, 256, size=(3,) + hw + (3,), dtype=np.uint8)
+    out = torch.empty((3, 112, 112, 3), dtype=torch.uint8, device="cuda")
+    h.resize_crops(torch.from_numpy(crops).cuda(), out)
+    got = out.cpu().numpy()
+    for i in range(3):
+        assert np.array_equal(got[i], resize_linear_u8(crops[i], 112, 112)), (hw, i)
+
+
+def test_resize_branch_embeddings_vs_reference(golden_dir):
+    """Non-112 crops through the reference wrapper (tests/golden/resize_ir_50.npz: reference
+    FaceEmbedder with the restated cv2.resize) vs the device resize + forward: mixed sizes in one
+    extract_embeddings_batch, the single-crop API, and the C ABI host entry with 224x224 input."""
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    f = np.load(os.path.join(golden_dir, "resize_ir_50.npz"))
+    r = np.random.Generator(np.random.PCG64(int(f["crop_seed"])))
+    crops = [r.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for h, w in f["sizes"]]
+    emb = FaceEmbedder(architecture="ir_50", model_path="synthetic", max_batch=8)
+    got = emb.extract_embeddings_batch(crops)
+    assert np.abs(got - f["emb"]).max() <= EMB_TOL
+    assert np.abs(emb.extract_embedding(crops[6]) - f["emb"][6]).max() <= EMB_TOL
+    # fr_embed_host with 224x224 input (the enrollment crop size, enroll_students.py:67-81,222)
+    from facerecognitionpipeline_amd import _lib
+    big = np.ascontiguousarray(np.stack(crops[:6]))
+    out = np.empty((6, 512), np.float32)
+    _lib.check(_lib.load().fr_embed_host(emb.model.h, big.ctypes.data, 6, 224, 224, out.ctypes.data, 1), emb.model.h)
+    assert np.abs(out - f["emb"][:6]).max() <= EMB_TOL
+    # 224x224 float crops with integer values give the same result (face_embedder.py:100 computes on them)
+    assert np.array_equal(emb.extract_embeddings_batch([crops[0].astype(np.float64)]), got[:1])

@@ -10,19 +10,36 @@ the reference's own ``face_embedder.FaceEmbedder`` and
   ``extract_embedding`` (face_embedder.py:112-135) on seeded probe crops, and
   reference ``GalleryManager.search(top_k=5)`` (gallery_manager.py:189-205)
   for every probe against a gallery built with ``add_student``.
+* ``c3_ir_101.npz`` — the headline configuration exactly (BASELINE.json
+  configs[2]): reference IR-101 ``extract_embeddings_batch`` of the bench's
+  1,000 gallery crops and 256 probe crops, a 1,000-row gallery built with the
+  reference ``GalleryManager.add_student``, and reference ``search(top_k=5)``
+  of every probe (gallery_manager.py:189-205).
+* ``resize_ir_50.npz`` — reference ``extract_embeddings_batch`` on crops that
+  are not 112x112 (224x224 enrollment crops, enroll_students.py:67-81,222, and
+  odd sizes), i.e. through the ``cv2.resize`` branch of face_embedder.py:94-96.
+  cv2 is absent, so for this file the stub's ``resize`` is the restatement of
+  OpenCV's INTER_LINEAR in ``oracle/scrfd.py``: the fixture pins the
+  reference wrapper's order of operations around it, not cv2 itself.
 * ``backup_<name>.npz`` — the reference's committed gallery backups
-  (``gallery/backups/*.json``, export format gallery_manager.py:246-270) as
-  arrays, plus reference ``GalleryManager`` templates rebuilt by
-  ``add_student`` and reference ``search`` results for every stored sample.
+  (``gallery/backups/*.json`` and ``backups/*.json``, export format
+  gallery_manager.py:246-270) as arrays, plus reference ``GalleryManager``
+  templates rebuilt by ``add_student`` and reference ``search`` results for
+  every stored sample.  ``backups/adaface_ir_50_backup_20251202_081742.json``
+  becomes ``backup_root_adaface_ir_50.npz``.
 
 Two modules the reference imports are absent from this image and are supplied
 in a temporary directory that is put on ``sys.path`` for this run only:
 ``net`` (upstream AdaFace, restated in ``oracle/adaface_net.py``) and ``cv2``
-(only ``cv2.resize``/``INTER_LINEAR`` are referenced on the embed path, and
-never called for 112x112 input; the stub raises if it is).  Weights are the
-seeded synthetic checkpoint of ``facerecognitionpipeline_amd.weights`` saved
-in the reference's checkpoint format.  Crops are regenerated from their seeds
-at test time; their SHA-256 is stored to pin them.
+(only ``cv2.resize``/``INTER_LINEAR`` are referenced on the embed path; the
+stub raises unless the resize restatement is switched on for the resize
+fixture).  Weights are the seeded synthetic checkpoint of
+``facerecognitionpipeline_amd.weights`` saved in the reference's checkpoint
+format.  Crops are regenerated from their seeds at test time; their SHA-256 is
+stored to pin them.
+
+Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups]`` (no
+argument: all).
 """
 from __future__ import annotations
 
@@ -48,9 +65,21 @@ N_GALLERY = 8
 N_PROBE = 8
 TOP_K = 5
 
-CV2_STUB = '''INTER_LINEAR = 1
-def resize(*a, **k):
-    raise RuntimeError("cv2 stub: resize is not expected on the 112x112 golden path")
+C3_GALLERY = 1000   # BASELINE.json configs[2]: gallery=1k, batch=256, top-5
+C3_PROBES = 256
+RESIZE_SIZES = ((224, 224),) * 6 + ((150, 130), (96, 96))   # (H, W) of the resize-branch crops
+RESIZE_SEED = 0xFACE0224
+
+CV2_STUB = '''import sys
+INTER_LINEAR = 1
+RESTATED_RESIZE = False
+def resize(img, dsize, interpolation=INTER_LINEAR):
+    if not RESTATED_RESIZE:
+        raise RuntimeError("cv2 stub: resize is not expected on the 112x112 golden path")
+    sys.path.insert(0, {repo!r})
+    from oracle.scrfd import resize_linear_u8  # restatement of cv::resize INTER_LINEAR (uint8)
+    assert interpolation == INTER_LINEAR
+    return resize_linear_u8(img, int(dsize[0]), int(dsize[1]))
 '''
 NET_SHIM = '''import sys
 sys.path.insert(0, {repo!r})
@@ -69,10 +98,11 @@ def quiet():
 def main() -> None:
     if not os.path.isdir(REF):
         raise SystemExit("reference not present; golden files are generated in the build container only")
+    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups"}
     os.makedirs(OUT, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="frgolden_")
     with open(os.path.join(tmp, "cv2.py"), "w") as f:
-        f.write(CV2_STUB)
+        f.write(CV2_STUB.format(repo=REPO))
     with open(os.path.join(tmp, "net.py"), "w") as f:
         f.write(NET_SHIM.format(repo=REPO))
     sys.path.insert(0, tmp)
@@ -82,59 +112,112 @@ def main() -> None:
     import face_embedder as ref_fe  # reference module
     import gallery_manager as ref_gm  # reference module
 
-    base = W.synthetic_crops(N_GALLERY, W.CROP_SEED_GALLERY)
-    probes = W.probe_crops(base, N_PROBE)
-    for arch in ("ir_50", "ir_101"):
-        sd = W.synthetic_state_dict(arch)
+    def embedder(arch):
         ckpt = os.path.join(tmp, f"{arch}.ckpt")
-        W.save_checkpoint(sd, ckpt)
+        if not os.path.exists(ckpt):
+            W.save_checkpoint(W.synthetic_state_dict(arch), ckpt)
         with quiet():
-            emb = ref_fe.FaceEmbedder(architecture=arch, model_path=ckpt, model_type="adaface",
-                                      device=torch.device("cpu"))
-            g = emb.extract_embeddings_batch(list(base), normalize=True, batch_size=32)
-            p = np.stack([emb.extract_embedding(x, normalize=True) for x in probes])
-            gm = ref_gm.GalleryManager(gallery_path=os.path.join(tmp, f"g_{arch}", "students.pkl"))
-            for i in range(N_GALLERY):
-                gm.add_student(f"S{i:03d}", f"N{i}", g[i])
-            res = [gm.search(q, top_k=TOP_K) for q in p]
+            return ref_fe.FaceEmbedder(architecture=arch, model_path=ckpt, model_type="adaface",
+                                       device=torch.device("cpu"))
+
+    def search_arrays(gm, queries):
+        with quiet():
+            res = [gm.search(q, top_k=TOP_K) for q in queries]
             gal, ids = gm.get_gallery_embeddings()
-        ids_arr = np.array([[ids.index(sid) for sid, _n, _s in r] for r in res], dtype=np.int32)
-        sc_arr = np.array([[s for _sid, _n, s in r] for r in res], dtype=np.float32)
+        pos = {sid: i for i, sid in enumerate(ids)}
+        idx = np.array([[pos[sid] for sid, _n, _s in r] for r in res], dtype=np.int32)
+        sc = np.array([[s for _sid, _n, s in r] for r in res], dtype=np.float32)
+        return gal, idx, sc
+
+    if "embed" in parts:
+        base = W.synthetic_crops(N_GALLERY, W.CROP_SEED_GALLERY)
+        probes = W.probe_crops(base, N_PROBE)
+        for arch in ("ir_50", "ir_101"):
+            emb = embedder(arch)
+            with quiet():
+                g = emb.extract_embeddings_batch(list(base), normalize=True, batch_size=32)
+                p = np.stack([emb.extract_embedding(x, normalize=True) for x in probes])
+                gm = ref_gm.GalleryManager(gallery_path=os.path.join(tmp, f"g_{arch}", "students.pkl"))
+                for i in range(N_GALLERY):
+                    gm.add_student(f"S{i:03d}", f"N{i}", g[i])
+            gal, ids_arr, sc_arr = search_arrays(gm, p)
+            np.savez_compressed(
+                os.path.join(OUT, f"embed_{arch}.npz"),
+                weight_seed=np.int64(W.DEFAULT_WEIGHT_SEED), gallery_seed=np.int64(W.CROP_SEED_GALLERY),
+                probe_seed=np.int64(W.CROP_SEED_PROBE),
+                gallery_crops_sha256=np.array(sha(base)), probe_crops_sha256=np.array(sha(probes)),
+                gallery_emb=g.astype(np.float32), probe_emb=p.astype(np.float32),
+                gallery_matrix=gal.astype(np.float32),
+                search_idx=ids_arr, search_score=sc_arr)
+            print(arch, "gallery", g.shape, "probe", p.shape, "top1", ids_arr[:, 0].tolist())
+
+    if "c3" in parts:
+        # exactly the bench workload (bench.py: W.synthetic_crops(1000, CROP_SEED_GALLERY) and rank 0's
+        # W.probe_crops(gal, 256, seed=CROP_SEED_PROBE)); every probe through the reference embedder,
+        # every gallery row through add_student, every search through the reference search
+        gal_crops = W.synthetic_crops(C3_GALLERY, W.CROP_SEED_GALLERY)
+        probes = W.probe_crops(gal_crops, C3_PROBES, seed=W.CROP_SEED_PROBE)
+        emb = embedder("ir_101")
+        with quiet():
+            g = emb.extract_embeddings_batch(list(gal_crops), normalize=True, batch_size=32)
+            p = emb.extract_embeddings_batch(list(probes), normalize=True, batch_size=32)
+            gm = ref_gm.GalleryManager(gallery_path=os.path.join(tmp, "c3", "students.pkl"))
+            for i in range(C3_GALLERY):
+                gm.add_student(f"S{i:04d}", f"N{i}", g[i])
+        gal, ids_arr, sc_arr = search_arrays(gm, p)
+        # single-sample add_student keeps the row as is (gallery_manager.py:298-299): the reference
+        # gallery matrix IS the embedding matrix, stored once
+        assert np.array_equal(gal, g)
         np.savez_compressed(
-            os.path.join(OUT, f"embed_{arch}.npz"),
+            os.path.join(OUT, "c3_ir_101.npz"),
             weight_seed=np.int64(W.DEFAULT_WEIGHT_SEED), gallery_seed=np.int64(W.CROP_SEED_GALLERY),
             probe_seed=np.int64(W.CROP_SEED_PROBE),
-            gallery_crops_sha256=np.array(sha(base)), probe_crops_sha256=np.array(sha(probes)),
+            gallery_crops_sha256=np.array(sha(gal_crops)), probe_crops_sha256=np.array(sha(probes)),
             gallery_emb=g.astype(np.float32), probe_emb=p.astype(np.float32),
-            gallery_matrix=gal.astype(np.float32),
             search_idx=ids_arr, search_score=sc_arr)
-        print(arch, "gallery", g.shape, "probe", p.shape, "top1", ids_arr[:, 0].tolist())
+        print("c3", g.shape, p.shape, "top1 == i mod G:", float((ids_arr[:, 0] == np.arange(C3_PROBES) % C3_GALLERY).mean()))
 
-    for path in sorted(glob.glob(os.path.join(REF, "gallery", "backups", "*.json"))):
-        name = os.path.basename(path).split("_backup_")[0]
-        with open(path) as f:
-            data = json.load(f)
-        sids = list(data["students"].keys())
-        emb = np.array([data["students"][s]["embeddings"] for s in sids], dtype=np.float32)
-        tmpl = np.array([data["students"][s]["template_embedding"] for s in sids], dtype=np.float32)
-        avg = np.array([data["students"][s]["metadata"].get("avg_similarity", np.nan) for s in sids],
-                       dtype=np.float64)
+    if "resize" in parts:
+        import cv2  # the stub above
+        cv2.RESTATED_RESIZE = True
+        r = np.random.Generator(np.random.PCG64(RESIZE_SEED))
+        crops = [r.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for h, w in RESIZE_SIZES]
+        emb = embedder("ir_50")
         with quiet():
-            gm = ref_gm.GalleryManager(gallery_path=os.path.join(tmp, f"b_{name}", "students.pkl"),
-                                       aggregation_method="mean")
-            for s in sids:
-                gm.add_student(s, data["students"][s]["name"], np.array(data["students"][s]["embeddings"],
-                                                                         dtype=np.float32))
-            gal, ids = gm.get_gallery_embeddings()
-            q = emb.reshape(-1, emb.shape[-1])
-            res = [gm.search(x, top_k=TOP_K) for x in q]
+            e = emb.extract_embeddings_batch(crops, normalize=True, batch_size=32)
+        cv2.RESTATED_RESIZE = False
         np.savez_compressed(
-            os.path.join(OUT, f"backup_{name}.npz"),
-            student_ids=np.array(sids), embeddings=emb, stored_template=tmpl, avg_similarity=avg,
-            ref_template=gal.astype(np.float32),
-            search_idx=np.array([[ids.index(sid) for sid, _n, _s in r] for r in res], dtype=np.int32),
-            search_score=np.array([[s for _sid, _n, s in r] for r in res], dtype=np.float32))
-        print(name, emb.shape)
+            os.path.join(OUT, "resize_ir_50.npz"), weight_seed=np.int64(W.DEFAULT_WEIGHT_SEED),
+            crop_seed=np.int64(RESIZE_SEED), sizes=np.array(RESIZE_SIZES, dtype=np.int32),
+            crops_sha256=np.array(sha(np.concatenate([c.ravel() for c in crops]))), emb=e.astype(np.float32))
+        print("resize", e.shape)
+
+    if "backups" in parts:
+        paths = sorted(glob.glob(os.path.join(REF, "gallery", "backups", "*.json")))
+        paths += sorted(glob.glob(os.path.join(REF, "backups", "*.json")))
+        for path in paths:
+            name = os.path.basename(path).split("_backup_")[0]
+            if os.path.dirname(path) == os.path.join(REF, "backups"):
+                name = "root_" + name
+            with open(path) as f:
+                data = json.load(f)
+            sids = list(data["students"].keys())
+            emb = np.array([data["students"][s]["embeddings"] for s in sids], dtype=np.float32)
+            tmpl = np.array([data["students"][s]["template_embedding"] for s in sids], dtype=np.float32)
+            avg = np.array([data["students"][s]["metadata"].get("avg_similarity", np.nan) for s in sids],
+                           dtype=np.float64)
+            with quiet():
+                gm = ref_gm.GalleryManager(gallery_path=os.path.join(tmp, f"b_{name}", "students.pkl"),
+                                           aggregation_method="mean")
+                for s in sids:
+                    gm.add_student(s, data["students"][s]["name"], np.array(data["students"][s]["embeddings"],
+                                                                             dtype=np.float32))
+            gal, idx, sc = search_arrays(gm, emb.reshape(-1, emb.shape[-1]))
+            np.savez_compressed(
+                os.path.join(OUT, f"backup_{name}.npz"),
+                student_ids=np.array(sids), embeddings=emb, stored_template=tmpl, avg_similarity=avg,
+                ref_template=gal.astype(np.float32), search_idx=idx, search_score=sc)
+            print(name, emb.shape)
 
 
 if __name__ == "__main__":
