@@ -1,99 +1,79 @@
-// Winograd F(4x4, 3x3) convolution in f32 on gfx950 MFMA (v_mfma_f32_32x32x2_f32).
+// Winograd F(4x4, 3x3) convolution in f32 on gfx950, in two passes:
+//
+//   1. wino4g_itrans_kernel: every 6x6 input patch of the layer is transformed ONCE,
+//      V = B^T d B (with the pre-activation BatchNorm applied to the in-image pixels first),
+//      and written to a V buffer laid out in MFMA A-fragment order.
+//   2. wino4g_gemm_kernel: per transform element xi (36) the layer is the GEMM
+//      M_xi[tile][cout] = sum_cin V_xi[tile][cin] U_xi[cin][cout] on v_mfma_f32_32x32x2_f32,
+//      with the output transform A^T M A and BN (+PReLU | +residual) fused in the epilogue.
 //
 // Replaces the stride-1 3x3 Conv2d of net.BasicBlockIR (res_layer[1] and the stride-1
-// res_layer[4]; reached through `self.model(batch)`, face_embedder.py:157) with the same
-// fused pre-BN / post-BN / PReLU / residual epilogues as the direct and F(2x2) kernels.
-// The arithmetic stays f32 throughout.  Per 4x4 output tile and (cin, cout) pair the
-// algorithm does 36 products instead of 144 (F(2x2): 64), so the MFMA work drops 4x:
+// res_layer[4], reached through `self.model(batch)`, face_embedder.py:157) and the
+// detector's stride-1 3x3 convs.  The one-pass kernel before it (round 1) transformed each
+// input patch again for every 32-output-channel block (8x at 256 channels) on VALU that
+// competes with the f32 MFMA pipe for the SIMD; here the transform costs one streaming pass
+// over the activations and the GEMM kernel is MFMA + loads only.
 //
-//   Y = A^T [ (G g G^T) (.) (B^T d B) ] A     d: 6x6 input patch, g: 3x3 filter
+// Transforms (Lavin & Gray 2016, points 0, +-1, +-2, inf):
 //   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
 //   G   = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1]
 //   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
-// (Lavin & Gray 2016, points 0, +-1, +-2, inf).  Simulated on the IR-101 oracle in f32 the
-// embeddings stay within 5e-7 of direct convolution.
+// Filters U = G g G^T are built once per model in double (launch_wino4_weights, no pre-BN
+// folding: the pre-BN is applied to the input in pass 1).
 //
-// Tiles live on a "canvas": images laid out NC per canvas row with a period of P rows /
-// columns.  P = H when 4 | H (every tile inside one image); otherwise P = H + 1 -- one zero
-// separator row/column between neighbouring images is all a 3x3 pad-1 conv needs, so a 4x4
-// tile may straddle two images and 14x14 images waste 15²/14² instead of 16²/14² of the
-// products.  Patch pixels on a separator or outside the canvas load as 0.
+// Tiles are cut from a "canvas" of the batch (wino4_canvas): images laid out NC per canvas
+// row with a period of P rows / columns.  P = H when 4 | H (every tile inside one image);
+// otherwise P = H + 1 -- one zero separator row/column between neighbouring images is all a
+// 3x3 pad-1 conv needs, so a 4x4 tile may straddle two images and 14x14 images cost 15^2/14^2
+// of the products instead of 16^2/14^2.  Patch pixels on a separator or outside the canvas
+// load as 0.
 //
-// Per transform element xi = 6a + b (36 of them) the layer is one GEMM
-//   M_xi[tile][cout] = sum_cin V_xi[tile][cin] * U_xi[cin][cout]
-// and one workgroup owns WT = 32 tiles x 32 couts for all 36.  Its 8 waves are specialised,
-// one of each kind per SIMD:
-//   * 4 MFMA waves: wave c owns xi = 9c .. 9c+8, i.e. 9 32x32 accumulator blocks
-//     (v_mfma_f32_32x32x2_f32, 144 registers), 72 MFMAs per K-step, and nothing else to do
-//     but read its A fragments from LDS and its B fragments (U, one K-step ahead) from L2.
-//   * 4 transform waves: thread (tile, channel pair) loads its 6x6 patch as 36 8-byte buffer
-//     loads (OOB offset -> 0 = zero padding) two K-steps ahead, transforms it with packed
-//     f32 math and writes 36 float2 of V to LDS V[xi][tile][16 ch] (rows XOR-swizzled by
-//     16-B slot: conflict-free ds_read_b128 fragment reads and ds_write_b64 stores).  Its
-//     VALU issues in the gaps of the MFMA wave on the same SIMD.
-//   * K-step = 16 input channels; V is double-buffered, one barrier per K-step.
-//   * U (transformed filters, built once per model by wino4_weight_kernel) never touches
-//     LDS: it is stored in MFMA-fragment order (1 KiB coalesced loads).
-//   * The pre-activation BatchNorm of conv1 is folded out of the K loop: its scale into the
-//     filters (U = G (g*sc) G^T), its shift into a per-(border class, cout) constant added
-//     in the epilogue (wino4_corr_kernel), so the transform is pure adds and fmas.
-//   * Epilogue: accumulators go through LDS as M[xi][tile][cout], every thread
-//     inverse-transforms 2 (tile, cout) pairs and applies BN (+PReLU | + residual) at the
-//     in-image pixels of each tile (residuals prefetched before the staging barrier).
+// Layouts (floats):
+//   V  [mblocks][KST][36 xi][2 q][64 lane][4]   one (tile block, K-step) chunk = 73,728 B;
+//      lane = 32 h + m holds channels 8h + 4q .. +3 of tile m of the block (the
+//      32x32x2 A-operand fragment: lane (m, h) supplies A[m][k = h])
+//   U  [36 xi][Cout/32][KST][2 q][64 lane][4]   lane = 32 h + n: channels 8h + 4q .. of cout n
+// with KST = Cin / 16 K-steps of 16 channels; MFMA j (0..7) of a K-step multiplies channel
+// 8h + j.
 //
-// Lane map of 32x32x2 MFMA: A operand lane (m = l%32, h = l/32) = A[m][k=h], B operand lane
-// (n = l%32, h) = B[k=h][n], C/D register r = D[8(r/4) + 4h + r%4][n].  MFMA j (0..7) of a
-// K-step multiplies channel 8h + j: lane (m, h) reads V[xi][m][8h .. 8h+7] with two
-// ds_read_b128 and the matching 8 U values with two 16-B loads.
+// GEMM workgroup: 32 tiles x 64 couts x all 36 xi, 12 waves (768 threads, 3 per SIMD):
+// wave w owns transform row a = w % 6 (xi = 6a .. 6a+5) for cout half w / 6, i.e. six
+// 32x32 accumulator blocks (96 registers).  The K loop is branch-free streaming: each wave
+// loads its A fragments (V) and B fragments (U) straight from L2 / the Infinity Cache in
+// fragment order (1 KiB coalesced loads; the other cout half's wave of the same row reads
+// the same V lines), three (K-step, xi) slots ahead in a register ring, no LDS, no barrier.
+// Owning whole rows lets the epilogue apply the b-direction of A^T M A in registers
+// (6 -> 4 per row) before the LDS exchange; the a-direction runs after it, per
+// (tile, column, cout), followed by BN / PReLU / residual and the stores.
 #include <algorithm>
-#include <cstdlib>
 
 #include "frhip_kernels.h"
-
-
-
-#ifdef W4_MFMA_ONLY  // ablation (tools/w4_variants.sh): K loop of MFMAs + fragment reads only
-#define W4_NO_PATCH
-#define W4_NO_TRANSFORM
-#define W4_NO_ULOAD
-#define W4_NO_BARRIER
-#endif
 
 namespace frhip {
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int NXI = 36;              // transform elements
-constexpr int WT = 32;               // 4x4 output tiles per workgroup (MFMA M)
-constexpr int KC = 16;               // input channels per K-step
-constexpr int XPW = 9;               // transform elements per wave
-constexpr int VPLANE = WT * KC;      // one xi plane of V: 512 floats
-constexpr int VBUF = NXI * VPLANE;   // one K-step of V: 18432 floats (72 KiB)
-constexpr int BF_PLANE = WT * 8;     // BF: one xi plane of V hi (or lo): 32 tiles x 16 bf16 = 256 words
-constexpr int BF_LO = NXI * BF_PLANE;  // BF: words from a hi plane to its lo plane
-static_assert(2 * BF_LO <= VBUF, "BF V buffer must fit the f32 one");
-constexpr int MROW = 33;             // epilogue staging row (32 couts + 1: conflict-free stores)
-constexpr int MPLANE = WT * MROW;    // epilogue: one xi plane of M[tile][cout]
-constexpr int LDS_FLOATS = (2 * VBUF > NXI * MPLANE) ? 2 * VBUF : NXI * MPLANE;
-constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum with it is past the range
-static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+constexpr int NXI = 36;                  // transform elements
+constexpr int WT = 32;                   // 4x4 output tiles per tile block (MFMA M)
+constexpr int KC = 16;                   // input channels per K-step
+constexpr int CHUNK = NXI * WT * KC;     // floats of one V chunk (18,432)
+constexpr int GEMM_THREADS = 768;        // 12 waves: 6 transform rows x 2 cout halves
+constexpr int RING = 3;                  // (K-step, xi) slots of operands in flight per wave
+constexpr int MROW = 33;                 // epilogue staging row (32 couts + 1)
+constexpr int EPI_FLOATS = 24 * WT * MROW;  // [6 a][4 b'][32 tiles][33]
+constexpr int BIGOFF = 0x7F000000;       // row/column offset of padding: any sum with it is past the range
+static_assert(EPI_FLOATS * 4 <= 160 * 1024, "LDS budget");
 
-// XOR of the 16-B slot of a V row, by tile: every ds_read_b128 lane group of the 32x32x2 A
-// fragment (tiles m, slot 2h + r) then hits 16 distinct slots
-__device__ __forceinline__ int vswz(int tile) { return (tile >> 2) & 3; }
-
-__device__ __forceinline__ int wino4_xcd_remap(int bid, int n) {
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
   const int xcd = bid & 7, loc = bid >> 3;
   const int q = n >> 3, r = n & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc4(const void* ptr, int bytes) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* ptr, int bytes) {
   const unsigned long long a = reinterpret_cast<unsigned long long>(ptr);
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
@@ -102,22 +82,27 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc4(const void* ptr,
                                            0x00020000);
 }
 
+// 16-byte buffer load: per-lane byte offset `off` + wave-uniform byte offset `soff` (an SGPR)
+__device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, int off, int soff = 0) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0);
+  return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+}
+
 // Canvas coordinate v (a row or a column) of a tile whose origin lies in image slot `base`:
 // returns the in-image coordinate and sets `slot` (base or base + 1), or -1 for padding.
 __device__ __forceinline__ int canvas_coord(int v, int base, int P, int H, bool sep, int& slot) {
-  const int y = v - base * P, y1 = y - P;  // branch-free: selects only
+  const int y = v - base * P, y1 = y - P;
   const bool in0 = (unsigned)y < (unsigned)H;
   const bool in1 = sep && (unsigned)y1 < (unsigned)H;
   slot = base + (in1 ? 1 : 0);
   return in0 ? y : (in1 ? y1 : -1);
 }
 
-// 1-D input transform B^T d (6 -> 6), two channels at once (packed f32)
-__device__ __forceinline__ void bt6(const f2 (&d)[6], f2 (&t)[6]) {
-  const f2 s1 = d[3] + d[4], s2 = d[1] + d[2];
-  const f2 s3 = d[4] - d[3], s4 = d[1] - d[2];
-  const f2 s5 = d[4] - d[2], s6 = d[3] - d[1];
-  // 14 ops (8 adds, 6 fmas); the nesting keeps t0/t5 at two fmas each
+// 1-D input transform B^T d (6 -> 6) of four channels
+__device__ __forceinline__ void bt6(const f4 (&d)[6], f4 (&t)[6]) {
+  const f4 s1 = d[3] + d[4], s2 = d[1] + d[2];
+  const f4 s3 = d[4] - d[3], s4 = d[1] - d[2];
+  const f4 s5 = d[4] - d[2], s6 = d[3] - d[1];
   t[0] = 4.f * d[0] + (-5.f * d[2] + d[4]);
   t[1] = -4.f * s2 + s1;
   t[2] = 4.f * s4 + s3;
@@ -136,328 +121,210 @@ __device__ __forceinline__ void at6(const float (&m)[6], float (&o)[4]) {
   o[3] = m12 + 8.f * m34 + m[5];
 }
 
-// BF (opt-in FR_PRECISION_BF16X3): V and U are split into bf16 hi + lo (x = hi + lo to ~2^-16),
-// the MFMA waves run v_mfma_f32_32x32x16_bf16 on lo*hi + hi*lo + hi*hi with f32 accumulation
-// (the lo*lo term, ~2^-16 relative, is dropped): 3 MFMAs of 32 cycles per transform element
-// and K-step instead of 8 of 64.  V in LDS: per xi plane hi [32 tiles][16 ch] bf16 then the lo
-// planes; 32-B rows, 16-B slot XOR (m >> 3) & 1.
-template <bool CORR, int EPI, bool BF, bool SPLIT>
-__global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
-  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+// ---- pass 1: input transform ------------------------------------------------------------
+// Block (tile block mb, 32-channel group g): 4 waves x (8 tiles x 8 channel quads).  Each
+// thread loads its 6x6 patch as 36 16-byte loads (a wave covers 8 pixels x 128 B = whole
+// lines), applies the pre-BN at in-image pixels, transforms and stores 36 float4 of V (per
+// (K-step, h, q) group a wave writes 8 tiles x 16 B = one 128-B segment).
+template <bool PRE>
+__global__ __launch_bounds__(256) void wino4g_itrans_kernel(Wino4Params p) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c4 = lane & 7, m = 8 * wv + (lane >> 3);
+  const int mb = blockIdx.x, g = blockIdx.y;
+  const int H = p.H, W = p.W, Cin = p.Cin, KST = Cin / KC;
+  const int T = mb * WT + m;
+  const int tr = T / p.TWc, tc = T - tr * p.TWc;
+  const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
+  const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
+  const int c0 = 32 * g + 4 * c4;
+  int roff[6], coff[6];
+  bool rin[6], cin[6];
+  int rslot[6], cslot[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int y = canvas_coord(4 * tr - 1 + i, ir0, p.Pr, H, sep_r, rslot[i]);
+    const int x = canvas_coord(4 * tc - 1 + i, ic0, p.Pc, W, sep_c, cslot[i]);
+    rin[i] = y >= 0 && T < p.ntiles;
+    cin[i] = x >= 0 && cslot[i] < p.NC;
+    roff[i] = rin[i] ? (rslot[i] * p.NC * H + y) * W * Cin * 4 : BIGOFF;
+    coff[i] = cin[i] ? ((cslot[i] * H * W + x) * Cin + c0) * 4 : BIGOFF;
+  }
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
+  f4 d[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) d[i][j] = ld4(xr, (int)((unsigned)roff[i] + (unsigned)coff[j]));
+  if constexpr (PRE) {
+    // BN(x) = x * scale + shift at in-image pixels only: the conv's zero padding (and the
+    // canvas separators / the images past B) stay 0, as in BN -> zero-padded Conv2d
+    const f4 sc = *reinterpret_cast<const f4*>(p.pre_scale + c0);
+    const f4 sh = *reinterpret_cast<const f4*>(p.pre_shift + c0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const bool in = rin[i] && cin[j] && (rslot[i] * p.NC + cslot[j]) < p.B;
+        const f4 v = d[i][j] * sc + sh;
+        d[i][j] = in ? v : f4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {  // columns: d[.][j] <- (B^T d)[.][j]
+    f4 c[6], o[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) c[i] = d[i][j];
+    bt6(c, o);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) d[i][j] = o[i];
+  }
+  const int s = 2 * g + (c4 >> 2), h = (c4 & 3) >> 1, q = c4 & 1;
+  float* vbase = p.v + ((size_t)mb * KST + s) * CHUNK + q * 256 + (32 * h + m) * 4;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    f4 v[6];
+    bt6(d[a], v);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) *reinterpret_cast<f4*>(vbase + (6 * a + b) * 512) = v[b];
+  }
+}
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  // SPLIT (small grids): workgroup (t, split) runs K-steps [s0, s0 + KS) of item t and writes
-  // its raw partial output to slab `split`; wino4_split_reduce_kernel finishes the layer
-  const int nT = p.mblocks * p.nblocks;
-  const int tt = wino4_xcd_remap(blockIdx.x, SPLIT ? nT * p.ksplit : nT);
+// ---- pass 2: transform-domain GEMM + output transform ----------------------------------
+// SPLIT (small grids): workgroup (item, split) runs K-steps [s0, s0 + KS) and writes its raw
+// inverse-transformed partial output to slab `split`; wino4g_split_reduce_kernel finishes.
+template <int EPI, bool SPLIT>
+__global__ __launch_bounds__(GEMM_THREADS, 1) void wino4g_gemm_kernel(Wino4Params p) {
+  __shared__ __attribute__((aligned(16))) float lds[EPI_FLOATS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: operand offsets stay scalar
+  const int ra = wid % 6, ch = wid / 6;  // transform row, cout half
+  const int NB = p.nblocks;              // 64-cout blocks
+  const int nT = p.mblocks * NB;
+  const int tt = xcd_remap(blockIdx.x, SPLIT ? nT * p.ksplit : nT);
   const int split = SPLIT ? tt / nT : 0;
   const int t = SPLIT ? tt - split * nT : tt;
-  // item t -> (tile block mb, cout block nb): consecutive items (one XCD's contiguous run)
-  // cycle through p.nbg cout blocks of a tile block before moving on, so those workgroups
-  // share the tile block's input in the XCD's L2 (nbg = 1: one cout block per run)
-  const int gsz = p.mblocks * p.nbg, g = t / gsz, rem = t - g * gsz;
-  const int mb = rem / p.nbg, nb = g * p.nbg + (rem - (rem / p.nbg) * p.nbg);
-  const int H = p.H, W = p.W, Cin = p.Cin;
-  const int KST = Cin / KC;  // K-steps of the whole reduction (filter layout stride)
+  // item t -> (tile block mb, cout block nb): one XCD's contiguous run of items covers GM tile
+  // blocks x all NB cout blocks, so the V chunks and U blocks it streams are shared in its L2
+  const int GM = p.nbg;
+  const int grp = t / (GM * NB), rem = t - grp * GM * NB;
+  const int gm = min(GM, p.mblocks - grp * GM);
+  const int nb = rem / gm, mb = grp * GM + (rem - (rem / gm) * gm);
+  const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout;
+  const int KST = Cin / KC;
   const int s0 = SPLIT ? split * p.ks_per : 0;
-  const int KS = SPLIT ? min(p.ks_per, KST - s0) : KST;  // K-steps this workgroup runs
-  const int NB32 = p.Cout / 32;
+  const int KS = SPLIT ? min(p.ks_per, KST - s0) : KST;
+  const int cout0 = nb * 64 + ch * 32;
+  const bool active = cout0 < Cout;  // Cout % 64 == 32: the last block's second half idles
+
+  floatx16 acc[6];
+#pragma unroll
+  for (int b = 0; b < 6; ++b)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+
+  if (active) {
+    const __amdgpu_buffer_rsrc_t vr = uniform_rsrc(p.v + (size_t)mb * KST * CHUNK, KST * CHUNK * 4);
+    const __amdgpu_buffer_rsrc_t ur = uniform_rsrc(p.u, NXI * Cout * Cin * 4);
+    const int NB32 = Cout / 32, nb32 = cout0 / 32;
+    // slot (K-step s, b) = (s, xi = 6 ra + b): the fragment of lane l sits at 16 l bytes (q = 0)
+    // and 1 KiB + 16 l (q = 1) of a wave-uniform 2-KiB block
+    const int lo = lane * 16;
+    f4 va[RING][2], ub[RING][2];
+    auto load = [&](int slot, int rs) {  // slot counts (K-step, b) pairs from s0; clamped at the end
+      const int s = s0 + min(slot / 6, KS - 1), b = slot % 6;
+      const int vo = (s * NXI + 6 * ra + b) * 2048;
+      const int uo = (((6 * ra + b) * NB32 + nb32) * KST + s) * 2048;
+      va[rs][0] = ld4(vr, lo, vo);
+      va[rs][1] = ld4(vr, lo, vo + 1024);
+      ub[rs][0] = ld4(ur, lo, uo);
+      ub[rs][1] = ld4(ur, lo, uo + 1024);
+    };
+#pragma unroll
+    for (int r = 0; r < RING; ++r) load(r, r);
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const int rs = b % RING;  // 6 slots per K-step, RING | 6: the ring phase is static
+        const f4 a0 = va[rs][0], a1 = va[rs][1], b0 = ub[rs][0], b1 = ub[rs][1];
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b0.x, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b0.y, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b0.z, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, b0.w, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, b1.x, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, b1.y, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, b1.z, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, b1.w, acc[b], 0, 0, 0);
+        load(6 * s + b + RING, rs);
+        // keep slot order: without this the scheduler clusters three slots' MFMAs and issues
+        // their refills together right before they are consumed (vmcnt(0) every half step)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // ---- epilogue -------------------------------------------------------------------------
+  // b-direction of A^T M A in registers: lane (n, h) register r holds (tile 8(r/4) + 4h + r%4,
+  // cout n) of all six b of row ra; z[b'] = (A^T m)[b'].  Staged per cout half as
+  // lds[a][b'][tile][cout] (row 33: conflict-free), then each thread finishes (tile, b', cout)
+  // columns along a and writes 4 output pixels.
+  const int ntile_cols = WT * 4 * 32;  // (tile, b', cout) columns of one cout half
+  const __amdgpu_buffer_rsrc_t yr =
+      uniform_rsrc(SPLIT ? p.part + split * p.part_stride : p.y, p.B * H * W * Cout * 4);
+  constexpr bool RES = !SPLIT && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
+  const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, RES ? p.B * H * W * Cout * 4 : 0);
   const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
-  const bool mfma_wave = wid < 4;  // waves 0-3 MFMA, 4-7 transform (one of each per SIMD)
-
-  floatx16 acc[XPW];
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass) __syncthreads();  // the previous half's columns are read
+    if (ch == pass && active) {
+      const int n = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int x = 0; x < XPW; ++x)
+      for (int r = 0; r < 16; ++r) {
+        const float m6[6] = {acc[0][r], acc[1][r], acc[2][r], acc[3][r], acc[4][r], acc[5][r]};
+        float z[4];
+        at6(m6, z);
+        const int tile = 8 * (r >> 2) + 4 * h + (r & 3);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[x][e] = 0.f;
-
-  if (!mfma_wave) {
-    // ---- transform waves: thread (tile tl, channel pair cp) -----------------------------
-#ifdef W4_TPRIO
-    __builtin_amdgcn_s_setprio(W4_TPRIO);
-#endif
-    // byte offset of patch pixel (i, j) = roff[i] + coff[j]; an out-of-image row or column
-    // carries BIGOFF, which puts the sum past the buffer range (load returns 0)
-    const int pt = tid - 256;
-    const int tl = pt >> 3, cp = pt & 7;
-    int roff[6], coff[6];
-    {
-      const int T = mb * WT + tl;
+        for (int bq = 0; bq < 4; ++bq) lds[((ra * 4 + bq) * WT + tile) * MROW + n] = z[bq];
+      }
+    }
+    __syncthreads();
+    if (nb * 64 + pass * 32 >= Cout) continue;  // uniform: this half has no couts
+    const int cout = nb * 64 + pass * 32 + (tid & 31);
+    const float sc = SPLIT ? 1.f : p.post_scale[cout], sh = SPLIT ? 0.f : p.post_shift[cout];
+    float al = 0.f;
+    if constexpr (!SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU)) al = p.prelu[cout];
+    for (int col = tid; col < ntile_cols; col += GEMM_THREADS) {
+      const int tb = col >> 5;  // (tile, b') pair
+      const int tile = tb >> 2, bq = tb & 3;
+      float m6[6];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) m6[a] = lds[((a * 4 + bq) * WT + tile) * MROW + (col & 31)];
+      float o[4];
+      at6(m6, o);
+      const int T = mb * WT + tile;
       const int tr = T / p.TWc, tc = T - tr * p.TWc;
       const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        int slot;
-        const int y = canvas_coord(4 * tr - 1 + i, ir0, p.Pr, H, sep_r, slot);
-        roff[i] = (y >= 0 && T < p.ntiles) ? (slot * p.NC * H + y) * W * Cin * 4 : BIGOFF;
-        const int x = canvas_coord(4 * tc - 1 + i, ic0, p.Pc, W, sep_c, slot);
-        coff[i] = (x >= 0 && slot < p.NC) ? ((slot * H * W + x) * Cin + 2 * cp) * 4 : BIGOFF;
-      }
-    }
-    const __amdgpu_buffer_rsrc_t xr = uniform_rsrc4(p.x, p.B * H * W * Cin * 4);
-    auto f2u = [](u32x2 v) { return f2{__uint_as_float(v.x), __uint_as_float(v.y)}; };
-    f2 dA[6][6], dB[6][6];
-    auto load_patch = [&](f2 (&d)[6][6], int s) {
-#ifdef W4_NO_PATCH
-      if (s > 1) return;
-#endif
-      const int so = (s0 + min(s, KS - 1)) * KC * 4;
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-          d[i][j] = f2u(__builtin_amdgcn_raw_buffer_load_b64(xr, (int)((unsigned)roff[i] + (unsigned)coff[j]), so, 0));
-    };
-    // physical float offset of this thread's channel pair inside its V row (16-B slot XOR)
-    float* const vdst = lds + tl * KC + ((((cp >> 1) ^ vswz(tl)) << 2) | ((cp & 1) << 1));
-    // BF: the pair as one word of 2 bf16 in the hi plane (lo plane BF_LO words later)
-    unsigned* const vdst_bf = reinterpret_cast<unsigned*>(lds) + tl * 8 + ((((cp >> 2) ^ ((tl >> 3) & 1)) << 2) | (cp & 3));
-    auto put_v = [&](int buf, int xi, f2 v) {
-      if constexpr (BF) {
-        const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y;
-        const __bf16 l0 = (__bf16)(v.x - (float)h0), l1 = (__bf16)(v.y - (float)h1);
-        unsigned* d0 = vdst_bf + buf * VBUF + xi * BF_PLANE;
-        d0[0] = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
-        d0[BF_LO] = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
-      } else {
-        *reinterpret_cast<f2*>(vdst + buf * VBUF + xi * VPLANE) = v;
-      }
-    };
-    auto store_v = [&](f2 (&d)[6][6], int buf) {
-#ifdef W4_NO_TRANSFORM
-#pragma unroll
-      for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int b = 0; b < 6; ++b) put_v(buf, 6 * a + b, d[a][b]);
-      return;
-#endif
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {  // columns: d[.][j] <- (B^T d)[.][j], in place
-        f2 c[6], o[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) c[i] = d[i][j];
-        bt6(c, o);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) d[i][j] = o[i];
-      }
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        f2 v[6];
-        bt6(d[a], v);
-#pragma unroll
-        for (int b = 0; b < 6; ++b) put_v(buf, 6 * a + b, v[b]);
-      }
-    };
-    // prologue: V(0) into buffer 0, patch 1 in flight; step s: issue patch s+2, transform
-    // patch s+1 (loaded a whole step ago) into buffer (s+1)&1, barrier
-    load_patch(dA, 0);
-    load_patch(dB, 1);
-    store_v(dA, 0);
-    __syncthreads();
-    for (int s = 0; s < KS; s += 2) {  // KS even or not: the tail step's extra work is harmless
-      load_patch(dA, s + 2);
-      store_v(dB, 1);
-#ifndef W4_NO_BARRIER
-      __syncthreads();
-#endif
-      if (s + 1 >= KS) break;
-      load_patch(dB, s + 3);
-      store_v(dA, 0);
-#ifndef W4_NO_BARRIER
-      __syncthreads();
-#endif
-    }
-  } else {
-    // ---- MFMA waves: wave wid owns xi = 9*wid + x ---------------------------------------
-#ifdef W4_PRIO
-    __builtin_amdgcn_s_setprio(W4_PRIO);  // MFMA waves win issue arbitration on their SIMD
-#endif
-    const __amdgpu_buffer_rsrc_t ur = uniform_rsrc4(p.u, NXI * p.Cout * Cin * 4);
-    auto f4u = [](u32x4 v) {
-      return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-    };
-    int ubase[XPW];
-#pragma unroll
-    for (int x = 0; x < XPW; ++x) ubase[x] = ((((XPW * wid + x) * NB32 + nb) * KST) * 2 * 64 + lane) * 16;
-    float4 u[XPW][2];
-    auto load_u = [&](int x, int s) {
-#ifdef W4_NO_ULOAD
-      if (s > 0) return;
-#endif
-      const int so = (s0 + min(s, KS - 1)) * 2 * 64 * 16;
-      u[x][0] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x], so, 0));
-      u[x][1] = f4u(__builtin_amdgcn_raw_buffer_load_b128(ur, ubase[x] + 64 * 16, so, 0));
-    };
-    const int m = lane & 31, h = lane >> 5;
-    const int rq = vswz(m);
-    // f32: the two 16-B slots of channels 8h..8h+7; BF: the hi and the lo slot of those channels
-    const float* vrd0 = BF ? lds + (XPW * wid) * BF_PLANE + m * 8 + ((h ^ ((m >> 3) & 1)) << 2)
-                           : lds + (XPW * wid) * VPLANE + m * KC + (((2 * h) ^ rq) << 2);
-    const float* vrd1 = BF ? vrd0 + BF_LO : lds + (XPW * wid) * VPLANE + m * KC + (((2 * h + 1) ^ rq) << 2);
-    constexpr int XPL = BF ? BF_PLANE : VPLANE;  // floats between consecutive xi planes
-#pragma unroll
-    for (int x = 0; x < XPW; ++x) load_u(x, 0);
-    __syncthreads();
-    for (int s = 0; s < KS; ++s) {
-#ifdef W4_MFMA_IDLE  // ablation: MFMA waves only keep the barrier cadence
-      __syncthreads();
-      continue;
-#endif
-      const int vb = (s & 1) * VBUF;
-      float4 fa[2][2];
-      fa[0][0] = *reinterpret_cast<const float4*>(vrd0 + vb);
-      fa[0][1] = *reinterpret_cast<const float4*>(vrd1 + vb);
-#pragma unroll
-      for (int x = 0; x < XPW; ++x) {
-        if (x + 1 < XPW) {
-          fa[(x + 1) & 1][0] = *reinterpret_cast<const float4*>(vrd0 + vb + (x + 1) * XPL);
-          fa[(x + 1) & 1][1] = *reinterpret_cast<const float4*>(vrd1 + vb + (x + 1) * XPL);
-        }
-        const float4 a0 = fa[x & 1][0], a1 = fa[x & 1][1];
-#ifdef W4_NO_MFMA
-        acc[x][0] += a0.x + a1.y + u[x][0].x;
-        if constexpr (false) {
-#else
-        if constexpr (BF) {
-#endif
-          const bf16x8 ah = __builtin_bit_cast(bf16x8, a0), al = __builtin_bit_cast(bf16x8, a1);
-          const bf16x8 bh = __builtin_bit_cast(bf16x8, u[x][0]), bl = __builtin_bit_cast(bf16x8, u[x][1]);
-          acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[x], 0, 0, 0);
-          acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[x], 0, 0, 0);
-          acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[x], 0, 0, 0);
-        } else {
-          const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-          const float bv[8] = {u[x][0].x, u[x][0].y, u[x][0].z, u[x][0].w,
-                               u[x][1].x, u[x][1].y, u[x][1].z, u[x][1].w};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc[x], 0, 0, 0);
-        }
-        load_u(x, s + 1);
-#ifdef W4_PIN_U
-        // keep the next step's U loads here, a whole step ahead of their use (the scheduler
-        // otherwise sinks them to the end of the step, right before the barrier)
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-#ifdef W4_PIN_U2
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-#endif
-      }
-#ifndef W4_NO_BARRIER
-      __syncthreads();
-#endif
-    }
-  }
-
-  // ---- epilogue: inverse transform (+ pre-BN correction) + BN (+PReLU | +residual) ---
-#ifdef W4_NO_EPILOGUE
-  {
-    float sum = 0.f;
-#pragma unroll
-    for (int x = 0; x < XPW; ++x) sum += acc[x][0] + acc[x][5] + acc[x][10] + acc[x][15];
-    if (sum == 12345.f) p.y[tid] = sum;
-    return;
-  }
-#endif
-  // per (tile slot q, output pixel): element offset into y / res (-1 outside the images) and
-  // border class; residuals are loaded before the staging barrier so their latency overlaps it
-  const int ec = tid & 31;
-  const int cout = nb * 32 + ec;
-  int opix[2][4][4];
-  int ocls[2][4][4];
-  float rv[2][4][4];
-  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc4(SPLIT ? p.part + split * p.part_stride : p.y, p.B * H * W * p.Cout * 4);
-  const __amdgpu_buffer_rsrc_t cr = uniform_rsrc4(p.corr, CORR ? 16 * p.Cout * 4 : 0);
-  constexpr bool RES = !SPLIT && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
-  const __amdgpu_buffer_rsrc_t rr = uniform_rsrc4(p.res, RES ? p.B * H * W * p.Cout * 4 : 0);
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int T = mb * WT + (tid >> 5) + 16 * q;
-    const int tr = T / p.TWc, tc = T - tr * p.TWc;
-    const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
-    int orow[4], ocol[4], rcls[4], ccls[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int slot;
-      const int y = canvas_coord(4 * tr + i, ir0, p.Pr, H, sep_r, slot);
-      const int nimg = slot * p.NC;
-      orow[i] = (y >= 0 && nimg < p.B && T < p.ntiles) ? (nimg * H + y) * W : -1;
-      rcls[i] = ((y == 0) ? 1 : 0) | ((y == H - 1) ? 2 : 0);
-      const int xx = canvas_coord(4 * tc + i, ic0, p.Pc, W, sep_c, slot);
-      ocol[i] = (xx >= 0 && slot < p.NC) ? slot * H * W + xx : -1;
-      ccls[i] = ((xx == 0) ? 1 : 0) | ((xx == W - 1) ? 2 : 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int pix = orow[r] + ocol[c];
-        const bool ok = orow[r] >= 0 && ocol[c] >= 0 && pix < p.B * H * W;
-        opix[q][r][c] = ok ? (pix * p.Cout + cout) * 4 : BIGOFF;  // byte offset; BIGOFF = dropped
-        ocls[q][r][c] = rcls[r] * 4 + ccls[c];
-        rv[q][r][c] = 0.f;
-#ifndef W4_EPI_NORES
-        if constexpr (RES)
-          rv[q][r][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, opix[q][r][c], 0, 0));
-#endif
-      }
-  }
-#ifdef W4_NO_BARRIER
-  __syncthreads();
-#endif
-  if (mfma_wave) {
-    const int m = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int x = 0; x < XPW; ++x) {
-      float* dst = lds + (XPW * wid + x) * MPLANE + m;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2) + 4 * h) * MROW] = acc[x][r];
-    }
-  }
-  __syncthreads();
-  const float sc = SPLIT ? 1.f : p.post_scale[cout], sh = SPLIT ? 0.f : p.post_shift[cout];
-  float al = 0.f;
-  if constexpr (!SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU)) al = p.prelu[cout];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int tile = (tid >> 5) + 16 * q;
-    float mv[6][6];
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-      for (int b = 0; b < 6; ++b) mv[a][b] = lds[(6 * a + b) * MPLANE + tile * MROW + ec];
-    float z[6][4];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) at6(mv[a], z[a]);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float col[6], o[4];
-#pragma unroll
-      for (int a = 0; a < 6; ++a) col[a] = z[a][c];
-      at6(col, o);
+      int cs;
+      const int xx = canvas_coord(4 * tc + bq, ic0, p.Pc, W, sep_c, cs);
+      const int ocol = (xx >= 0 && cs < p.NC) ? cs * H * W + xx : -1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int oo = opix[q][r][c];
+        int rsl;
+        const int y = canvas_coord(4 * tr + r, ir0, p.Pr, H, sep_r, rsl);
+        const int nimg = rsl * p.NC;
+        const int orow = (y >= 0 && nimg < p.B && T < p.ntiles) ? (nimg * H + y) * W : -1;
+        const int pix = orow + ocol;
+        const bool ok = orow >= 0 && ocol >= 0 && pix < p.B * H * W;
+        const int oo = ok ? (pix * Cout + cout) * 4 : BIGOFF;  // BIGOFF: the store is dropped
         float v = o[r];
-        if constexpr (CORR) {  // the correction is linear: split 0 carries it
-          if (!SPLIT || split == 0)
-            v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(cr, (ocls[q][r][c] * p.Cout + cout) * 4, 0, 0));
-        }
         if constexpr (!SPLIT) {
           v = v * sc + sh;
           if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
-          if constexpr (EPI == EPI_AFFINE_RES) v += rv[q][r][c];
-          if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
-            v += rv[q][r][c];
-            v = v > 0.f ? v : v * al;
+          if constexpr (RES) {
+            v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, oo, 0, 0));
+            if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = v > 0.f ? v : v * al;
           }
         }
-#ifdef W4_EPI_NOSTORE
-        if (v == 12345.f)
-#endif
-        // branch-free: stores of pixels outside the images carry BIGOFF and are dropped
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), yr, oo, 0, 0);
       }
     }
@@ -465,16 +332,15 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 }
 
 // Split-K finish: y = epilogue(sum over splits of the raw partial outputs), summed in split
-// order (deterministic).  Pixels outside the images were never stored by any split, and
-// none of them is read here (n covers exactly the B*H*W*Cout outputs).
+// order (deterministic).  Pixels outside the images were never stored by any split, and none
+// of them is read here (n4 covers exactly the B*H*W*Cout outputs).
 template <int EPI>
-__global__ void wino4_split_reduce_kernel(const float* __restrict__ part, int S, long long stride, long long n4,
-                                          int Cout, const float* __restrict__ sc, const float* __restrict__ sh,
-                                          const float* __restrict__ prelu, const float* __restrict__ res,
-                                          float* __restrict__ y) {
+__global__ void wino4g_split_reduce_kernel(const float* __restrict__ part, int S, long long stride, long long n4,
+                                           int Cout, const float* __restrict__ sc, const float* __restrict__ sh,
+                                           const float* __restrict__ prelu, const float* __restrict__ res,
+                                           float* __restrict__ y) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  // all slab loads in flight at once (S <= 16 in practice), then summed in split order
   float4 w[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s)
@@ -499,15 +365,15 @@ __global__ void wino4_split_reduce_kernel(const float* __restrict__ part, int S,
   float o[4] = {v.x, v.y, v.z, v.w};
   float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
   if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) r = reinterpret_cast<const float4*>(res)[i];
-  const float rr[4] = {r.x, r.y, r.z, r.w};
+  const float rv[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = c0 + j;
     float t = o[j] * sc[c] + sh[c];
     if constexpr (EPI == EPI_AFFINE_PRELU) t = t > 0.f ? t : t * prelu[c];
-    if constexpr (EPI == EPI_AFFINE_RES) t += rr[j];
+    if constexpr (EPI == EPI_AFFINE_RES) t += rv[j];
     if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
-      t += rr[j];
+      t += rv[j];
       t = t > 0.f ? t : t * prelu[c];
     }
     o[j] = t;
@@ -515,34 +381,10 @@ __global__ void wino4_split_reduce_kernel(const float* __restrict__ part, int S,
   reinterpret_cast<float4*>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
-// Pre-activation BatchNorm folded out of the transform (conv1 of every block):
-//   conv(sc*x + sh, zero padded) = conv(w*sc, x) + sum_{cin, in-image taps} w*sh
-// The second term depends only on which taps of the 3x3 window fall outside the image:
-// class = 4*rowcls + colcls, rowcls bit 0 = top row missing (y == 0), bit 1 = bottom row
-// missing (y == H-1); colcls likewise.  corr[class][cout], summed in double.
-__global__ void wino4_corr_kernel(const float* __restrict__ w, const float* __restrict__ shift,
-                                  float* __restrict__ corr, int Cout, int Cin) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= 16 * Cout) return;
-  const int cls = idx / Cout, o = idx - cls * Cout;
-  const int rc = cls >> 2, cc = cls & 3;
-  double acc = 0.0;
-  for (int ky = 0; ky < 3; ++ky) {
-    if ((ky == 0 && (rc & 1)) || (ky == 2 && (rc & 2))) continue;
-    for (int kx = 0; kx < 3; ++kx) {
-      if ((kx == 0 && (cc & 1)) || (kx == 2 && (cc & 2))) continue;
-      const float* wr = w + ((long long)(o * 3 + ky) * 3 + kx) * Cin;
-      for (int i = 0; i < Cin; ++i) acc += (double)wr[i] * (double)shift[i];
-    }
-  }
-  corr[idx] = (float)acc;
-}
-
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into
 // the fragment order wino4_kernel reads: [xi][Cout/32][Cin/16][q][lane][4] with
 // lane = 32*(c/8) + cout%32, q = (c%8)/4, element = c%4 for c = cin%16.
-__global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __restrict__ pre_scale,
-                                    float* __restrict__ u, int Cout, int Cin) {
+__global__ void wino4_weight_kernel(const float* __restrict__ w, float* __restrict__ u, int Cout, int Cin) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= Cout * Cin) return;
   const int o = idx / Cin, i = idx - o * Cin;
@@ -557,13 +399,6 @@ __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __
   for (int y = 0; y < 3; ++y)
 #pragma unroll
     for (int x = 0; x < 3; ++x) g[y][x] = w[((long long)(o * 3 + y) * 3 + x) * Cin + i];
-  if (pre_scale) {
-    const double ps = pre_scale[i];
-#pragma unroll
-    for (int y = 0; y < 3; ++y)
-#pragma unroll
-      for (int x = 0; x < 3; ++x) g[y][x] *= ps;
-  }
   double tg[6][3];
 #pragma unroll
   for (int a = 0; a < 6; ++a)
@@ -583,50 +418,14 @@ __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __
     }
 }
 
-// bf16 hi/lo split of the transformed filters, fragment order of the BF kernel:
-// [xi][Cout/32][Cin/16][hl][lane][8] bf16 with lane = 32*(c/8) + cout%32, element c%8.
-__global__ void wino4_weight_bf_kernel(const float* __restrict__ u32, unsigned short* __restrict__ ubf, int Cout,
-                                       int Cin) {
-  // u32 is the f32 fragment-ordered U ([xi][Cout/32][Cin/16][q][lane][4], q = (c%8)/4)
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long n = (long long)NXI * Cout * Cin;
-  if (idx >= n) return;
-  const int e4 = (int)(idx & 3);
-  const int ln = (int)((idx >> 2) & 63);
-  const int q = (int)((idx >> 8) & 1);
-  const long long blk = idx >> 9;  // (xi, nb32, s)
-  const float v = u32[idx];
-  const __bf16 hi = (__bf16)v;
-  const __bf16 lo = (__bf16)(v - (float)hi);
-  const long long o = ((blk * 2) * 64 + ln) * 8 + 4 * q + e4;  // hi; lo is 64*8 later
-  ubf[o] = __builtin_bit_cast(unsigned short, hi);
-  ubf[o + 64 * 8] = __builtin_bit_cast(unsigned short, lo);
-}
-
 }  // namespace
-
-hipError_t launch_wino4_weights_bf(const float* u32, void* ubf, int Cout, int Cin, hipStream_t s) {
-  if (Cout % 32 || Cin % KC) return hipErrorInvalidValue;
-  const long long n = (long long)NXI * Cout * Cin;
-  hipLaunchKernelGGL(wino4_weight_bf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u32,
-                     static_cast<unsigned short*>(ubf), Cout, Cin);
-  return hipGetLastError();
-}
-
-bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
-  return kh == 3 && kw == 3 && stride == 1 && pad == 1 && Cin % KC == 0 && Cin >= KC && Cout % 32 == 0 && Cout >= 32;
-}
 
 size_t wino4_weight_floats(int Cout, int Cin) { return (size_t)NXI * Cout * Cin; }
 
-hipError_t launch_wino4_weights(const float* w, const float* pre_scale, const float* pre_shift, float* u,
-                                float* corr, int Cout, int Cin, hipStream_t s) {
-  if (Cout % 32 || Cin % KC || (pre_scale && (!pre_shift || !corr))) return hipErrorInvalidValue;
+hipError_t launch_wino4_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s) {
+  if (Cout % 32 || Cin % KC) return hipErrorInvalidValue;
   const int n = Cout * Cin;
-  hipLaunchKernelGGL(wino4_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, pre_scale, u, Cout, Cin);
-  if (pre_scale)
-    hipLaunchKernelGGL(wino4_corr_kernel, dim3((16 * Cout + 255) / 256), dim3(256), 0, s, w, pre_shift, corr, Cout,
-                       Cin);
+  hipLaunchKernelGGL(wino4_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, u, Cout, Cin);
   return hipGetLastError();
 }
 
@@ -647,38 +446,40 @@ void wino4_canvas(Wino4Params& p) {
   p.ntiles = TRc * p.TWc;
 }
 
-hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s, bool bf) {
-  Wino4Params p = p0;
-  if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
-      (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF ||
-      (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) || (long long)NXI * p.Cout * p.Cin * 4 >= (1ll << 31))
+bool wino4g_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
+  return kh == 3 && kw == 3 && stride == 1 && pad == 1 && Cin % 32 == 0 && Cin >= 32 && Cout % 32 == 0 && Cout >= 32;
+}
+
+size_t wino4g_v_floats(int B, int H, int W, int Cin) {
+  Wino4Params p{};
+  p.B = B;
+  p.H = H;
+  p.W = W;
+  wino4_canvas(p);
+  const size_t mblocks = (p.ntiles + WT - 1) / WT;
+  return mblocks * (size_t)(Cin / KC) * CHUNK;
+}
+
+hipError_t wino4g_prepare(Wino4Params& p) {
+  if (!wino4g_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 || !p.v ||
+      (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF || (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) ||
+      (long long)NXI * p.Cout * p.Cin * 4 >= (1ll << 31))
     return hipErrorInvalidValue;
   wino4_canvas(p);
   p.mblocks = (p.ntiles + WT - 1) / WT;
-  p.nblocks = p.Cout / 32;
-  // 4 cout blocks per tile block (C3: 9,515 -> 9,707 faces/s; 2: 9,673, 8: 9,704);
-  // FRHIP_W4_NBG overrides for experiments
-  static const int nbg_env = [] {
-    const char* e = getenv("FRHIP_W4_NBG");
-    return e ? atoi(e) : 4;
-  }();
-  p.nbg = 1;
-  while (p.nbg * 2 <= nbg_env && p.nblocks % (p.nbg * 2) == 0) p.nbg *= 2;
-  // split-K when the grid leaves most CUs idle (small batches): as many splits as fit one
-  // round of 256 workgroups, bounded by the K-steps and by the partial-output workspace
+  if ((size_t)p.mblocks * (p.Cin / KC) * CHUNK > (size_t)p.v_floats) return hipErrorInvalidValue;
+  p.nblocks = (p.Cout + 63) / 64;
+  p.nbg = std::max(1, std::min(p.mblocks, 32 / p.nblocks));  // tile blocks per XCD group (32 items)
+  // split-K when the grid leaves most CUs idle (serving batches): as many splits as fit one
+  // round of 256 workgroups, bounded by the K-steps and the partial-output workspace
   const int KST = p.Cin / KC;
+  const int nT = p.mblocks * p.nblocks;
   const long long elems = (long long)p.B * p.H * p.W * p.Cout;
-  int S = 1;
   const bool aligned = ((reinterpret_cast<uintptr_t>(p.y) | reinterpret_cast<uintptr_t>(p.res) |
                          reinterpret_cast<uintptr_t>(p.part)) & 15) == 0;
-  // grids of up to 128 workgroups split (>= 2 splits fit one round); FRHIP_W4_SPLIT_WG overrides
-  // that bound for experiments (tools/serve_latency.py sweeps: 96 / 256 / 512 were slower)
-  static const int split_max = [] {
-    const char* e = getenv("FRHIP_W4_SPLIT_WG");
-    return e ? atoi(e) : 128;
-  }();
-  if (!bf && p.part && aligned && p.mblocks * p.nblocks <= split_max && KST > 1) {
-    S = std::min(KST, 256 / (p.mblocks * p.nblocks));  // all splits in one round of 256 CUs
+  int S = 1;
+  if (p.part && aligned && nT <= 128 && KST > 1) {
+    S = std::min(KST, 256 / nT);
     S = (int)std::min<long long>(S, std::min<long long>(p.part_floats, (1ll << 29) - 1) / elems);
     if (S > 1) {
       p.ks_per = (KST + S - 1) / S;
@@ -687,32 +488,51 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s,
   }
   p.ksplit = S > 1 ? S : 1;
   p.part_stride = elems;
-  const dim3 grid(p.mblocks * p.nblocks * p.ksplit), block(512);
+  return hipSuccess;
+}
+
+hipError_t launch_wino4g_transform(const Wino4Params& p, bool pre, hipStream_t s) {
+  if (pre && (!p.pre_scale || !p.pre_shift)) return hipErrorInvalidValue;
+  const dim3 tgrid(p.mblocks, p.Cin / 32);
+  if (pre)
+    hipLaunchKernelGGL(wino4g_itrans_kernel<true>, tgrid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(wino4g_itrans_kernel<false>, tgrid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_wino4g_gemm(const Wino4Params& p, Epi epi, hipStream_t s) {
+  const int nT = p.mblocks * p.nblocks;
   const bool split = p.ksplit > 1;
-#define FR_WINO4_CASE(PRE_, EPI_)                                                                      \
-  if (pre == PRE_ && epi == EPI_) {                                                                    \
-    if (bf)                                                                                            \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, true, false>), grid, block, 0, s, p);                \
-    else if (split)                                                                                    \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, false, true>), grid, block, 0, s, p);                \
-    else                                                                                               \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, false, false>), grid, block, 0, s, p);               \
-    if (split) {                                                                                       \
-      const long long n4 = elems / 4;                                                                  \
-      hipLaunchKernelGGL((wino4_split_reduce_kernel<EPI_>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), \
-                         0, s, p.part, p.ksplit, p.part_stride, n4, p.Cout, p.post_scale, p.post_shift,  \
-                         p.prelu, p.res, p.y);                                                          \
-    }                                                                                                  \
-    return hipGetLastError();                                                                          \
+  const dim3 grid(nT * p.ksplit), block(GEMM_THREADS);
+#define FR_W4G_CASE(EPI_)                                                                                  \
+  if (epi == EPI_) {                                                                                       \
+    if (split)                                                                                             \
+      hipLaunchKernelGGL((wino4g_gemm_kernel<EPI_, true>), grid, block, 0, s, p);                          \
+    else                                                                                                   \
+      hipLaunchKernelGGL((wino4g_gemm_kernel<EPI_, false>), grid, block, 0, s, p);                         \
+    if (split) {                                                                                           \
+      const long long n4 = p.part_stride / 4;                                                              \
+      hipLaunchKernelGGL((wino4g_split_reduce_kernel<EPI_>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), \
+                         0, s, p.part, p.ksplit, p.part_stride, n4, p.Cout, p.post_scale, p.post_shift,      \
+                         p.prelu, p.res, p.y);                                                              \
+    }                                                                                                      \
+    return hipGetLastError();                                                                              \
   }
-  if (pre && !p.corr) return hipErrorInvalidValue;
-  FR_WINO4_CASE(true, EPI_AFFINE_PRELU)   // IR conv1: pre-BN, BN, PReLU
-  FR_WINO4_CASE(false, EPI_AFFINE_RES)    // IR conv2: BN + identity shortcut
-  FR_WINO4_CASE(false, EPI_AFFINE_PRELU)  // SCRFD conv + BN + ReLU (zero slopes)
-  FR_WINO4_CASE(false, EPI_AFFINE)        // SCRFD conv + BN / bias
-  FR_WINO4_CASE(false, EPI_AFFINE_RES_PRELU)  // SCRFD BasicBlock conv2 + BN + add + ReLU
-#undef FR_WINO4_CASE
+  FR_W4G_CASE(EPI_AFFINE_PRELU)      // IR conv1: (pre-BN in pass 1), BN, PReLU; SCRFD conv + BN + ReLU
+  FR_W4G_CASE(EPI_AFFINE_RES)        // IR conv2: BN + identity shortcut
+  FR_W4G_CASE(EPI_AFFINE)            // SCRFD conv + BN / bias
+  FR_W4G_CASE(EPI_AFFINE_RES_PRELU)  // SCRFD BasicBlock conv2 + BN + add + ReLU
+#undef FR_W4G_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_wino4g(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
+  Wino4Params p = p0;
+  hipError_t e = wino4g_prepare(p);
+  if (e == hipSuccess) e = launch_wino4g_transform(p, pre, s);
+  if (e == hipSuccess) e = launch_wino4g_gemm(p, epi, s);
+  return e;
 }
 
 }  // namespace frhip

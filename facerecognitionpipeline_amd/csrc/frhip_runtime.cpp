@@ -309,13 +309,27 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   const bool wino4_epi = wino_epi || (!cw.pre_scale && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE ||
                                                         ((epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU) &&
                                                          (res_H == 0 || res_H == p.Ho) && (res_W == 0 || res_W == p.Wo))));
-  // Winograd F(4x4,3x3) for the stride-1 3x3 convs (f32 parity path only)
-  const bool w4bf = h->prec == PREC_BF16X3 && cw.wino4_bf;
-  if (h->winograd && h->wino_m == 4 && (h->prec == PREC_F32 || w4bf) && cw.wino4 && wino4_epi) {
+  // Winograd F(4x4,3x3) for the stride-1 3x3 convs (f32 parity path only): input transform
+  // pass + transform-domain GEMM (conv_wino4g.hip)
+  if (h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 && wino4_epi &&
+      wino4g_supported(cw.cin, cw.cout, cw.kh, cw.kw, cw.stride, cw.pad)) {
+    const size_t need = wino4g_v_floats(B, H, W, cw.cin);
+    if ((long long)need > h->w4v_floats) {
+      // the embedding nets size this at fr_finalize for max_batch (graphs keep the pointer);
+      // other callers (the detector) grow it here, never inside a capture
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        return fail(h, FR_ERR_STATE, "winograd workspace too small inside a graph capture");
+      FR_HIP(h, hipStreamSynchronize(s));
+      FR_HIP(h, hipFree(h->w4v));
+      h->w4v = nullptr;
+      h->w4v_floats = 0;
+      FR_HIP(h, hipMalloc((void**)&h->w4v, need * sizeof(float)));
+      h->w4v_floats = (long long)need;
+    }
     Wino4Params wp{};
     wp.x = x;
-    wp.u = w4bf ? static_cast<const float*>(cw.wino4_bf) : cw.wino4;
-    wp.corr = cw.wino4_corr;
+    wp.u = cw.wino4;
     wp.y = y;
     wp.pre_scale = cw.pre_scale;
     wp.pre_shift = cw.pre_shift;
@@ -330,14 +344,22 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.Cout = cw.cout;
     wp.part = h->w4part;
     wp.part_floats = h->w4part ? fr_handle::W4PART_FLOATS : 0;
-    Wino4Params cv = wp;
-    wino4_canvas(cv);
-    // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair (bf16x3: 3 bf16 MFMA
-    // products each)
-    const double exec = (w4bf ? 3.0 : 1.0) * 2.0 * 36.0 * cv.ntiles * (double)cw.cin * cw.cout;
-    ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
-    hipError_t e = launch_wino4(wp, cw.pre_scale != nullptr, epi, s, w4bf);
+    wp.v = h->w4v;
+    wp.v_floats = h->w4v_floats;
+    hipError_t e = wino4g_prepare(wp);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
+    {
+      // FR_PROF_WINO_TRANSFORM reports algorithmic bytes in the exec slot: input read + V written
+      const double bytes = 4.0 * ((double)B * H * W * cw.cin + (double)wp.mblocks * 32 * 36 * cw.cin);
+      ProfScope ps(h, s, 0.0, FR_PROF_WINO_TRANSFORM, bytes);
+      e = launch_wino4g_transform(wp, cw.pre_scale != nullptr, s);
+    }
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 transform: ") + hipGetErrorString(e));
+    // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
+    const double exec = 2.0 * 36.0 * wp.ntiles * (double)cw.cin * cw.cout;
+    ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
+    e = launch_wino4g_gemm(wp, epi, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 gemm: ") + hipGetErrorString(e));
     return FR_OK;
   }
   // Winograd F(2x2,3x3) for the stride-1 3x3 convs (f32 parity path only)
@@ -769,81 +791,59 @@ static int ensure_wino4(fr_handle* h) {
     for (ConvW* c : {&b.conv1, &b.conv2}) all.push_back(c);
   detector_convs(h->det, all);
   for (ConvW* c : all) {
-      c->wino4 = nullptr;
-      c->wino4_corr = nullptr;
-      if (c->w && wino4_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
-        wconvs.push_back(c);
-        wfloats += wino4_weight_floats(c->cout, c->cin) + (c->pre_scale ? 16 * (size_t)c->cout : 0);
-      }
+    c->wino4 = nullptr;
+    if (c->w && wino4g_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
+      wconvs.push_back(c);
+      wfloats += wino4_weight_floats(c->cout, c->cin);
     }
+  }
   if (!wfloats) return FR_OK;
   FR_HIP(h, hipMalloc((void**)&h->wino4_arena, wfloats * sizeof(float)));
   size_t off = 0;
   for (ConvW* c : wconvs) {
+    // U = G g G^T of the raw filters: the pre-activation BN is applied to the input in the
+    // transform pass (conv_wino4g.hip), not folded into U
     c->wino4 = h->wino4_arena + off;
     off += wino4_weight_floats(c->cout, c->cin);
-    if (c->pre_scale) {
-      c->wino4_corr = h->wino4_arena + off;
-      off += 16 * (size_t)c->cout;
+    FR_HIP(h, launch_wino4_weights(c->w, c->wino4, c->cout, c->cin, nullptr));
+  }
+  FR_HIP(h, hipDeviceSynchronize());
+  // transformed-input workspace for max_batch crops through every stride-1 3x3 conv of the
+  // embedding net (fixed before any graph capture; the detector grows it in run_conv)
+  if (!h->detector) {
+    size_t need = 0;
+    int HW = 112;
+    for (const auto& b : h->blocks) {
+      need = std::max(need, wino4g_v_floats(h->max_batch, HW, HW, b.conv1.cin));
+      HW /= b.spec.stride;
+      if (b.spec.stride == 1) need = std::max(need, wino4g_v_floats(h->max_batch, HW, HW, b.conv2.cin));
     }
-    FR_HIP(h, launch_wino4_weights(c->w, c->pre_scale, c->pre_shift, c->wino4, c->wino4_corr, c->cout, c->cin,
-                                   nullptr));
+    if ((long long)need > h->w4v_floats) {
+      FR_HIP(h, hipFree(h->w4v));
+      h->w4v = nullptr;
+      h->w4v_floats = 0;
+      FR_HIP(h, hipMalloc((void**)&h->w4v, need * sizeof(float)));
+      h->w4v_floats = (long long)need;
+    }
   }
-  FR_HIP(h, hipDeviceSynchronize());
-  return FR_OK;
-}
-
-// bf16 hi/lo split of every F(4x4) filter set (FR_PRECISION_BF16X3 with FR_CONV_WINOGRAD4)
-static int ensure_wino4_bf(fr_handle* h) {
-  if (h->wino4_bf_arena || !h->wino4_arena) return FR_OK;
-  std::vector<ConvW*> all;
-  for (auto& b : h->blocks)
-    for (ConvW* c : {&b.conv1, &b.conv2}) all.push_back(c);
-  detector_convs(h->det, all);
-  size_t bytes = 0;
-  for (ConvW* c : all)
-    if (c->wino4) bytes += wino4_weight_floats(c->cout, c->cin) * sizeof(float);
-  if (!bytes) return FR_OK;
-  FR_HIP(h, hipMalloc(&h->wino4_bf_arena, bytes));
-  size_t off = 0;
-  for (ConvW* c : all) {
-    c->wino4_bf = nullptr;
-    if (!c->wino4) continue;
-    c->wino4_bf = static_cast<char*>(h->wino4_bf_arena) + off;
-    FR_HIP(h, launch_wino4_weights_bf(c->wino4, c->wino4_bf, c->cout, c->cin, nullptr));
-    off += wino4_weight_floats(c->cout, c->cin) * sizeof(float);
-  }
-  FR_HIP(h, hipDeviceSynchronize());
   return FR_OK;
 }
 
 static void drop_wino4(fr_handle* h) {
   (void)hipFree(h->wino4_arena);
-  (void)hipFree(h->wino4_bf_arena);
   h->wino4_arena = nullptr;
-  h->wino4_bf_arena = nullptr;
   std::vector<ConvW*> all;
   for (auto& b : h->blocks)
     for (ConvW* c : {&b.conv1, &b.conv2}) all.push_back(c);
   detector_convs(h->det, all);
-  for (ConvW* c : all) {
-    c->wino4 = nullptr;
-    c->wino4_corr = nullptr;
-    c->wino4_bf = nullptr;
-  }
+  for (ConvW* c : all) c->wino4 = nullptr;
 }
 
 static int ensure_winograd(fr_handle* h) {
   if (!h->winograd) return FR_OK;
   if (h->wino_m == 2) return ensure_wino2(h);
-  int rc = ensure_wino4(h);
-  // bf16x3 on the F(4x4) kernel is measured slower than the direct split-bf16 kernel (the
-  // Winograd kernel is bound by its transform and load paths, not by the MFMA pipe, and the
-  // hi/lo split adds to the former: DESIGN.md §4), so bf16x3 runs the direct kernel unless
-  // FRHIP_WINO4_BF=1 asks for the Winograd variant
-  const char* ev = getenv("FRHIP_WINO4_BF");
-  if (rc == FR_OK && h->prec == PREC_BF16X3 && ev && ev[0] == '1') rc = ensure_wino4_bf(h);
-  return rc;
+  // bf16x3 runs the direct split-bf16 kernel; the F(4x4) path is f32 only
+  return ensure_wino4(h);
 }
 
 int fr_finalize(fr_handle* h) {
@@ -1367,7 +1367,7 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
   std::lock_guard<std::mutex> lk(h->mu);
   DeviceGuard dg(h->device);
   double tms = 0;
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < 4; ++k) {
     h->last_ms[k] = h->last_flop[k] = h->last_exec[k] = 0;
     h->last_n[k] = 0;
   }
@@ -1376,7 +1376,7 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
     float ms = 0.f;
     FR_HIP(h, hipEventElapsedTime(&ms, e.a, e.b));
     tms += ms;
-    const int k = e.kind >= 0 && e.kind < 3 ? e.kind : 0;
+    const int k = e.kind >= 0 && e.kind < 4 ? e.kind : 0;
     h->last_ms[k] += ms;
     h->last_flop[k] += e.flop;
     h->last_exec[k] += e.exec_flop;
@@ -1385,7 +1385,8 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
     h->pool.push_back(e.b);
   }
   h->events.clear();
-  if (conv_ms) *conv_ms = h->last_ms[1] + h->last_ms[2];
+  // conv time includes the Winograd input-transform passes (they are part of each conv)
+  if (conv_ms) *conv_ms = h->last_ms[1] + h->last_ms[2] + h->last_ms[3];
   if (conv_flop) *conv_flop = h->last_flop[1] + h->last_flop[2];
   if (conv_launches) *conv_launches = h->last_n[1] + h->last_n[2];
   if (total_ms) *total_ms = tms;
@@ -1394,7 +1395,8 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
 
 int fr_profile_kernel(fr_handle* h, int kind, double* ms, double* flop, double* exec_flop, int64_t* launches) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
-  if (kind < 0 || kind > 2) return fail(h, FR_ERR_INVALID_ARGUMENT, "kind must be FR_PROF_OTHER/CONV_DIRECT/CONV_WINOGRAD");
+  if (kind < 0 || kind > 3)
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "kind must be FR_PROF_OTHER/CONV_DIRECT/CONV_WINOGRAD/WINO_TRANSFORM");
   std::lock_guard<std::mutex> lk(h->mu);
   if (ms) *ms = h->last_ms[kind];
   if (flop) *flop = h->last_flop[kind];
@@ -1508,22 +1510,23 @@ int frt_set_wino4_split(int on) {
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                         const float* pre_scale, const float* pre_shift, const float* post_scale,
                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream) {
-  if (!wino4_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
+  if (!wino4g_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
       (epi == EPI_AFFINE_PRELU && (!pre_scale || !pre_shift || !prelu)) || (epi == EPI_AFFINE_RES && (pre_scale || !res)) ||
       !post_scale || !post_shift || B < 1 || H < 1 || W < 1)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  float* u = nullptr;
-  if (hipMalloc((void**)&u, (wino4_weight_floats(cout, cin) + 16 * (size_t)cout) * sizeof(float)) != hipSuccess)
+  float *u = nullptr, *v = nullptr, *part = nullptr;
+  const size_t vf = wino4g_v_floats(B, H, W, cin);
+  if (hipMalloc((void**)&u, wino4_weight_floats(cout, cin) * sizeof(float)) != hipSuccess ||
+      hipMalloc((void**)&v, vf * sizeof(float)) != hipSuccess) {
+    (void)hipFree(u);
     return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4: allocation failed");
-  float* corr = pre_scale ? u + wino4_weight_floats(cout, cin) : nullptr;
-  float* part = nullptr;
-  hipError_t e = launch_wino4_weights(w, pre_scale, pre_shift, u, corr, cout, cin, s);
+  }
+  hipError_t e = launch_wino4_weights(w, u, cout, cin, s);
   if (e == hipSuccess) {
     Wino4Params p{};
     p.x = x;
     p.u = u;
-    p.corr = corr;
     p.y = y;
     p.pre_scale = pre_scale;
     p.pre_shift = pre_shift;
@@ -1536,65 +1539,21 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.W = W;
     p.Cin = cin;
     p.Cout = cout;
+    p.v = v;
+    p.v_floats = (long long)vf;
     if (g_frt_wino4_split) {  // split-K workspace: small grids take the split path
       p.part_floats = (long long)B * H * W * cout * std::min(cin / 16, 16);
       if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;
       p.part = part;
     }
-    if (e == hipSuccess) e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s);
+    if (e == hipSuccess) e = launch_wino4g(p, pre_scale != nullptr, (Epi)epi, s);
   }
   const hipError_t se = hipStreamSynchronize(s);
   (void)hipFree(u);
+  (void)hipFree(v);
   (void)hipFree(part);
   if (e == hipSuccess) e = se;
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd4: ") + hipGetErrorString(e));
-  return FR_OK;
-}
-
-int frt_conv2d_winograd4_bf(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
-                        const float* pre_scale, const float* pre_shift, const float* post_scale,
-                        const float* post_shift, const float* prelu, const float* res, int epi, void* stream) {
-  if (!wino4_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
-      (epi == EPI_AFFINE_PRELU && (!pre_scale || !pre_shift || !prelu)) || (epi == EPI_AFFINE_RES && (pre_scale || !res)) ||
-      !post_scale || !post_shift || B < 1 || H < 1 || W < 1)
-    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4_bf: bad arguments");
-  hipStream_t s = (hipStream_t)stream;
-  float* u = nullptr;
-  if (hipMalloc((void**)&u, (wino4_weight_floats(cout, cin) + 16 * (size_t)cout) * sizeof(float)) != hipSuccess)
-    return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4_bf: allocation failed");
-  float* corr = pre_scale ? u + wino4_weight_floats(cout, cin) : nullptr;
-  hipError_t e = launch_wino4_weights(w, pre_scale, pre_shift, u, corr, cout, cin, s);
-  if (e == hipSuccess) {
-    Wino4Params p{};
-    p.x = x;
-    p.u = u;
-    p.corr = corr;
-    p.y = y;
-    p.pre_scale = pre_scale;
-    p.pre_shift = pre_shift;
-    p.post_scale = post_scale;
-    p.post_shift = post_shift;
-    p.prelu = prelu;
-    p.res = res;
-    p.B = B;
-    p.H = H;
-    p.W = W;
-    p.Cin = cin;
-    p.Cout = cout;
-    void* ubf = nullptr;
-    e = hipMalloc(&ubf, wino4_weight_floats(cout, cin) * sizeof(float));
-    if (e == hipSuccess) e = launch_wino4_weights_bf(u, ubf, cout, cin, s);
-    if (e == hipSuccess) {
-      p.u = static_cast<const float*>(ubf);
-      e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s, true);
-    }
-    (void)hipStreamSynchronize(s);
-    (void)hipFree(ubf);
-  }
-  const hipError_t se = hipStreamSynchronize(s);
-  (void)hipFree(u);
-  if (e == hipSuccess) e = se;
-  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd4_bf: ") + hipGetErrorString(e));
   return FR_OK;
 }
 

@@ -26,9 +26,7 @@ struct ConvW {
   float* post_shift = nullptr;
   float* prelu = nullptr;
   float* wino = nullptr;  // Winograd-transformed filters (stride-1 3x3 only), or null
-  float* wino4 = nullptr; // F(4x4,3x3) transformed filters (built on demand), or null
-  float* wino4_corr = nullptr;  // [16][Cout] pre-BN shift correction of the F(4x4) path (conv1 only)
-  void* wino4_bf = nullptr;     // bf16 hi/lo split of wino4 (FR_PRECISION_BF16X3), built on demand
+  float* wino4 = nullptr; // F(4x4,3x3) transformed filters G g G^T (built on demand), or null
   int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
 };
 
@@ -38,7 +36,8 @@ struct BlockW {
   bool has_sc_conv = false;
 };
 
-// kind: 0 other launch, 1 direct implicit-GEMM conv, 2 Winograd conv (frhip.h FR_PROF_*)
+// kind: 0 other launch, 1 direct implicit-GEMM conv, 2 Winograd conv (GEMM pass), 3 Winograd
+// input transform pass (frhip.h FR_PROF_*)
 struct ProfEvent {
   hipEvent_t a, b;
   double flop;       // algorithmic (direct-conv) FLOPs
@@ -125,9 +124,10 @@ struct fr_handle {
   bool winograd = true;          // FR_CONV_WINOGRAD / _WINOGRAD4 for stride-1 3x3 convs
   int wino_m = 4;                // output tile of the Winograd algorithm: 4 = F(4x4,3x3) (default), 2 = F(2x2,3x3)
   float* wino_arena = nullptr;   // F(2x2) filters, built when that algorithm is selected
-  float* wino4_arena = nullptr;  // F(4x4) filters (+ pre-BN corrections), likewise
-  void* wino4_bf_arena = nullptr;  // their bf16 hi/lo split, built when bf16x3 is selected
+  float* wino4_arena = nullptr;  // F(4x4) filters, likewise
   float* w4part = nullptr;         // F(4x4) split-K partial outputs (small batches), W4PART_FLOATS
+  float* w4v = nullptr;            // F(4x4) transformed input V (conv_wino4g.hip), w4v_floats
+  long long w4v_floats = 0;
   static constexpr long long W4PART_FLOATS = 16ll << 20;
 
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
@@ -147,8 +147,8 @@ struct fr_handle {
   bool prof = false;
   std::vector<frhip_rt::ProfEvent> events;
   std::vector<hipEvent_t> pool;
-  double last_ms[3] = {0, 0, 0}, last_flop[3] = {0, 0, 0}, last_exec[3] = {0, 0, 0};
-  int64_t last_n[3] = {0, 0, 0};
+  double last_ms[4] = {0, 0, 0, 0}, last_flop[4] = {0, 0, 0, 0}, last_exec[4] = {0, 0, 0, 0};
+  int64_t last_n[4] = {0, 0, 0, 0};
 
   ~fr_handle() {
     frhip_rt::detector_destroy(det);
@@ -162,8 +162,8 @@ struct fr_handle {
     (void)hipFree(arena);
     (void)hipFree(wino_arena);
     (void)hipFree(wino4_arena);
-    (void)hipFree(wino4_bf_arena);
     (void)hipFree(w4part);
+    (void)hipFree(w4v);
     for (auto p : act) (void)hipFree(p);
     (void)hipFree(sc_buf);
     (void)hipFree(partial);

@@ -18,8 +18,6 @@ def lib():
         L.frt_conv2d_winograd.argtypes = [_P, _P, _P] + [_I] * 5 + [_P] * 6 + [_I, _P]
         L.frt_conv2d_winograd4.restype = _I
         L.frt_conv2d_winograd4.argtypes = [_P, _P, _P] + [_I] * 5 + [_P] * 6 + [_I, _P]
-        L.frt_conv2d_winograd4_bf.restype = _I
-        L.frt_conv2d_winograd4_bf.argtypes = [_P, _P, _P] + [_I] * 5 + [_P] * 6 + [_I, _P]
         L.frt_set_wino4_split.restype = _I
         L.frt_set_wino4_split.argtypes = [_I]
         L.frt_stem.restype = _I
@@ -51,13 +49,13 @@ def conv2d(x, w, B, H, W, cin, cout, kh, kw, stride, pad, pre=None, post=None, p
     return y if nsplit > 1 else y[0]
 
 
-def conv2d_winograd(x, w, B, H, W, cin, cout, pre=None, post=None, prelu=None, res=None, epi=1, m=2, bf=False):
-    """Winograd F(mxm,3x3) stride-1 conv (m = 2 or 4; bf: F(4x4) in split-bf16);
+def conv2d_winograd(x, w, B, H, W, cin, cout, pre=None, post=None, prelu=None, res=None, epi=1, m=2):
+    """Winograd F(mxm,3x3) stride-1 conv (m = 2 or 4);
     x NHWC cuda f32, w [cout][3][3][cin] cuda f32."""
     y = torch.full((B, H, W, cout), float("nan"), device=x.device)
     ps, ph = (pre if pre is not None else (None, None))
     qs, qh = post
-    fn = (lib().frt_conv2d_winograd4_bf if bf else lib().frt_conv2d_winograd4) if m == 4 else lib().frt_conv2d_winograd
+    fn = lib().frt_conv2d_winograd4 if m == 4 else lib().frt_conv2d_winograd
     rc = fn(_p(x), _p(w), _p(y), B, H, W, cin, cout, _p(ps), _p(ph), _p(qs), _p(qh),
             _p(prelu), _p(res), epi, torch.cuda.current_stream().cuda_stream)
     _lib.check(rc)
