@@ -337,8 +337,8 @@ def main():
             alg_bytes = kj.get("alg_bytes_per_launch")
             if traffic is not None:
                 traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
-        kernel_name = {"winograd": ("wino4g_gemm_kernel (Winograd F(4x4,3x3) f32 transform-domain GEMM + output "
-                                    "transform, every stride-1 3x3 conv)"
+        kernel_name = {"winograd": ("wino4_kernel (Winograd F(4x4,3x3) f32: fused input transform, 16x16x4 "
+                                    "MFMA, lane-local output transform; every stride-1 3x3 conv)"
                                     if args.conv_algorithm == "winograd4" else
                                     "wino_kernel (Winograd F(2x2,3x3) f32, every stride-1 3x3 conv)"),
                        "direct": "conv_mfma_kernel (implicit-GEMM; every conv/FC launch in this mode)"}[dom]
@@ -362,13 +362,6 @@ def main():
                                 + " and cin x cout pair); alg_equiv_tflops counts direct-conv FLOPs (2*M*N*K), "
                                   "which Winograd needs " + ("4x" if args.conv_algorithm == "winograd4" else "2.25x")
                                 + " fewer of, so it can exceed the peak")
-        tp = prof.get("wino_transform", {})
-        if tp.get("launches"):
-            roofline["transform_pass"] = {
-                "kernel": "wino4g_itrans_kernel (pre-BN + B^T d B of every 6x6 patch, once per conv)",
-                "bound": "hbm", "launches": tp["launches"], "avg_launch_ms": round(tp["ms"] / tp["launches"], 5),
-                "alg_gbps": round(tp["exec_flop"] / (tp["ms"] * 1e-3) / 1e9, 1), "peak_gbps": 8000.0,
-                "share_of_step": round(tp["ms"] / max(prof["total_ms"], 1e-9), 4)}
         if "direct" in fams and dom != "direct":
             d = fams["direct"]
             roofline["other_conv_kernel"] = {"kernel": "conv_mfma_kernel (stride-2 / 1x1 convs, FC, gallery scores)",

@@ -286,7 +286,7 @@ class Handle:
         check(self._lib.fr_profile_read(self.h, ctypes.byref(cms), ctypes.byref(cfl), ctypes.byref(cn),
                                         ctypes.byref(tms)), self.h)
         out = {"conv_ms": cms.value, "conv_flop": cfl.value, "conv_launches": cn.value, "total_ms": tms.value}
-        for kind, name in ((0, "other"), (1, "direct"), (2, "winograd"), (3, "wino_transform")):
+        for kind, name in ((0, "other"), (1, "direct"), (2, "winograd")):
             ms, fl, ex = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
             n = ctypes.c_int64()
             check(self._lib.fr_profile_kernel(self.h, kind, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(ex),

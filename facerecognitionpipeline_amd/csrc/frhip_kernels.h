@@ -92,45 +92,38 @@ size_t wino_weight_floats(int Cout, int Cin);
 hipError_t launch_wino_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s);
 hipError_t launch_wino(const WinoParams& p, bool pre, Epi epi, hipStream_t s);
 
-// Winograd F(4x4,3x3) stride-1 pad-1 conv in f32 (conv_winograd4.hip), NHWC like ConvParams, in
-// two passes: input transform into v, then the transform-domain GEMM with the output transform
-// and the epilogue fused.  u: launch_wino4_weights output (wino4_weight_floats(Cout, Cin)).
-// Tiles are cut from a canvas of the batch (period Pr x Pc per image, NC images per canvas
-// row, one zero separator row/column when 4 does not divide H/W).
+// Winograd F(4x4,3x3) stride-1 pad-1 conv in f32 (conv_winograd4.hip), NHWC like ConvParams:
+// one fused persistent kernel (transform waves -> LDS ring -> 16x16x4 MFMA waves with the
+// output transform and the epilogue lane-local).  u: launch_wino4_weights output
+// (wino4_weight_floats(Cout, Cin) floats).  Tiles are cut from a canvas of the batch (period
+// Pr x Pc per image, NC images per canvas row, one zero separator row/column when 4 does not
+// divide H/W).
 struct Wino4Params {
   const float* x;
   const float* u;
   float* y;
-  const float* pre_scale;  // pre-activation BN, applied to the in-image input pixels in pass 1
+  const float* pre_scale;  // pre-activation BN, applied to the in-image input pixels
   const float* pre_shift;
   const float* post_scale;
   const float* post_shift;
   const float* prelu;
   const float* res;   // same shape as y
   int B, H, W, Cin, Cout;
-  int Pr, Pc, NC, TWc, ntiles, mblocks, nblocks;  // set by launch_wino4g (wino4_canvas)
-  int nbg;  // tile blocks per XCD group of items (set by launch_wino4g)
-  // split-K workspace (optional): raw partial outputs [ksplit][B*H*W*Cout]; launch_wino4g splits
-  // the K loop over workgroups when the grid is small and part_floats holds the slabs
+  int Pr, Pc, NC, TWc, ntiles, mblocks, nblocks;  // set by launch_wino4 (wino4_canvas)
+  int nbg;  // tile blocks per XCD group of items (set by launch_wino4)
+  // split-K workspace (optional): raw partial outputs [ksplit][B*H*W*Cout]; launch_wino4 splits
+  // the K loop over items when the grid is small and part_floats holds the slabs
   float* part;
   long long part_floats;
-  int ksplit, ks_per;      // set by launch_wino4g
-  long long part_stride;   // set by launch_wino4g
-  float* v;                // transformed input, wino4g_v_floats(B, H, W, Cin) floats
-  long long v_floats;
+  int ksplit, ks_per;      // set by launch_wino4
+  long long part_stride;   // set by launch_wino4
 };
-bool wino4g_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 32, Cout % 32
+bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16
 size_t wino4_weight_floats(int Cout, int Cin);
-size_t wino4g_v_floats(int B, int H, int W, int Cin);
 void wino4_canvas(Wino4Params& p);
 // w: [Cout][3][3][Cin] -> u = G w G^T in fragment order
 hipError_t launch_wino4_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s);
-// the two passes separately (per-kernel profiling): wino4g_prepare fills the derived fields
-// (canvas, blocks, split-K), then the transform pass, then the GEMM pass (+ split-K reduce)
-hipError_t wino4g_prepare(Wino4Params& p);
-hipError_t launch_wino4g_transform(const Wino4Params& p, bool pre, hipStream_t s);
-hipError_t launch_wino4g_gemm(const Wino4Params& p, Epi epi, hipStream_t s);
-hipError_t launch_wino4g(const Wino4Params& p, bool pre, Epi epi, hipStream_t s);
+hipError_t launch_wino4(const Wino4Params& p, bool pre, Epi epi, hipStream_t s);
 
 // uint8 RGB HWC 112x112 -> (BGR, LUT normalise) -> conv3x3 3->64 -> BN -> PReLU, NHWC f32.
 hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64,

@@ -309,24 +309,9 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   const bool wino4_epi = wino_epi || (!cw.pre_scale && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE ||
                                                         ((epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU) &&
                                                          (res_H == 0 || res_H == p.Ho) && (res_W == 0 || res_W == p.Wo))));
-  // Winograd F(4x4,3x3) for the stride-1 3x3 convs (f32 parity path only): input transform
-  // pass + transform-domain GEMM (conv_wino4g.hip)
+  // Winograd F(4x4,3x3) for the stride-1 3x3 convs (f32 parity path only)
   if (h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 && wino4_epi &&
-      wino4g_supported(cw.cin, cw.cout, cw.kh, cw.kw, cw.stride, cw.pad)) {
-    const size_t need = wino4g_v_floats(B, H, W, cw.cin);
-    if ((long long)need > h->w4v_floats) {
-      // the embedding nets size this at fr_finalize for max_batch (graphs keep the pointer);
-      // other callers (the detector) grow it here, never inside a capture
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-        return fail(h, FR_ERR_STATE, "winograd workspace too small inside a graph capture");
-      FR_HIP(h, hipStreamSynchronize(s));
-      FR_HIP(h, hipFree(h->w4v));
-      h->w4v = nullptr;
-      h->w4v_floats = 0;
-      FR_HIP(h, hipMalloc((void**)&h->w4v, need * sizeof(float)));
-      h->w4v_floats = (long long)need;
-    }
+      wino4_supported(cw.cin, cw.cout, cw.kh, cw.kw, cw.stride, cw.pad)) {
     Wino4Params wp{};
     wp.x = x;
     wp.u = cw.wino4;
@@ -344,22 +329,13 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.Cout = cw.cout;
     wp.part = h->w4part;
     wp.part_floats = h->w4part ? fr_handle::W4PART_FLOATS : 0;
-    wp.v = h->w4v;
-    wp.v_floats = h->w4v_floats;
-    hipError_t e = wino4g_prepare(wp);
-    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
-    {
-      // FR_PROF_WINO_TRANSFORM reports algorithmic bytes in the exec slot: input read + V written
-      const double bytes = 4.0 * ((double)B * H * W * cw.cin + (double)wp.mblocks * 32 * 36 * cw.cin);
-      ProfScope ps(h, s, 0.0, FR_PROF_WINO_TRANSFORM, bytes);
-      e = launch_wino4g_transform(wp, cw.pre_scale != nullptr, s);
-    }
-    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 transform: ") + hipGetErrorString(e));
+    Wino4Params cv = wp;
+    wino4_canvas(cv);
     // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
-    const double exec = 2.0 * 36.0 * wp.ntiles * (double)cw.cin * cw.cout;
+    const double exec = 2.0 * 36.0 * cv.ntiles * (double)cw.cin * cw.cout;
     ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
-    e = launch_wino4g_gemm(wp, epi, s);
-    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 gemm: ") + hipGetErrorString(e));
+    hipError_t e = launch_wino4(wp, cw.pre_scale != nullptr, epi, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
     return FR_OK;
   }
   // Winograd F(2x2,3x3) for the stride-1 3x3 convs (f32 parity path only)
@@ -792,7 +768,7 @@ static int ensure_wino4(fr_handle* h) {
   detector_convs(h->det, all);
   for (ConvW* c : all) {
     c->wino4 = nullptr;
-    if (c->w && wino4g_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
+    if (c->w && wino4_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
       wconvs.push_back(c);
       wfloats += wino4_weight_floats(c->cout, c->cin);
     }
@@ -801,31 +777,13 @@ static int ensure_wino4(fr_handle* h) {
   FR_HIP(h, hipMalloc((void**)&h->wino4_arena, wfloats * sizeof(float)));
   size_t off = 0;
   for (ConvW* c : wconvs) {
-    // U = G g G^T of the raw filters: the pre-activation BN is applied to the input in the
-    // transform pass (conv_wino4g.hip), not folded into U
+    // U = G g G^T of the raw filters: the pre-activation BN is applied to the input by the
+    // transform waves (conv_winograd4.hip), not folded into U
     c->wino4 = h->wino4_arena + off;
     off += wino4_weight_floats(c->cout, c->cin);
     FR_HIP(h, launch_wino4_weights(c->w, c->wino4, c->cout, c->cin, nullptr));
   }
   FR_HIP(h, hipDeviceSynchronize());
-  // transformed-input workspace for max_batch crops through every stride-1 3x3 conv of the
-  // embedding net (fixed before any graph capture; the detector grows it in run_conv)
-  if (!h->detector) {
-    size_t need = 0;
-    int HW = 112;
-    for (const auto& b : h->blocks) {
-      need = std::max(need, wino4g_v_floats(h->max_batch, HW, HW, b.conv1.cin));
-      HW /= b.spec.stride;
-      if (b.spec.stride == 1) need = std::max(need, wino4g_v_floats(h->max_batch, HW, HW, b.conv2.cin));
-    }
-    if ((long long)need > h->w4v_floats) {
-      FR_HIP(h, hipFree(h->w4v));
-      h->w4v = nullptr;
-      h->w4v_floats = 0;
-      FR_HIP(h, hipMalloc((void**)&h->w4v, need * sizeof(float)));
-      h->w4v_floats = (long long)need;
-    }
-  }
   return FR_OK;
 }
 
@@ -1367,7 +1325,7 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
   std::lock_guard<std::mutex> lk(h->mu);
   DeviceGuard dg(h->device);
   double tms = 0;
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 3; ++k) {
     h->last_ms[k] = h->last_flop[k] = h->last_exec[k] = 0;
     h->last_n[k] = 0;
   }
@@ -1376,7 +1334,7 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
     float ms = 0.f;
     FR_HIP(h, hipEventElapsedTime(&ms, e.a, e.b));
     tms += ms;
-    const int k = e.kind >= 0 && e.kind < 4 ? e.kind : 0;
+    const int k = e.kind >= 0 && e.kind < 3 ? e.kind : 0;
     h->last_ms[k] += ms;
     h->last_flop[k] += e.flop;
     h->last_exec[k] += e.exec_flop;
@@ -1385,8 +1343,7 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
     h->pool.push_back(e.b);
   }
   h->events.clear();
-  // conv time includes the Winograd input-transform passes (they are part of each conv)
-  if (conv_ms) *conv_ms = h->last_ms[1] + h->last_ms[2] + h->last_ms[3];
+  if (conv_ms) *conv_ms = h->last_ms[1] + h->last_ms[2];
   if (conv_flop) *conv_flop = h->last_flop[1] + h->last_flop[2];
   if (conv_launches) *conv_launches = h->last_n[1] + h->last_n[2];
   if (total_ms) *total_ms = tms;
@@ -1395,8 +1352,7 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
 
 int fr_profile_kernel(fr_handle* h, int kind, double* ms, double* flop, double* exec_flop, int64_t* launches) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
-  if (kind < 0 || kind > 3)
-    return fail(h, FR_ERR_INVALID_ARGUMENT, "kind must be FR_PROF_OTHER/CONV_DIRECT/CONV_WINOGRAD/WINO_TRANSFORM");
+  if (kind < 0 || kind > 2) return fail(h, FR_ERR_INVALID_ARGUMENT, "kind must be FR_PROF_OTHER/CONV_DIRECT/CONV_WINOGRAD");
   std::lock_guard<std::mutex> lk(h->mu);
   if (ms) *ms = h->last_ms[kind];
   if (flop) *flop = h->last_flop[kind];
@@ -1510,18 +1466,14 @@ int frt_set_wino4_split(int on) {
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                         const float* pre_scale, const float* pre_shift, const float* post_scale,
                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream) {
-  if (!wino4g_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
+  if (!wino4_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
       (epi == EPI_AFFINE_PRELU && (!pre_scale || !pre_shift || !prelu)) || (epi == EPI_AFFINE_RES && (pre_scale || !res)) ||
       !post_scale || !post_shift || B < 1 || H < 1 || W < 1)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  float *u = nullptr, *v = nullptr, *part = nullptr;
-  const size_t vf = wino4g_v_floats(B, H, W, cin);
-  if (hipMalloc((void**)&u, wino4_weight_floats(cout, cin) * sizeof(float)) != hipSuccess ||
-      hipMalloc((void**)&v, vf * sizeof(float)) != hipSuccess) {
-    (void)hipFree(u);
+  float *u = nullptr, *part = nullptr;
+  if (hipMalloc((void**)&u, wino4_weight_floats(cout, cin) * sizeof(float)) != hipSuccess)
     return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4: allocation failed");
-  }
   hipError_t e = launch_wino4_weights(w, u, cout, cin, s);
   if (e == hipSuccess) {
     Wino4Params p{};
@@ -1539,18 +1491,15 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.W = W;
     p.Cin = cin;
     p.Cout = cout;
-    p.v = v;
-    p.v_floats = (long long)vf;
     if (g_frt_wino4_split) {  // split-K workspace: small grids take the split path
       p.part_floats = (long long)B * H * W * cout * std::min(cin / 16, 16);
       if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;
       p.part = part;
     }
-    if (e == hipSuccess) e = launch_wino4g(p, pre_scale != nullptr, (Epi)epi, s);
+    if (e == hipSuccess) e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s);
   }
   const hipError_t se = hipStreamSynchronize(s);
   (void)hipFree(u);
-  (void)hipFree(v);
   (void)hipFree(part);
   if (e == hipSuccess) e = se;
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd4: ") + hipGetErrorString(e));

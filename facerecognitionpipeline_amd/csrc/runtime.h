@@ -36,8 +36,7 @@ struct BlockW {
   bool has_sc_conv = false;
 };
 
-// kind: 0 other launch, 1 direct implicit-GEMM conv, 2 Winograd conv (GEMM pass), 3 Winograd
-// input transform pass (frhip.h FR_PROF_*)
+// kind: 0 other launch, 1 direct implicit-GEMM conv, 2 Winograd conv (frhip.h FR_PROF_*)
 struct ProfEvent {
   hipEvent_t a, b;
   double flop;       // algorithmic (direct-conv) FLOPs
@@ -126,8 +125,6 @@ struct fr_handle {
   float* wino_arena = nullptr;   // F(2x2) filters, built when that algorithm is selected
   float* wino4_arena = nullptr;  // F(4x4) filters, likewise
   float* w4part = nullptr;         // F(4x4) split-K partial outputs (small batches), W4PART_FLOATS
-  float* w4v = nullptr;            // F(4x4) transformed input V (conv_wino4g.hip), w4v_floats
-  long long w4v_floats = 0;
   static constexpr long long W4PART_FLOATS = 16ll << 20;
 
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
@@ -147,8 +144,8 @@ struct fr_handle {
   bool prof = false;
   std::vector<frhip_rt::ProfEvent> events;
   std::vector<hipEvent_t> pool;
-  double last_ms[4] = {0, 0, 0, 0}, last_flop[4] = {0, 0, 0, 0}, last_exec[4] = {0, 0, 0, 0};
-  int64_t last_n[4] = {0, 0, 0, 0};
+  double last_ms[3] = {0, 0, 0}, last_flop[3] = {0, 0, 0}, last_exec[3] = {0, 0, 0};
+  int64_t last_n[3] = {0, 0, 0};
 
   ~fr_handle() {
     frhip_rt::detector_destroy(det);
@@ -163,7 +160,6 @@ struct fr_handle {
     (void)hipFree(wino_arena);
     (void)hipFree(wino4_arena);
     (void)hipFree(w4part);
-    (void)hipFree(w4v);
     for (auto p : act) (void)hipFree(p);
     (void)hipFree(sc_buf);
     (void)hipFree(partial);

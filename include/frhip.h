@@ -188,9 +188,7 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
  * launch count. */
 #define FR_PROF_OTHER 0
 #define FR_PROF_CONV_DIRECT 1
-#define FR_PROF_CONV_WINOGRAD 2   /* F(4x4): the transform-domain GEMM pass; F(2x2): the whole conv */
-#define FR_PROF_WINO_TRANSFORM 3  /* F(4x4): the input-transform pass (HBM-bound): flop 0, exec_flop =
-                                     algorithmic bytes (input read + transformed input written) */
+#define FR_PROF_CONV_WINOGRAD 2
 int fr_profile_kernel(fr_handle* h, int kind, double* ms, double* flop, double* exec_flop, int64_t* launches);
 
 /* Last error message of this handle (or of the last failed fr_create if h is NULL). */

@@ -35,10 +35,9 @@ int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, in
 int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                         const float* pre_scale, const float* pre_shift, const float* post_scale,
                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
-/* Winograd F(4x4,3x3) (the FR_CONV_WINOGRAD4 path: input transform pass + transform-domain
- * GEMM, conv_wino4g.hip), same arguments; cin % 32 == 0, cout % 32 == 0.
- * frt_conv2d_winograd4 gives launch_wino4g a split-K workspace (small grids then split the K
- * loop over workgroups + a reduce pass) unless frt_set_wino4_split(0). */
+/* Winograd F(4x4,3x3) (the FR_CONV_WINOGRAD4 path, conv_winograd4.hip), same arguments;
+ * cin % 16 == 0, cout % 16 == 0.  frt_conv2d_winograd4 gives launch_wino4 a split-K workspace
+ * (small grids then split the K loop over items + a reduce pass) unless frt_set_wino4_split(0). */
 int frt_set_wino4_split(int on);
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                          const float* pre_scale, const float* pre_shift, const float* post_scale,

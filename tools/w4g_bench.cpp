@@ -1,0 +1,88 @@
+// Stand-alone timing of one F(4x4) Winograd conv layer (launches back to back), linked
+// against a (possibly modified) copy of csrc/conv_winograd4.hip by tools/w4g_variants.py.
+// usage: w4g_bench B H Cin Cout epi iters   (epi 1 = pre-BN + BN + PReLU, 2 = BN + residual)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "frhip_kernels.h"
+
+using namespace frhip;
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+static float* dev_rand(size_t n, float lo, float hi, unsigned seed) {
+  std::vector<float> h(n);
+  std::mt19937 g(seed);
+  std::uniform_real_distribution<float> d(lo, hi);
+  for (auto& v : h) v = d(g);
+  float* p = nullptr;
+  CK(hipMalloc((void**)&p, n * sizeof(float)));
+  CK(hipMemcpy(p, h.data(), n * sizeof(float), hipMemcpyHostToDevice));
+  return p;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 7) {
+    fprintf(stderr, "usage: %s B H Cin Cout epi iters\n", argv[0]);
+    return 2;
+  }
+  const int B = atoi(argv[1]), H = atoi(argv[2]), Cin = atoi(argv[3]), Cout = atoi(argv[4]);
+  const int epi = atoi(argv[5]), iters = atoi(argv[6]);
+  const size_t nx = (size_t)B * H * H * Cin, ny = (size_t)B * H * H * Cout;
+  float* x = dev_rand(nx, -1.f, 1.f, 1);
+  float* w = dev_rand((size_t)Cout * 9 * Cin, -0.05f, 0.05f, 2);
+  float* res = dev_rand(ny, -1.f, 1.f, 3);
+  float* psc = dev_rand(Cin, 0.5f, 1.5f, 4);
+  float* psh = dev_rand(Cin, -0.1f, 0.1f, 5);
+  float* qsc = dev_rand(Cout, 0.5f, 1.5f, 6);
+  float* qsh = dev_rand(Cout, -0.1f, 0.1f, 7);
+  float* al = dev_rand(Cout, 0.1f, 0.3f, 8);
+  float *u = nullptr, *y = nullptr;
+  CK(hipMalloc((void**)&u, wino4_weight_floats(Cout, Cin) * sizeof(float)));
+  CK(hipMalloc((void**)&y, ny * sizeof(float)));
+  CK(launch_wino4_weights(w, u, Cout, Cin, nullptr));
+  Wino4Params p{};
+  p.x = x;
+  p.u = u;
+  p.y = y;
+  const bool pre = epi == 1;
+  p.pre_scale = pre ? psc : nullptr;
+  p.pre_shift = pre ? psh : nullptr;
+  p.post_scale = qsc;
+  p.post_shift = qsh;
+  p.prelu = al;
+  p.res = epi == 2 ? res : nullptr;
+  p.B = B;
+  p.H = H;
+  p.W = H;
+  p.Cin = Cin;
+  p.Cout = Cout;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 3; ++i) CK(launch_wino4(p, pre, (Epi)epi, nullptr));
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0, nullptr));
+  for (int i = 0; i < iters; ++i) CK(launch_wino4(p, pre, (Epi)epi, nullptr));
+  CK(hipEventRecord(e1, nullptr));
+  CK(hipEventSynchronize(e1));
+  float t = 0;
+  CK(hipEventElapsedTime(&t, e0, e1));
+  Wino4Params c = p;
+  wino4_canvas(c);
+  const double exec = 2.0 * 36.0 * c.ntiles * (double)Cin * Cout;
+  printf("B=%d H=%d %d->%d epi=%d: %.1f us (%.1f TF executed)\n", B, H, Cin, Cout, epi, 1e3 * t / iters,
+         exec / (1e-3 * t / iters) / 1e12);
+  return 0;
+}

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Where the F(4x4) GEMM kernel's time goes: textual variants of the shipping
+csrc/conv_winograd4.hip (tools only, never shipped), each linked with tools/w4g_bench.cpp.
+
+usage: w4g_variants.py build [names...]   (here, hipcc cross-compiles)
+       w4g_variants.py run [names...]     (on the GPU box)
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "facerecognitionpipeline_amd", "csrc")
+SRC = os.path.join(CSRC, "conv_winograd4.hip")
+BENCH = os.path.join(REPO, "tools", "w4g_bench.cpp")
+OUT = os.path.join(REPO, "tools", "wv")
+SHAPES = [(256, 14, 256, 256, 2), (256, 14, 256, 256, 1), (256, 28, 128, 128, 2), (256, 56, 64, 64, 2),
+          (256, 7, 512, 512, 2)]
+
+EPI_START = "    if (!live) continue;\n"
+EPI_END = "\n  }\n}\n\n// Split-K finish"
+MFMA4 = "".join(f"        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.{c}, u.{c}, acc[x], 0, 0, 0);\n" for c in "xyzw")
+TRANS_TURN = """      if (g >= NBUF && g < G && (g & 3) == t) {
+        store(g);
+        if (g + NBUF < G) load(g + NBUF);
+      }"""
+
+
+def noepi(s):
+    a = s.index(EPI_START)
+    b = s.index(EPI_END, a)
+    dummy = ("    float sum = 0.f;\n#pragma unroll\n    for (int x = 0; x < NXI; ++x) sum += acc[x][0] + acc[x][3];\n"
+             "    if (sum == 12345.f) p.y[tid] = 1.f;")
+    return s[:a] + dummy + s[b:]
+
+
+VARIANTS = {
+    "base": lambda s: s,
+    "noepi": noepi,
+    "notrans": lambda s: s.replace(TRANS_TURN, ""),
+    "nomfma": lambda s: s.replace(MFMA4, "        acc[x][0] += a.x * u.x + a.w * u.w;\n"),
+    "nouload": lambda s: s.replace("""        uring[x % URING] = x + URING < NXI ? ld4(ur, lo, (x + URING) * XS + cur)
+                                           : ld4(ur, lo, (x + URING - NXI) * XS + nxt);""", ""),
+    "mfmaonly": lambda s: noepi(s).replace(TRANS_TURN, "").replace("""        uring[x % URING] = x + URING < NXI ? ld4(ur, lo, (x + URING) * XS + cur)
+                                           : ld4(ur, lo, (x + URING - NXI) * XS + nxt);""", ""),
+}
+
+
+def build(name):
+    s = open(SRC).read()
+    v = VARIANTS[name](s)
+    assert name == "base" or v != s, name
+    os.makedirs(OUT, exist_ok=True)
+    src = os.path.join(OUT, f"w4g_{name}.hip")
+    open(src, "w").write(v)
+    exe = os.path.join(OUT, f"w4g_{name}")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I" + CSRC,
+                    "-I" + os.path.join(REPO, "include"), "-x", "hip", src, "-x", "hip", BENCH, "-o", exe], check=True)
+    return exe
+
+
+def main():
+    cmd, names = sys.argv[1], sys.argv[2:] or list(VARIANTS)
+    if cmd == "build":
+        with ThreadPoolExecutor(8) as ex:
+            print(list(ex.map(build, names)))
+    else:
+        for n in names:
+            for shp in SHAPES:
+                r = subprocess.run(["timeout", "-k", "5", "60", os.path.join(OUT, f"w4g_{n}")] + [str(x) for x in shp] + ["20"],
+                                   capture_output=True, text=True)
+                print(f"{n:9s} {r.stdout.strip()} {r.stderr.strip()[-200:]}", flush=True)
+                if r.returncode:
+                    return r.returncode
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
