@@ -26,6 +26,9 @@ SOURCES = ["conv_winograd4.hip", "conv_winograd.hip","conv_f32_w4.hip", "conv_f3
            "embed_misc.hip", "align.hip", "gallery.hip", "detect.hip", "frhip_runtime.cpp", "detector.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
+# F(4x4): keep the transform's f32 math scalar -- packed f32 VALU beside MFMAs costs more issue
+# cycles than the two scalar ops it replaces (MI355X_MICROARCH.md, 'price of one filler')
+EXTRA = {"conv_winograd4.hip": ["-fno-slp-vectorize"]}
 LDFLAGS = ["-shared", f"--offload-arch={ARCH}", f"-Wl,-rpath,{ROCM}/lib", "-Wl,--no-undefined"]
 
 
@@ -36,7 +39,7 @@ def _digest(path: str) -> str:
               os.path.join(REPO, "include", "frhip.h"), os.path.join(REPO, "include", "frhip_testing.h")]:
         with open(p, "rb") as f:
             h.update(f.read())
-    h.update(" ".join(CFLAGS).encode())
+    h.update(" ".join(CFLAGS + EXTRA.get(os.path.basename(path), [])).encode())
     return h.hexdigest()[:16]
 
 
@@ -44,7 +47,7 @@ def _compile(src: str) -> str:
     path = os.path.join(CSRC, src)
     obj = os.path.join(BUILD, f"{src}.{_digest(path)}.o")
     if not os.path.exists(obj):
-        cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", path, "-o", obj + ".tmp"]
+        cmd = [HIPCC, *CFLAGS, *EXTRA.get(src, []), "-x", "hip", "-c", path, "-o", obj + ".tmp"]
         subprocess.run(cmd, check=True)
         os.replace(obj + ".tmp", obj)
     return obj

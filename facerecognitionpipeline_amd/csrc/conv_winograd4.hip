@@ -22,14 +22,17 @@
 //     9 xi-slots ahead in a register ring), 4 MFMAs.  Because a lane holds all 36 xi of its
 //     (tile, cout) positions, the output transform A^T M A is lane-local: no LDS exchange and
 //     no barrier in the epilogue.
-//   * 4 transform waves, one per SIMD: transform wave t produces every K-step g = t (mod 4) of
-//     the workgroup's stream: thread (tile i, channel quad q) loads its 6x6 patch (36 16-byte
-//     loads, issued a whole turn ahead), applies the pre-activation BN at in-image pixels,
-//     transforms and writes 36 float4 (ds_write_b128) into ring slot g % 4.  Its turn comes
-//     every fourth K-step, so its VALU is spread thin beside the MFMA wave of its SIMD.
+//   * 4 transform waves, one per SIMD: every K-step, transform wave t handles tiles 4t..4t+3 of
+//     the item for the step's 16 channels, one 6x6 patch per lane (36 4-byte loads issued a
+//     whole step ahead, addressed from a per-item geometry kept in registers), applies the
+//     pre-activation BN at in-image pixels, transforms and writes its 36 values into the ring
+//     (ds_write_b32).  Each SIMD thus carries a quarter of the transform every step, beside its
+//     MFMA wave.
 //   * One workgroup barrier per K-step (s_barrier with an LDS-only wait: prefetched global
-//     loads stay in flight across it).  Step g is written after barrier g-3 (the slot's
-//     previous step, g-4, was read before it) and read between barriers g and g+1.
+//     loads stay in flight across it).  Step g + 2 is written between barriers g and g + 1
+//     (its slot last held step g - 2, read before barrier g - 1) and read between barriers
+//     g + 2 and g + 3.  The transform waves also leave each item's output geometry in LDS
+//     for the epilogue.
 // Compared with one 32-output-channel block per workgroup and the transform redone for each
 // (round 1), each patch is transformed Cout/64 times instead of Cout/32, and the epilogue
 // needs neither LDS staging nor barriers.
@@ -44,7 +47,7 @@
 // Fragment layouts (v_mfma_f32_16x16x4_f32: A[l&15][k=l>>4], B[k=l>>4][l&15], C/D row
 // (l>>4)*4 + reg, column l&15).  MFMA m (0..3) of a K-step consumes channel 4k + m, so a lane
 // reads the 4 consecutive channels 4k..4k+3 of its tile (V) or of its cout (U) as one float4:
-//   V ring slot (one K-step): [36 xi][64 lane = 16 k + tile][4]           (36,864 B)
+//   V ring slot (one K-step): [36 xi][64 lane = 16 k + tile, as vslot()][4]  (36,864 B)
 //   U: [36 xi][Cout/16][Cin/16][64 lane = 16 k + cout][4]
 #include <algorithm>
 
@@ -64,7 +67,7 @@ constexpr int NBUF = 4;              // LDS ring of transformed K-steps
 constexpr int VSTEP = NXI * FT * KC; // floats of one ring slot (9,216)
 constexpr int URING = 9;             // xi-slots of U in flight per MFMA wave (36 % URING == 0)
 constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum with it is past the range
-static_assert(NBUF * VSTEP * 4 <= 160 * 1024, "LDS budget");
+static_assert((NBUF * VSTEP + 4 * FT * 8) * 4 <= 160 * 1024, "LDS budget");
 static_assert(NXI % URING == 0, "U ring phase must repeat every K-step");
 
 __device__ __forceinline__ int xcd_remap(int bid, int n) {
@@ -87,6 +90,12 @@ __device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, int off, int soff = 
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0);
   return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
 }
+
+// 16-byte slot of A-fragment lane l = 16 k + i in a ring plane: tile bits 2-3 XOR k.  The
+// fragment reads stay one permuted 16-lane row per k (conflict-free ds_read_b128); the
+// transform waves' scalar stores (4 tiles x 16 channels per wave) spread over all 64 banks
+// instead of 16.
+__device__ __forceinline__ int vslot(int l) { return l ^ ((l >> 4) << 2); }
 
 // Workgroup barrier that waits for this wave's LDS operations only: global loads issued ahead
 // (U fragments, the next turn's patches) stay in flight across it.
@@ -111,6 +120,19 @@ __device__ __forceinline__ void bt6(const f4 (&d)[6], f4 (&t)[6]) {
   const f4 s1 = d[3] + d[4], s2 = d[1] + d[2];
   const f4 s3 = d[4] - d[3], s4 = d[1] - d[2];
   const f4 s5 = d[4] - d[2], s6 = d[3] - d[1];
+  t[0] = 4.f * d[0] + (-5.f * d[2] + d[4]);
+  t[1] = -4.f * s2 + s1;
+  t[2] = 4.f * s4 + s3;
+  t[3] = 2.f * s6 + s5;
+  t[4] = -2.f * s6 + s5;
+  t[5] = 4.f * d[1] + (-5.f * d[3] + d[5]);
+}
+
+// the same on one channel
+__device__ __forceinline__ void bt6(const float (&d)[6], float (&t)[6]) {
+  const float s1 = d[3] + d[4], s2 = d[1] + d[2];
+  const float s3 = d[4] - d[3], s4 = d[1] - d[2];
+  const float s5 = d[4] - d[2], s6 = d[3] - d[1];
   t[0] = 4.f * d[0] + (-5.f * d[2] + d[4]);
   t[1] = -4.f * s2 + s1;
   t[2] = 4.f * s4 + s3;
@@ -150,7 +172,7 @@ __device__ __forceinline__ Item item_of(const Wino4Params& p, int t) {
 
 template <bool PRE, int EPI, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
-  __shared__ __attribute__((aligned(16))) float ring[NBUF * VSTEP];
+  __shared__ __attribute__((aligned(16))) float ring[NBUF * VSTEP + 4 * FT * 8];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout;
@@ -165,92 +187,147 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   auto steps_of = [&](const Item& it) { return SPLIT ? min(KS, KST - it.split * KS) : KST; };
   const int G = nloc * KS;  // K-steps in this workgroup's stream (one barrier each)
 
+  int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [4 items][16 tiles][8]
   if (wid >= 4) {
-    // ---- transform waves: wave t writes the stream's steps g = t (mod 4) ------------------
+    // ---- transform waves: every K-step, wave t transforms tiles 4t .. 4t+3 of the item for
+    // the step's 16 channels: lane (ii, ch) = channel ch of tile 4t + ii, one 6x6 patch per
+    // lane (a patch row's loads cover 4 runs of 64 contiguous bytes).  Step g + 2 is written
+    // during the period between barriers g and g + 1 (its ring slot last held step g - 2, read
+    // before barrier g - 1); its patch loads were issued one period earlier, so they have a
+    // whole MFMA step to land.
     const int t = wid - 4;
-    const int i = lane & 15, q = lane >> 4;  // tile of the item, channel quad of the step
+    const int ch = lane & 15, i = 4 * t + (lane >> 4);
     const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
+    const __amdgpu_buffer_rsrc_t xr_none = uniform_rsrc(p.x, 0);
     const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
-    f4 d[6][6];
-    bool rin[6], cin[6];
-    int rimg[6], cimg[6];
-    f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
-    // issue the patch loads of step g (registers only; no LDS)
-    auto load = [&](int g) {
-      const int j = g / KS, s = g - j * KS;
-      const Item it = item_at(j);
-      const int step = (SPLIT ? it.split * KS : 0) + min(s, steps_of(it) - 1);
+    // the item's patch geometry, recomputed when the load stream enters a new item
+    int roff[6], coff[6];
+    unsigned long long inmask = 0;  // bit 6r + c: patch pixel (r, c) is inside an image (PRE)
+    int lj = 0, ls = 0, ks_real = KS, step0 = 0;
+    auto enter_item = [&](int j) {
+      const Item it = item_at(min(j, nloc - 1));
+      ks_real = steps_of(it);
+      step0 = SPLIT ? it.split * KS : 0;
       const int T = it.mb * FT + i;
       const int tr = T / p.TWc, tc = T - tr * p.TWc;
       const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
-      int roff[6], coff[6];
-      const int c0 = step * KC + 4 * q;
+      int rimg[6], cimg[6];
+      bool rin[6], cin[6];
 #pragma unroll
       for (int e = 0; e < 6; ++e) {
         int rs, cs;
         const int y = canvas_coord(4 * tr - 1 + e, ir0, p.Pr, H, sep_r, rs);
         const int x = canvas_coord(4 * tc - 1 + e, ic0, p.Pc, W, sep_c, cs);
-        rin[e] = y >= 0 && T < p.ntiles && s < steps_of(it);
+        rin[e] = y >= 0 && T < p.ntiles;
         cin[e] = x >= 0 && cs < p.NC;
         rimg[e] = rs * p.NC;
         cimg[e] = cs;
         roff[e] = rin[e] ? (rs * p.NC * H + y) * W * Cin * 4 : BIGOFF;
-        coff[e] = cin[e] ? ((cs * H * W + x) * Cin + c0) * 4 : BIGOFF;
+        coff[e] = cin[e] ? ((cs * H * W + x) * Cin + ch) * 4 : BIGOFF;
       }
+      if constexpr (PRE) {
+        inmask = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+          for (int b = 0; b < 6; ++b)
+            inmask |= (rin[a] && cin[b] && rimg[a] + cimg[b] < p.B) ? 1ull << (6 * a + b) : 0ull;
+      }
+      // output geometry of the item's tiles, for the MFMA waves' epilogue (not for the
+      // stream's overrun: item j - 4's table may still be in use)
+      if (ch == 0 && j < nloc) {
+        int* gt = geo + ((j & 3) * FT + i) * 8;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int rs, cs;
+          const int y = canvas_coord(4 * tr + e, ir0, p.Pr, H, sep_r, rs);
+          const int x = canvas_coord(4 * tc + e, ic0, p.Pc, W, sep_c, cs);
+          gt[e] = (y >= 0 && rs * p.NC < p.B && T < p.ntiles) ? (rs * p.NC * H + y) * W : -1;
+          gt[4 + e] = (x >= 0 && cs < p.NC) ? cs * H * W + x : -1;
+        }
+      }
+    };
+    float pa[6][6], pb[6][6];
+    float sc_a = 1.f, sh_a = 0.f, sc_b = 1.f, sh_b = 0.f;
+    // issue the patch loads of the next step of the stream (steps are loaded in order)
+    auto load = [&](float (&d)[6][6], float& sc, float& sh, unsigned long long& mask) {
+      if (ls == 0) enter_item(lj);
+      // split-K padding step: every load is out of range (num_records 0) and reads zeros, and
+      // the BN shift is masked off
+      const bool live = !SPLIT || ls < ks_real;
+      const __amdgpu_buffer_rsrc_t r = live ? xr : xr_none;
+      mask = live ? inmask : 0ull;
+      const int step = step0 + min(ls, ks_real - 1);
+      const int soff = step * KC * 4;
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
-        for (int b = 0; b < 6; ++b) d[a][b] = ld4(xr, (int)((unsigned)roff[a] + (unsigned)coff[b]));
+        for (int b = 0; b < 6; ++b)
+          d[a][b] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(r, (int)((unsigned)roff[a] + (unsigned)coff[b]), soff, 0));
       if constexpr (PRE) {
-        sc = *reinterpret_cast<const f4*>(p.pre_scale + c0);
-        sh = *reinterpret_cast<const f4*>(p.pre_shift + c0);
+        sc = p.pre_scale[step * KC + ch];
+        sh = p.pre_shift[step * KC + ch];
+      }
+      if (++ls == KS) {
+        ls = 0;
+        ++lj;
       }
     };
-    // transform the loaded patch and write it into ring slot g % NBUF
-    auto store = [&](int g) {
+    // transform a loaded patch and write it into ring slot g % NBUF
+    auto store = [&](float (&d)[6][6], float sc, float sh, unsigned long long mask, int g) {
       if constexpr (PRE) {
         // BN(x) = x * scale + shift at in-image pixels only: the conv's zero padding (and the
         // canvas separators / the images past B) stay 0, as in BN -> zero-padded Conv2d
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
-          for (int b = 0; b < 6; ++b) {
-            const bool in = rin[a] && cin[b] && (rimg[a] + cimg[b]) < p.B;
-            const f4 v = d[a][b] * sc + sh;
-            d[a][b] = in ? v : f4{0.f, 0.f, 0.f, 0.f};
-          }
+          for (int b = 0; b < 6; ++b) d[a][b] = (mask >> (6 * a + b)) & 1ull ? d[a][b] * sc + sh : 0.f;
       }
 #pragma unroll
       for (int b = 0; b < 6; ++b) {  // columns: d[.][b] <- (B^T d)[.][b]
-        f4 c[6], o[6];
+        float c[6], o[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) c[a] = d[a][b];
         bt6(c, o);
 #pragma unroll
         for (int a = 0; a < 6; ++a) d[a][b] = o[a];
       }
-      float* dst = ring + (g % NBUF) * VSTEP + lane * 4;
+      // A-fragment slot of (tile i, channel ch): lane 16 k + i (k = ch / 4), element ch % 4,
+      // stored at 16-byte slot 16 k + (i ^ 4k) (vslot) so a wave's 64 stores hit 64 banks
+      float* dst = ring + (g % NBUF) * VSTEP + vslot(16 * (ch >> 2) + i) * 4 + (ch & 3);
 #pragma unroll
       for (int a = 0; a < 6; ++a) {
-        f4 v[6];
+        float v[6];
         bt6(d[a], v);
 #pragma unroll
-        for (int b = 0; b < 6; ++b) *reinterpret_cast<f4*>(dst + (6 * a + b) * 256) = v[b];
+        for (int b = 0; b < 6; ++b) dst[(6 * a + b) * 256] = v[b];
       }
     };
-    // prologue: steps 0..3 (wave t: step t) written before the first barrier
-    if (t < G) {
-      load(t);
-      store(t);
-      if (t + NBUF < G) load(t + NBUF);
-    }
-    for (int b = 0; b < G; ++b) {
-      lds_barrier();  // barrier b: step b is readable; slot (b + 3) % 4 is free (step b - 1 read)
-      const int g = b + 3;
-      if (g >= NBUF && g < G && (g & 3) == t) {
-        store(g);
-        if (g + NBUF < G) load(g + NBUF);
-      }
+    // prologue: steps 0 and 1 written before the first barrier, step 2 in flight.  The BN mask
+    // travels with its patch (mask_a / mask_b): the load stream may enter the next item first.
+    unsigned long long mask_a, mask_b = 0;
+    load(pa, sc_a, sh_a, mask_a);
+    store(pa, sc_a, sh_a, mask_a, 0);
+    load(pa, sc_a, sh_a, mask_a);
+    store(pa, sc_a, sh_a, mask_a, 1);
+    load(pa, sc_a, sh_a, mask_a);
+    // The loads are unconditional (past the stream's end they fetch whatever the clamped
+    // geometry names, and are never stored): a branch around them would make the compiler's
+    // wait-count tracking wait for the freshly issued loads before the store.
+    // Stores past the end are unconditional too: step g >= G's slot held step g - 4, already
+    // read, and nothing reads it again.
+    for (int b = 0;; b += 2) {  // two periods per trip: the patch registers ping-pong
+      lds_barrier();            // barrier b
+      load(pb, sc_b, sh_b, mask_b);
+      __builtin_amdgcn_sched_barrier(0);  // the loads go out first, a whole period ahead
+      store(pa, sc_a, sh_a, mask_a, b + 2);
+      if (b + 1 >= G) break;
+      lds_barrier();  // barrier b + 1
+      load(pa, sc_a, sh_a, mask_a);
+      __builtin_amdgcn_sched_barrier(0);
+      store(pb, sc_b, sh_b, mask_b, b + 3);
+      if (b + 2 >= G) break;
     }
     return;
   }
@@ -274,7 +351,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   int ub = ubase(0), ul = ulast(0);
 #pragma unroll
   for (int r = 0; r < URING; ++r) uring[r] = ld4(ur, lo, r * XS + ub);
-  const float* vrd = ring + lane * 4;
+  const float* vrd = ring + vslot(lane) * 4;
   int g = 0;
   for (int j = 0; j < nloc; ++j) {
     const Item it = item_at(j);
@@ -290,24 +367,37 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       // U refills: xi + URING of this step, or xi + URING - 36 of the next step (or item)
       const int cur = ub + min(s, ul) * 1024;
       const int nxt = s + 1 < KS ? ub + min(s + 1, ul) * 1024 : ub_next;
-      // A fragments one xi ahead (the LDS read of xi + 1 is in flight during xi's MFMAs); an
-      // idle quarter (!live) computes on a clamped U block and is never stored
-      f4 a_next = *reinterpret_cast<const f4*>(vb);
+      // xi in pairs: the two accumulation chains interleave (a 16x16x4 MFMA's result is not
+      // ready for the next one on the same accumulator at issue rate).  A fragments one pair
+      // ahead (the LDS reads of pair x + 2 are in flight during pair x's MFMAs); an idle
+      // quarter (!live) computes on a clamped U block and is never stored.
+      f4 a0n = *reinterpret_cast<const f4*>(vb), a1n = *reinterpret_cast<const f4*>(vb + 256);
 #pragma unroll
-      for (int x = 0; x < NXI; ++x) {
-        const f4 a = a_next;
-        if (x + 1 < NXI) a_next = *reinterpret_cast<const f4*>(vb + (x + 1) * 256);
-        const f4 u = uring[x % URING];
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, u.x, acc[x], 0, 0, 0);
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, u.y, acc[x], 0, 0, 0);
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, u.z, acc[x], 0, 0, 0);
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, u.w, acc[x], 0, 0, 0);
-        uring[x % URING] = x + URING < NXI ? ld4(ur, lo, (x + URING) * XS + cur)
-                                           : ld4(ur, lo, (x + URING - NXI) * XS + nxt);
-        // pin the slot's order: LDS read of xi + 1, the 4 MFMAs of xi, the U refill
-        if (x + 1 < NXI) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      for (int x = 0; x < NXI; x += 2) {
+        const f4 a0 = a0n, a1 = a1n;
+        if (x + 2 < NXI) {
+          a0n = *reinterpret_cast<const f4*>(vb + (x + 2) * 256);
+          a1n = *reinterpret_cast<const f4*>(vb + (x + 3) * 256);
+        }
+        const f4 u0 = uring[x % URING], u1 = uring[(x + 1) % URING];
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, u0.x, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, u1.x, acc[x + 1], 0, 0, 0);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, u0.y, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, u1.y, acc[x + 1], 0, 0, 0);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, u0.z, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, u1.z, acc[x + 1], 0, 0, 0);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, u0.w, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, u1.w, acc[x + 1], 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int y = x + e;
+          uring[y % URING] = y + URING < NXI ? ld4(ur, lo, (y + URING) * XS + cur)
+                                             : ld4(ur, lo, (y + URING - NXI) * XS + nxt);
+        }
+        // pin the slot's order: LDS reads of the next pair, the 8 MFMAs, the 2 U refills
+        if (x + 2 < NXI) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -325,21 +415,16 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     const float sc = SPLIT ? 1.f : p.post_scale[cout], sh = SPLIT ? 0.f : p.post_shift[cout];
     float al = 0.f;
     if constexpr (!SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU)) al = p.prelu[cout];
-    const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
     int oo[4][4];
     float rv[4][4];
+    const int* gj = geo + (j & 3) * FT * 8;
     auto geometry = [&](int r) {  // byte offsets of tile 4rg + r's 16 outputs (BIGOFF: dropped)
-      const int T = it.mb * FT + 4 * rg + r;
-      const int tr = T / p.TWc, tc = T - tr * p.TWc;
-      const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
+      const int* gt = gj + (4 * rg + r) * 8;
       int orow[4], ocol[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        int rs, cs;
-        const int y = canvas_coord(4 * tr + e, ir0, p.Pr, H, sep_r, rs);
-        const int x = canvas_coord(4 * tc + e, ic0, p.Pc, W, sep_c, cs);
-        orow[e] = (y >= 0 && rs * p.NC < p.B && T < p.ntiles) ? (rs * p.NC * H + y) * W : -1;
-        ocol[e] = (x >= 0 && cs < p.NC) ? cs * H * W + x : -1;
+        orow[e] = gt[e];
+        ocol[e] = gt[4 + e];
       }
 #pragma unroll
       for (int y = 0; y < 4; ++y)

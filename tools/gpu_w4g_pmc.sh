@@ -23,7 +23,7 @@ d = sys.argv[1]
 tot = collections.defaultdict(float); n = collections.defaultdict(int)
 for f in glob.glob(d + "/p*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "gemm" not in r["Kernel_Name"]:
+        if "wino4_kernel" not in r["Kernel_Name"]:
             continue
         tot[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
 print(d.split("/")[-1], {k: round(v / max(1, n[k] / (1 if k.startswith("GRBM") or k.startswith("TCC") else 1)), 0) for k, v in sorted(tot.items())})

@@ -20,11 +20,24 @@ SHAPES = [(256, 14, 256, 256, 2), (256, 14, 256, 256, 1), (256, 28, 128, 128, 2)
 
 EPI_START = "    if (!live) continue;\n"
 EPI_END = "\n  }\n}\n\n// Split-K finish"
-MFMA4 = "".join(f"        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.{c}, u.{c}, acc[x], 0, 0, 0);\n" for c in "xyzw")
-TRANS_TURN = """      if (g >= NBUF && g < G && (g & 3) == t) {
-        store(g);
-        if (g + NBUF < G) load(g + NBUF);
-      }"""
+MFMA8 = "".join(f"        acc[x{o}] = __builtin_amdgcn_mfma_f32_16x16x4f32(a{e}.{c}, u{e}.{c}, acc[x{o}], 0, 0, 0);\n"
+                for c in "xyzw" for e, o in ((0, ""), (1, " + 1")))
+ULOAD = """          uring[y % URING] = y + URING < NXI ? ld4(ur, lo, (y + URING) * XS + cur)
+                                             : ld4(ur, lo, (y + URING - NXI) * XS + nxt);"""
+
+
+def nouload(s):
+    assert ULOAD in s
+    return s.replace(ULOAD, "")
+
+
+TRANS_TURN = """      store(pa, sc_a, sh_a, mask_a, b + 2);"""
+TRANS_TURN2 = """      store(pb, sc_b, sh_b, mask_b, b + 3);"""
+
+
+def notrans(s):
+    assert TRANS_TURN in s and TRANS_TURN2 in s
+    return s.replace(TRANS_TURN, "").replace(TRANS_TURN2, "")
 
 
 def noepi(s):
@@ -38,12 +51,16 @@ def noepi(s):
 VARIANTS = {
     "base": lambda s: s,
     "noepi": noepi,
-    "notrans": lambda s: s.replace(TRANS_TURN, ""),
-    "nomfma": lambda s: s.replace(MFMA4, "        acc[x][0] += a.x * u.x + a.w * u.w;\n"),
-    "nouload": lambda s: s.replace("""        uring[x % URING] = x + URING < NXI ? ld4(ur, lo, (x + URING) * XS + cur)
-                                           : ld4(ur, lo, (x + URING - NXI) * XS + nxt);""", ""),
-    "mfmaonly": lambda s: noepi(s).replace(TRANS_TURN, "").replace("""        uring[x % URING] = x + URING < NXI ? ld4(ur, lo, (x + URING) * XS + cur)
-                                           : ld4(ur, lo, (x + URING - NXI) * XS + nxt);""", ""),
+    "notrans": notrans,
+    "noload": lambda s: s.replace("""          d[a][b] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(r, (int)((unsigned)roff[a] + (unsigned)coff[b]), soff, 0));""", "          d[a][b] = __int_as_float(roff[a] + coff[b] + soff);"),
+    "nomfma": lambda s: s.replace(MFMA8, "        acc[x][0] += a0.x * u0.x + a1.w * u1.w;\n"),
+    "nouload": nouload,
+    "mfmaonly": lambda s: nouload(notrans(noepi(s))),
+    "nomfma_noload": lambda s: VARIANTS["noload"](VARIANTS["nomfma"](s)),
+    "nomfma_notrans": lambda s: notrans(VARIANTS["nomfma"](s)),
+    "nomfma_noepi": lambda s: noepi(VARIANTS["nomfma"](s)),
+    "skeleton": lambda s: nouload(notrans(noepi(VARIANTS["nomfma"](s)))),
 }
 
 
@@ -55,7 +72,7 @@ def build(name):
     src = os.path.join(OUT, f"w4g_{name}.hip")
     open(src, "w").write(v)
     exe = os.path.join(OUT, f"w4g_{name}")
-    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I" + CSRC,
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-slp-vectorize", "-I" + CSRC,
                     "-I" + os.path.join(REPO, "include"), "-x", "hip", src, "-x", "hip", BENCH, "-o", exe], check=True)
     return exe
 
