@@ -25,7 +25,8 @@
 //   * 4 transform waves, one per SIMD: every K-step, transform wave t handles tiles 4t..4t+3 of
 //     the item for the step's 16 channels, one 6x6 patch per lane (36 4-byte loads issued a
 //     whole step ahead, addressed from a per-item geometry kept in registers), applies the
-//     pre-activation BN at in-image pixels, transforms and writes its 36 values into the ring
+//     pre-activation BN (folded: scale into U, shift/scale added at in-image pixels),
+//     transforms and writes its 36 values into the ring
 //     (ds_write_b32).  Each SIMD thus carries a quarter of the transform every step, beside its
 //     MFMA wave.
 //   * One workgroup barrier per K-step (s_barrier with an LDS-only wait: prefetched global
@@ -48,6 +49,8 @@
 // (l>>4)*4 + reg, column l&15).  MFMA m (0..3) of a K-step consumes channel 4k + m, so a lane
 // reads the 4 consecutive channels 4k..4k+3 of its tile (V) or of its cout (U) as one float4:
 //   V ring slot (one K-step): [36 xi][64 lane = 16 k + tile, as vslot()][4]  (36,864 B)
+// U is the MFMA's A operand (rows = couts) and V the B operand (columns = tiles), so the
+// accumulator of lane (tile l&15, row group l>>4) holds 4 consecutive couts of one tile.
 //   U: [36 xi][Cout/16][Cin/16][64 lane = 16 k + cout][4]
 #include <algorithm>
 
@@ -115,30 +118,21 @@ __device__ __forceinline__ int canvas_coord(int v, int base, int P, int H, bool 
   return in0 ? y : (in1 ? y1 : -1);
 }
 
-// 1-D input transform B^T d (6 -> 6) of four channels
-__device__ __forceinline__ void bt6(const f4 (&d)[6], f4 (&t)[6]) {
-  const f4 s1 = d[3] + d[4], s2 = d[1] + d[2];
-  const f4 s3 = d[4] - d[3], s4 = d[1] - d[2];
-  const f4 s5 = d[4] - d[2], s6 = d[3] - d[1];
-  t[0] = 4.f * d[0] + (-5.f * d[2] + d[4]);
-  t[1] = -4.f * s2 + s1;
-  t[2] = 4.f * s4 + s3;
-  t[3] = 2.f * s6 + s5;
-  t[4] = -2.f * s6 + s5;
-  t[5] = 4.f * d[1] + (-5.f * d[3] + d[5]);
-}
-
-// the same on one channel
+// 1-D input transform B^T d (6 -> 6), 12 ops:
+//   t0 = 4 d0 - 5 d2 + d4 = 4 (d0 - d2) + r        r = d4 - d2,  u = d3 - d1
+//   t1 = -4 (d1 + d2) + d3 + d4 = p + q            p = d4 - 4 d2, q = d3 - 4 d1
+//   t2 = 4 (d1 - d2) - d3 + d4 = p - q
+//   t3 = 2 (d3 - d1) + d4 - d2 = r + 2u,  t4 = r - 2u
+//   t5 = 4 d1 - 5 d3 + d5 = (d5 - d3) - 4u
 __device__ __forceinline__ void bt6(const float (&d)[6], float (&t)[6]) {
-  const float s1 = d[3] + d[4], s2 = d[1] + d[2];
-  const float s3 = d[4] - d[3], s4 = d[1] - d[2];
-  const float s5 = d[4] - d[2], s6 = d[3] - d[1];
-  t[0] = 4.f * d[0] + (-5.f * d[2] + d[4]);
-  t[1] = -4.f * s2 + s1;
-  t[2] = 4.f * s4 + s3;
-  t[3] = 2.f * s6 + s5;
-  t[4] = -2.f * s6 + s5;
-  t[5] = 4.f * d[1] + (-5.f * d[3] + d[5]);
+  const float r = d[4] - d[2], u = d[3] - d[1];
+  const float pp = __builtin_fmaf(-4.f, d[2], d[4]), q = __builtin_fmaf(-4.f, d[1], d[3]);
+  t[0] = __builtin_fmaf(4.f, d[0] - d[2], r);
+  t[1] = pp + q;
+  t[2] = pp - q;
+  t[3] = __builtin_fmaf(2.f, u, r);
+  t[4] = __builtin_fmaf(-2.f, u, r);
+  t[5] = __builtin_fmaf(-4.f, u, d[5] - d[3]);
 }
 
 // 1-D output transform A^T m (6 -> 4)
@@ -200,9 +194,14 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
     const __amdgpu_buffer_rsrc_t xr_none = uniform_rsrc(p.x, 0);
     const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
-    // the item's patch geometry, recomputed when the load stream enters a new item
-    int roff[6], coff[6];
-    unsigned long long inmask = 0;  // bit 6r + c: patch pixel (r, c) is inside an image (PRE)
+    // the item's patch geometry, recomputed when the load stream enters a new item: byte
+    // offset of every patch pixel (channel ch of step 0; BIGOFF sums for padding)
+    int poff[6][6];
+    // PRE: in-image masks of the patch rows / columns (1 or 0).  Separable: a patch pixel of an
+    // image past B (partial last canvas row) is never inside the 3x3 window of a stored output
+    // (a separator row / column lies between; launch_wino4 forces one below every image row
+    // when such a canvas row exists), so it may take the shift like an in-image pixel.
+    float rowm[6], colm[6];
     int lj = 0, ls = 0, ks_real = KS, step0 = 0;
     auto enter_item = [&](int j) {
       const Item it = item_at(min(j, nloc - 1));
@@ -211,28 +210,28 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       const int T = it.mb * FT + i;
       const int tr = T / p.TWc, tc = T - tr * p.TWc;
       const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
-      int rimg[6], cimg[6];
+      int roff[6], coff[6];
       bool rin[6], cin[6];
 #pragma unroll
       for (int e = 0; e < 6; ++e) {
         int rs, cs;
         const int y = canvas_coord(4 * tr - 1 + e, ir0, p.Pr, H, sep_r, rs);
         const int x = canvas_coord(4 * tc - 1 + e, ic0, p.Pc, W, sep_c, cs);
-        rin[e] = y >= 0 && T < p.ntiles;
+        rin[e] = y >= 0 && rs * p.NC < p.B && T < p.ntiles;
         cin[e] = x >= 0 && cs < p.NC;
-        rimg[e] = rs * p.NC;
-        cimg[e] = cs;
         roff[e] = rin[e] ? (rs * p.NC * H + y) * W * Cin * 4 : BIGOFF;
         coff[e] = cin[e] ? ((cs * H * W + x) * Cin + ch) * 4 : BIGOFF;
       }
-      if constexpr (PRE) {
-        inmask = 0;
 #pragma unroll
-        for (int a = 0; a < 6; ++a)
+      for (int a = 0; a < 6; ++a)
 #pragma unroll
-          for (int b = 0; b < 6; ++b)
-            inmask |= (rin[a] && cin[b] && rimg[a] + cimg[b] < p.B) ? 1ull << (6 * a + b) : 0ull;
-      }
+        for (int b = 0; b < 6; ++b) poff[a][b] = (int)((unsigned)roff[a] + (unsigned)coff[b]);
+      if constexpr (PRE)
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+          rowm[e] = rin[e] ? 1.f : 0.f;
+          colm[e] = cin[e] ? 1.f : 0.f;
+        }
       // output geometry of the item's tiles, for the MFMA waves' epilogue (not for the
       // stream's overrun: item j - 4's table may still be in use)
       if (ch == 0 && j < nloc) {
@@ -247,27 +246,35 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         }
       }
     };
-    float pa[6][6], pb[6][6];
-    float sc_a = 1.f, sh_a = 0.f, sc_b = 1.f, sh_b = 0.f;
+    // a patch buffer: the 6x6 values and, for PRE, the folded shift t = shift / scale of its
+    // channel at its item's in-image rows (trow) and columns (colm)
+    struct Patch {
+      float d[6][6];
+      float trow[6], colm[6];
+    };
+    Patch pa, pb, pc;
     // issue the patch loads of the next step of the stream (steps are loaded in order)
-    auto load = [&](float (&d)[6][6], float& sc, float& sh, unsigned long long& mask) {
+    auto load = [&](Patch& P) {
       if (ls == 0) enter_item(lj);
       // split-K padding step: every load is out of range (num_records 0) and reads zeros, and
-      // the BN shift is masked off
+      // the BN shift is dropped
       const bool live = !SPLIT || ls < ks_real;
       const __amdgpu_buffer_rsrc_t r = live ? xr : xr_none;
-      mask = live ? inmask : 0ull;
       const int step = step0 + min(ls, ks_real - 1);
       const int soff = step * KC * 4;
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
         for (int b = 0; b < 6; ++b)
-          d[a][b] = __uint_as_float(
-              __builtin_amdgcn_raw_buffer_load_b32(r, (int)((unsigned)roff[a] + (unsigned)coff[b]), soff, 0));
+          P.d[a][b] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(r, poff[a][b], soff, 0));
       if constexpr (PRE) {
-        sc = p.pre_scale[step * KC + ch];
-        sh = p.pre_shift[step * KC + ch];
+        const float t = live ? p.pre_t[step * KC + ch] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+          P.trow[e] = t * rowm[e];
+          P.colm[e] = colm[e];
+        }
       }
       if (++ls == KS) {
         ls = 0;
@@ -275,15 +282,15 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       }
     };
     // transform a loaded patch and write it into ring slot g % NBUF
-    auto store = [&](float (&d)[6][6], float sc, float sh, unsigned long long mask, int g) {
-      if constexpr (PRE) {
-        // BN(x) = x * scale + shift at in-image pixels only: the conv's zero padding (and the
-        // canvas separators / the images past B) stay 0, as in BN -> zero-padded Conv2d
+    auto store = [&](Patch& P, int g) {
+      float (&d)[6][6] = P.d;
+      if constexpr (PRE)
+        // BN(x) = scale (x + t) with the scale folded into U: add t at in-image pixels only,
+        // the conv's zero padding and the canvas separators stay 0 (BN -> zero-padded Conv2d)
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
-          for (int b = 0; b < 6; ++b) d[a][b] = (mask >> (6 * a + b)) & 1ull ? d[a][b] * sc + sh : 0.f;
-      }
+          for (int b = 0; b < 6; ++b) d[a][b] = __builtin_fmaf(P.trow[a], P.colm[b], d[a][b]);
 #pragma unroll
       for (int b = 0; b < 6; ++b) {  // columns: d[.][b] <- (B^T d)[.][b]
         float c[6], o[6];
@@ -304,30 +311,36 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         for (int b = 0; b < 6; ++b) dst[(6 * a + b) * 256] = v[b];
       }
     };
-    // prologue: steps 0 and 1 written before the first barrier, step 2 in flight.  The BN mask
-    // travels with its patch (mask_a / mask_b): the load stream may enter the next item first.
-    unsigned long long mask_a, mask_b = 0;
-    load(pa, sc_a, sh_a, mask_a);
-    store(pa, sc_a, sh_a, mask_a, 0);
-    load(pa, sc_a, sh_a, mask_a);
-    store(pa, sc_a, sh_a, mask_a, 1);
-    load(pa, sc_a, sh_a, mask_a);
-    // The loads are unconditional (past the stream's end they fetch whatever the clamped
-    // geometry names, and are never stored): a branch around them would make the compiler's
-    // wait-count tracking wait for the freshly issued loads before the store.
+    // prologue: steps 0 and 1 written before the first barrier, steps 2 and 3 in flight (the
+    // load stream runs ahead, into the next item at item ends: each buffer carries its own t)
+    load(pa);
+    store(pa, 0);
+    load(pa);
+    store(pa, 1);
+    load(pa);
+    load(pb);
+    // Step g + 2 is stored in period g from loads issued two periods earlier (three patch
+    // buffers rotate).  The loads are unconditional (past the stream's end they fetch whatever
+    // the clamped geometry names, and are never read): a branch around them would make the
+    // compiler's wait-count tracking wait for the freshly issued loads before the store.
     // Stores past the end are unconditional too: step g >= G's slot held step g - 4, already
     // read, and nothing reads it again.
-    for (int b = 0;; b += 2) {  // two periods per trip: the patch registers ping-pong
-      lds_barrier();            // barrier b
-      load(pb, sc_b, sh_b, mask_b);
-      __builtin_amdgcn_sched_barrier(0);  // the loads go out first, a whole period ahead
-      store(pa, sc_a, sh_a, mask_a, b + 2);
+    for (int b = 0;; b += 3) {
+      lds_barrier();  // barrier b
+      load(pc);
+      __builtin_amdgcn_sched_barrier(0);  // the loads go out first
+      store(pa, b + 2);
       if (b + 1 >= G) break;
       lds_barrier();  // barrier b + 1
-      load(pa, sc_a, sh_a, mask_a);
+      load(pa);
       __builtin_amdgcn_sched_barrier(0);
-      store(pb, sc_b, sh_b, mask_b, b + 3);
+      store(pb, b + 3);
       if (b + 2 >= G) break;
+      lds_barrier();  // barrier b + 2
+      load(pb);
+      __builtin_amdgcn_sched_barrier(0);
+      store(pc, b + 4);
+      if (b + 3 >= G) break;
     }
     return;
   }
@@ -380,14 +393,14 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
           a1n = *reinterpret_cast<const f4*>(vb + (x + 3) * 256);
         }
         const f4 u0 = uring[x % URING], u1 = uring[(x + 1) % URING];
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, u0.x, acc[x], 0, 0, 0);
-        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, u1.x, acc[x + 1], 0, 0, 0);
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, u0.y, acc[x], 0, 0, 0);
-        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, u1.y, acc[x + 1], 0, 0, 0);
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, u0.z, acc[x], 0, 0, 0);
-        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, u1.z, acc[x + 1], 0, 0, 0);
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, u0.w, acc[x], 0, 0, 0);
-        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, u1.w, acc[x + 1], 0, 0, 0);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0.x, a0.x, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1.x, a1.x, acc[x + 1], 0, 0, 0);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0.y, a0.y, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1.y, a1.y, acc[x + 1], 0, 0, 0);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0.z, a0.z, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1.z, a1.z, acc[x + 1], 0, 0, 0);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0.w, a0.w, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1.w, a1.w, acc[x + 1], 0, 0, 0);
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int y = x + e;
@@ -404,42 +417,35 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     ub = ub_next;
     ul = ulast(j + 1);
     if (!live) continue;
-    // ---- epilogue (lane-local): lane (cout column n, row group rg) holds tiles 4rg + r of
-    // cout n for every xi; Y = A^T M A per (tile, cout), BN (+PReLU | +residual), store
+    // ---- epilogue (lane-local): U is the A operand, so lane (tile n, row group rg) holds
+    // couts 4rg .. 4rg+3 of tile n for every xi; Y = A^T M A per (tile, cout), BN (+PReLU |
+    // +residual), one 16-byte store of the 4 couts per output pixel
     const int n = lane & 15, rg = lane >> 4;
-    const int cout = it.nb * 64 + w * 16 + n;
+    const int cout0 = it.nb * 64 + w * 16 + 4 * rg;
     const __amdgpu_buffer_rsrc_t yr =
         uniform_rsrc(SPLIT ? p.part + it.split * p.part_stride : p.y, p.B * H * W * Cout * 4);
     constexpr bool RES = !SPLIT && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
+    constexpr bool PRELU = !SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU);
     const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, RES ? p.B * H * W * Cout * 4 : 0);
-    const float sc = SPLIT ? 1.f : p.post_scale[cout], sh = SPLIT ? 0.f : p.post_shift[cout];
-    float al = 0.f;
-    if constexpr (!SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU)) al = p.prelu[cout];
+    // byte offsets of tile n's 16 outputs (BIGOFF: outside the images, dropped)
+    const int* gt = geo + ((j & 3) * FT + n) * 8;
     int oo[4][4];
-    float rv[4][4];
-    const int* gj = geo + (j & 3) * FT * 8;
-    auto geometry = [&](int r) {  // byte offsets of tile 4rg + r's 16 outputs (BIGOFF: dropped)
-      const int* gt = gj + (4 * rg + r) * 8;
-      int orow[4], ocol[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        orow[e] = gt[e];
-        ocol[e] = gt[4 + e];
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int orow = gt[y], ocol = gt[4 + x], pix = orow + ocol;
+        const bool ok = orow >= 0 && ocol >= 0 && pix < p.B * H * W;
+        oo[y][x] = ok ? (pix * Cout + cout0) * 4 : BIGOFF;
       }
+    // residual rows: row 0 in flight during the output transform, row y + 1 during row y
+    f4 rv[2][4];
+    if constexpr (RES)
 #pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const int pix = orow[y] + ocol[x];
-          const bool ok = orow[y] >= 0 && ocol[x] >= 0 && pix < p.B * H * W;
-          oo[y][x] = ok ? (pix * Cout + cout) * 4 : BIGOFF;
-          rv[y][x] = 0.f;
-          if constexpr (RES) rv[y][x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, oo[y][x], 0, 0));
-        }
-    };
+      for (int x = 0; x < 4; ++x) rv[0][x] = ld4(rr, oo[0][x]);
+    float out[4][4][4];  // [cout r][y][x]
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      geometry(r);
       float z[6][4];
 #pragma unroll
       for (int a = 0; a < 6; ++a) {  // rows: A^T along b
@@ -453,18 +459,38 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         float o[4];
         at6(c6, o);
 #pragma unroll
-        for (int y = 0; y < 4; ++y) {
-          float v = o[y];
-          if constexpr (!SPLIT) {
-            v = v * sc + sh;
-            if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
+        for (int y = 0; y < 4; ++y) out[r][y][x] = o[y];
+      }
+    }
+    f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f}, al = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (!SPLIT) {
+      sc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
+      sh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
+    }
+    if constexpr (PRELU) al = *reinterpret_cast<const f4*>(p.prelu + cout0);
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      if constexpr (RES)
+        if (y + 1 < 4)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) rv[(y + 1) & 1][x] = ld4(rr, oo[y + 1][x]);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        f4 v = {out[0][y][x], out[1][y][x], out[2][y][x], out[3][y][x]};
+        if constexpr (!SPLIT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t = v[r] * sc[r] + sh[r];
+            if constexpr (EPI == EPI_AFFINE_PRELU) t = t > 0.f ? t : t * al[r];
             if constexpr (RES) {
-              v += rv[y][x];
-              if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = v > 0.f ? v : v * al;
+              t += rv[y & 1][x][r];
+              if constexpr (EPI == EPI_AFFINE_RES_PRELU) t = t > 0.f ? t : t * al[r];
             }
+            v[r] = t;
           }
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), yr, oo[y][x], 0, 0);
         }
+        const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(bits, yr, oo[y][x], 0, 0);
       }
     }
   }
@@ -523,7 +549,8 @@ __global__ void wino4_split_reduce_kernel(const float* __restrict__ part, int S,
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
 // B-fragment order wino4_kernel reads: [xi][Cout/16][Cin/16][lane = 16 k + cout%16][m] with
 // cin % 16 = 4k + m.
-__global__ void wino4_weight_kernel(const float* __restrict__ w, float* __restrict__ u, int Cout, int Cin) {
+__global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __restrict__ pre_scale,
+                                    float* __restrict__ u, int Cout, int Cin) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= Cout * Cin) return;
   const int o = idx / Cin, i = idx - o * Cin;
@@ -537,7 +564,8 @@ __global__ void wino4_weight_kernel(const float* __restrict__ w, float* __restri
 #pragma unroll
   for (int y = 0; y < 3; ++y)
 #pragma unroll
-    for (int x = 0; x < 3; ++x) g[y][x] = w[((long long)(o * 3 + y) * 3 + x) * Cin + i];
+    for (int x = 0; x < 3; ++x)
+      g[y][x] = (double)w[((long long)(o * 3 + y) * 3 + x) * Cin + i] * (pre_scale ? (double)pre_scale[i] : 1.0);
   double tg[6][3];
 #pragma unroll
   for (int a = 0; a < 6; ++a)
@@ -561,10 +589,10 @@ __global__ void wino4_weight_kernel(const float* __restrict__ w, float* __restri
 
 size_t wino4_weight_floats(int Cout, int Cin) { return (size_t)NXI * Cout * Cin; }
 
-hipError_t launch_wino4_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s) {
+hipError_t launch_wino4_weights(const float* w, const float* pre_scale, float* u, int Cout, int Cin, hipStream_t s) {
   if (Cout % 16 || Cin % KC) return hipErrorInvalidValue;
   const int n = Cout * Cin;
-  hipLaunchKernelGGL(wino4_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, u, Cout, Cin);
+  hipLaunchKernelGGL(wino4_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, pre_scale, u, Cout, Cin);
   return hipGetLastError();
 }
 
@@ -592,10 +620,16 @@ bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
 hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
   Wino4Params p = p0;
   if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
-      (pre && (!p.pre_scale || !p.pre_shift)) || (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF ||
+      (pre && !p.pre_t) || (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF ||
       (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) || (long long)NXI * p.Cout * p.Cin * 4 >= (1ll << 31))
     return hipErrorInvalidValue;
   wino4_canvas(p);
+  if (pre && p.NC > 1 && p.B % p.NC && p.Pr == p.H) {
+    // a partial last canvas row directly below full ones: give every image row a separator
+    // row so the absent images' pixels stay outside every stored output's window (PRE masks)
+    p.Pr = p.H + 1;
+    p.ntiles = ((((p.B + p.NC - 1) / p.NC) * p.Pr + 3) / 4) * p.TWc;
+  }
   p.mblocks = (p.ntiles + FT - 1) / FT;
   p.nblocks = (p.Cout + FN - 1) / FN;
   p.nbg = std::max(1, std::min(p.mblocks, 32 / p.nblocks));  // tile blocks per XCD group (32 items)

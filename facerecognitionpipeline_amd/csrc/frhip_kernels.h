@@ -102,8 +102,9 @@ struct Wino4Params {
   const float* x;
   const float* u;
   float* y;
-  const float* pre_scale;  // pre-activation BN, applied to the in-image input pixels
-  const float* pre_shift;
+  // pre-activation BN folded into the filters: U built from w * scale (launch_wino4_weights),
+  // and t = shift / scale per input channel added to the in-image input pixels
+  const float* pre_t;
   const float* post_scale;
   const float* post_shift;
   const float* prelu;
@@ -121,8 +122,8 @@ struct Wino4Params {
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16
 size_t wino4_weight_floats(int Cout, int Cin);
 void wino4_canvas(Wino4Params& p);
-// w: [Cout][3][3][Cin] -> u = G w G^T in fragment order
-hipError_t launch_wino4_weights(const float* w, float* u, int Cout, int Cin, hipStream_t s);
+// w: [Cout][3][3][Cin] -> u = G (w * pre_scale[cin]) G^T in fragment order (pre_scale nullable)
+hipError_t launch_wino4_weights(const float* w, const float* pre_scale, float* u, int Cout, int Cin, hipStream_t s);
 hipError_t launch_wino4(const Wino4Params& p, bool pre, Epi epi, hipStream_t s);
 
 // uint8 RGB HWC 112x112 -> (BGR, LUT normalise) -> conv3x3 3->64 -> BN -> PReLU, NHWC f32.

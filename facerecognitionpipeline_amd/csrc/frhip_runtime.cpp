@@ -316,8 +316,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.x = x;
     wp.u = cw.wino4;
     wp.y = y;
-    wp.pre_scale = cw.pre_scale;
-    wp.pre_shift = cw.pre_shift;
+    wp.pre_t = cw.wino4_t;
     wp.post_scale = cw.post_scale;
     wp.post_shift = cw.post_shift;
     wp.prelu = cw.prelu;
@@ -758,9 +757,27 @@ static int ensure_wino2(fr_handle* h) {
 
 // F(4x4,3x3) filters of every eligible conv, built on the device from the arena the first
 // time the algorithm is selected after fr_finalize (36/9 = 4x the 3x3 weights).
+// The pre-activation BN of a conv1 is folded: U = G (g * scale) G^T and t = shift / scale is
+// added to the in-image input pixels, so BN(x) = scale (x + t).  A conv whose BN scale has a
+// zero (t not finite) keeps the direct kernel.
+static bool wino4_pre_fold(const ConvW* c, std::vector<float>& t) {
+  t.assign(c->cin, 0.f);
+  if (!c->pre_scale) return true;
+  std::vector<float> sc(c->cin), sh(c->cin);
+  if (hipMemcpy(sc.data(), c->pre_scale, c->cin * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(sh.data(), c->pre_shift, c->cin * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+    return false;
+  for (int i = 0; i < c->cin; ++i) {
+    t[i] = sh[i] / sc[i];
+    if (sc[i] == 0.f || !std::isfinite(t[i])) return false;
+  }
+  return true;
+}
+
 static int ensure_wino4(fr_handle* h) {
   if (h->wino4_arena) return FR_OK;
   std::vector<ConvW*> wconvs;
+  std::vector<std::vector<float>> ts;
   size_t wfloats = 0;
   std::vector<ConvW*> all;
   for (auto& b : h->blocks)
@@ -768,20 +785,27 @@ static int ensure_wino4(fr_handle* h) {
   detector_convs(h->det, all);
   for (ConvW* c : all) {
     c->wino4 = nullptr;
-    if (c->w && wino4_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad)) {
+    c->wino4_t = nullptr;
+    std::vector<float> t;
+    if (c->w && wino4_supported(c->cin, c->cout, c->kh, c->kw, c->stride, c->pad) && wino4_pre_fold(c, t)) {
       wconvs.push_back(c);
-      wfloats += wino4_weight_floats(c->cout, c->cin);
+      ts.push_back(std::move(t));
+      wfloats += wino4_weight_floats(c->cout, c->cin) + (c->pre_scale ? c->cin : 0);
     }
   }
   if (!wfloats) return FR_OK;
   FR_HIP(h, hipMalloc((void**)&h->wino4_arena, wfloats * sizeof(float)));
   size_t off = 0;
-  for (ConvW* c : wconvs) {
-    // U = G g G^T of the raw filters: the pre-activation BN is applied to the input by the
-    // transform waves (conv_winograd4.hip), not folded into U
+  for (size_t k = 0; k < wconvs.size(); ++k) {
+    ConvW* c = wconvs[k];
     c->wino4 = h->wino4_arena + off;
     off += wino4_weight_floats(c->cout, c->cin);
-    FR_HIP(h, launch_wino4_weights(c->w, c->wino4, c->cout, c->cin, nullptr));
+    FR_HIP(h, launch_wino4_weights(c->w, c->pre_scale, c->wino4, c->cout, c->cin, nullptr));
+    if (c->pre_scale) {
+      c->wino4_t = h->wino4_arena + off;
+      off += c->cin;
+      FR_HIP(h, hipMemcpy(c->wino4_t, ts[k].data(), c->cin * sizeof(float), hipMemcpyHostToDevice));
+    }
   }
   FR_HIP(h, hipDeviceSynchronize());
   return FR_OK;
@@ -794,7 +818,10 @@ static void drop_wino4(fr_handle* h) {
   for (auto& b : h->blocks)
     for (ConvW* c : {&b.conv1, &b.conv2}) all.push_back(c);
   detector_convs(h->det, all);
-  for (ConvW* c : all) c->wino4 = nullptr;
+  for (ConvW* c : all) {
+    c->wino4 = nullptr;
+    c->wino4_t = nullptr;
+  }
 }
 
 static int ensure_winograd(fr_handle* h) {
@@ -1471,17 +1498,25 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
       !post_scale || !post_shift || B < 1 || H < 1 || W < 1)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  float *u = nullptr, *part = nullptr;
-  if (hipMalloc((void**)&u, wino4_weight_floats(cout, cin) * sizeof(float)) != hipSuccess)
+  ConvW cw;
+  cw.cin = cin;
+  cw.pre_scale = const_cast<float*>(pre_scale);
+  cw.pre_shift = const_cast<float*>(pre_shift);
+  std::vector<float> t;
+  if (hipStreamSynchronize(s) != hipSuccess || !wino4_pre_fold(&cw, t))
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4: pre-BN scale has a zero");
+  float *u = nullptr, *part = nullptr, *pre_t = nullptr;
+  if (hipMalloc((void**)&u, (wino4_weight_floats(cout, cin) + cin) * sizeof(float)) != hipSuccess)
     return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4: allocation failed");
-  hipError_t e = launch_wino4_weights(w, u, cout, cin, s);
+  pre_t = u + wino4_weight_floats(cout, cin);
+  hipError_t e = hipMemcpy(pre_t, t.data(), cin * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_wino4_weights(w, pre_scale, u, cout, cin, s);
   if (e == hipSuccess) {
     Wino4Params p{};
     p.x = x;
     p.u = u;
     p.y = y;
-    p.pre_scale = pre_scale;
-    p.pre_shift = pre_shift;
+    p.pre_t = pre_scale ? pre_t : nullptr;
     p.post_scale = post_scale;
     p.post_shift = post_shift;
     p.prelu = prelu;

@@ -26,7 +26,8 @@ struct ConvW {
   float* post_shift = nullptr;
   float* prelu = nullptr;
   float* wino = nullptr;  // Winograd-transformed filters (stride-1 3x3 only), or null
-  float* wino4 = nullptr; // F(4x4,3x3) transformed filters G g G^T (built on demand), or null
+  float* wino4 = nullptr; // F(4x4,3x3) transformed filters G (g * pre_scale) G^T (built on demand), or null
+  float* wino4_t = nullptr;  // F(4x4) folded pre-BN: pre_shift / pre_scale per input channel
   int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
 };
 

@@ -105,6 +105,16 @@ def test_winograd4_split_k_small_grids(B, H, cin, cout, epi):
     assert torch.equal(again, outs[1]), "split-K result is not run-to-run deterministic"
 
 
+@pytest.mark.parametrize("B,H,W", [(5, 8, 14), (3, 12, 5), (6, 16, 10)])
+def test_winograd4_pre_bn_partial_canvas_row(B, H, W):
+    """Folded pre-BN (U from w * scale, shift / scale added at in-image pixels) on canvases
+    whose last row of images is partial and whose image rows have no separator of their own
+    (4 | H, W needs one): launch_wino4 adds the separator row so the absent images' pixels stay
+    out of every stored output's window."""
+    got, ref = _wino_case(B, H, 32, 48, 1, seed=910 + B + H + W, W=W, m=4)
+    _close(got, ref, rel=REL[4])
+
+
 def test_winograd4_small_cin():
     """Cin = 32: one transform-pass channel group, two 16-channel K-steps."""
     got, ref = _wino_case(2, 12, 32, 32, 1, seed=420, m=4)

@@ -7,7 +7,9 @@
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-template <bool DO_MFMA, bool DO_VALU>
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <bool DO_MFMA, bool DO_VALU, bool PK = false>
 __global__ __launch_bounds__(512, 1) void k(float* out, int n_mfma, int n_valu, float s) {
   const int wid = threadIdx.x >> 6;
   if (wid < 4) {
@@ -24,28 +26,43 @@ __global__ __launch_bounds__(512, 1) void k(float* out, int n_mfma, int n_valu, 
     if (r.x == 1234.5f) out[threadIdx.x] = r.y;
   } else {
     if (!DO_VALU) return;
-    float v[8];
+    if constexpr (PK) {  // the same flops as n_valu scalar fmas, 2 per v_pk_fma_f32
+      f2 v[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = s * (threadIdx.x + j);
-    for (int i = 0; i < n_valu; i += 8) {
+      for (int j = 0; j < 4; ++j) v[j] = f2{s * (threadIdx.x + j), s + j};
+      const f2 m = {s, s}, c = {0.5f, 0.5f};
+      for (int i = 0; i < n_valu; i += 8) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = __builtin_fmaf(v[j], s, 0.5f);
+        for (int j = 0; j < 4; ++j) v[j] = __builtin_elementwise_fma(v[j], m, c);
+      }
+      float r = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r += v[j].x + v[j].y;
+      if (r == 1234.5f) out[threadIdx.x] = r;
+    } else {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = s * (threadIdx.x + j);
+      for (int i = 0; i < n_valu; i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = __builtin_fmaf(v[j], s, 0.5f);
+      }
+      float r = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r += v[j];
+      if (r == 1234.5f) out[threadIdx.x] = r;
     }
-    float r = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r += v[j];
-    if (r == 1234.5f) out[threadIdx.x] = r;
   }
 }
 
-template <bool A, bool B>
+template <bool A, bool B, bool PK = false>
 float run(float* out, int nm, int nv) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  hipLaunchKernelGGL((k<A, B>), dim3(256), dim3(512), 0, 0, out, nm, nv, 1.0001f);
+  hipLaunchKernelGGL((k<A, B, PK>), dim3(256), dim3(512), 0, 0, out, nm, nv, 1.0001f);
   hipEventRecord(e0);
-  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((k<A, B>), dim3(256), dim3(512), 0, 0, out, nm, nv, 1.0001f);
+  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((k<A, B, PK>), dim3(256), dim3(512), 0, 0, out, nm, nv, 1.0001f);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
@@ -60,6 +77,8 @@ int main() {
   for (int nv : {2048, 8192, 16384, 32768}) {
     const float tm = run<true, false>(out, nm, nv), tv = run<false, true>(out, nm, nv), tb = run<true, true>(out, nm, nv);
     printf("mfma %d/wave: %.1f us | valu %d fma/wave: %.1f us | both: %.1f us (sum %.1f)\n", nm, tm, nv, tv, tb, tm + tv);
+    const float pv = run<false, true, true>(out, nm, nv), pb = run<true, true, true>(out, nm, nv);
+    printf("   packed: valu %d fma-equivalents/wave: %.1f us | both: %.1f us (sum %.1f)\n", nv, pv, pb, tm + pv);
   }
   return 0;
 }

@@ -51,14 +51,13 @@ int main(int argc, char** argv) {
   float *u = nullptr, *y = nullptr;
   CK(hipMalloc((void**)&u, wino4_weight_floats(Cout, Cin) * sizeof(float)));
   CK(hipMalloc((void**)&y, ny * sizeof(float)));
-  CK(launch_wino4_weights(w, u, Cout, Cin, nullptr));
+  const bool pre = epi == 1;
+  CK(launch_wino4_weights(w, pre ? psc : nullptr, u, Cout, Cin, nullptr));
   Wino4Params p{};
   p.x = x;
   p.u = u;
   p.y = y;
-  const bool pre = epi == 1;
-  p.pre_scale = pre ? psc : nullptr;
-  p.pre_shift = pre ? psh : nullptr;
+  p.pre_t = pre ? psh : nullptr;  // any per-channel t: the timing does not depend on its values
   p.post_scale = qsc;
   p.post_shift = qsh;
   p.prelu = al;

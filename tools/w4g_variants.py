@@ -31,13 +31,15 @@ def nouload(s):
     return s.replace(ULOAD, "")
 
 
-TRANS_TURN = """      store(pa, sc_a, sh_a, mask_a, b + 2);"""
-TRANS_TURN2 = """      store(pb, sc_b, sh_b, mask_b, b + 3);"""
+TRANS_TURNS = ["      store(pa, sc_a, sh_a, mask_a, b + 2);", "      store(pb, sc_b, sh_b, mask_b, b + 3);",
+               "      store(pc, sc_c, sh_c, mask_c, b + 4);"]
 
 
 def notrans(s):
-    assert TRANS_TURN in s and TRANS_TURN2 in s
-    return s.replace(TRANS_TURN, "").replace(TRANS_TURN2, "")
+    for t in TRANS_TURNS:
+        assert t in s
+        s = s.replace(t, "")
+    return s
 
 
 def noepi(s):
@@ -53,7 +55,7 @@ VARIANTS = {
     "noepi": noepi,
     "notrans": notrans,
     "noload": lambda s: s.replace("""          d[a][b] = __uint_as_float(
-              __builtin_amdgcn_raw_buffer_load_b32(r, (int)((unsigned)roff[a] + (unsigned)coff[b]), soff, 0));""", "          d[a][b] = __int_as_float(roff[a] + coff[b] + soff);"),
+              __builtin_amdgcn_raw_buffer_load_b32(r, poff[a][b], soff, 0));""", "          d[a][b] = __int_as_float(poff[a][b] + soff);"),
     "nomfma": lambda s: s.replace(MFMA8, "        acc[x][0] += a0.x * u0.x + a1.w * u1.w;\n"),
     "nouload": nouload,
     "mfmaonly": lambda s: nouload(notrans(noepi(s))),
