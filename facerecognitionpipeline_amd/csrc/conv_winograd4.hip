@@ -53,6 +53,7 @@
 // accumulator of lane (tile l&15, row group l>>4) holds 4 consecutive couts of one tile.
 //   U: [36 xi][Cout/16][Cin/16][64 lane = 16 k + cout][4]
 #include <algorithm>
+#include <cmath>
 
 #include "frhip_kernels.h"
 
@@ -164,8 +165,14 @@ __device__ __forceinline__ Item item_of(const Wino4Params& p, int t) {
   return it;
 }
 
-template <bool PRE, int EPI, bool SPLIT>
+// MODE: 0 = whole items round-robin over the persistent grid; 1 = split-K (small grids: every
+// item's K loop cut into ksplit parts, raw partial outputs + wino4_split_reduce_kernel);
+// 2 = stream-K (large grids whose items do not fill whole rounds: the item-step space is cut
+// into equal contiguous ranges, one per workgroup; an item cut at a range boundary leaves two raw
+// partial outputs in a compact slab, summed by wino4_sk_fixup_kernel).
+template <bool PRE, int EPI, int MODE>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
+  constexpr bool SPLIT = MODE == 1, SK = MODE == 2;
   __shared__ __attribute__((aligned(16))) float ring[NBUF * VSTEP + 4 * FT * 8];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -173,13 +180,23 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   const int KST = Cin / KC;                       // K-steps of the whole reduction
   const int KS = SPLIT ? p.ks_per : KST;          // stream steps per item
   const int nitems = p.mblocks * p.nblocks * p.ksplit;
-  // this workgroup's items: blockIdx.x, blockIdx.x + gridDim.x, ... of the XCD-remapped order
+  // MODE 0/1: this workgroup's items are blockIdx.x, blockIdx.x + gridDim.x, ... of the
+  // XCD-remapped order (item_at(j), j local).  SK: it owns item-steps [u_lo, u_hi) of the
+  // nT * KST space (its logical index XCD-remapped, so an XCD's workgroups hold one contiguous
+  // run of items); item_at(t) then takes the global item index t.
   const int nloc = (nitems - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  auto item_at = [&](int j) { return item_of(p, xcd_remap(blockIdx.x + j * gridDim.x, nitems)); };
+  const int nT = p.mblocks * p.nblocks;
+  const int bl = SK ? xcd_remap(blockIdx.x, gridDim.x) : 0;
+  const int u_lo = SK ? (int)((long long)bl * nT * KST / gridDim.x) : 0;
+  const int u_hi = SK ? (int)((long long)(bl + 1) * nT * KST / gridDim.x) : 0;
+  const int t_first = u_lo / KST, t_last = SK ? (u_hi - 1) / KST : nloc - 1;
+  auto item_at = [&](int j) {
+    return SK ? item_of(p, j) : item_of(p, xcd_remap(blockIdx.x + j * gridDim.x, nitems));
+  };
   // K-steps item `it` really has (split-K: the last split may be short; its stream is padded
   // with steps whose patches load as zeros, so every item is KS stream steps long)
   auto steps_of = [&](const Item& it) { return SPLIT ? min(KS, KST - it.split * KS) : KST; };
-  const int G = nloc * KS;  // K-steps in this workgroup's stream (one barrier each)
+  const int G = SK ? u_hi - u_lo : nloc * KS;  // K-steps in this workgroup's stream (one barrier each)
 
   int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [4 items][16 tiles][8]
   if (wid >= 4) {
@@ -202,9 +219,10 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     // (a separator row / column lies between; launch_wino4 forces one below every image row
     // when such a canvas row exists), so it may take the shift like an in-image pixel.
     float rowm[6], colm[6];
-    int lj = 0, ls = 0, ks_real = KS, step0 = 0;
+    int lj = SK ? t_first : 0, ls = SK ? u_lo - t_first * KST : 0, ks_real = KS, step0 = 0;
+    bool first = true;
     auto enter_item = [&](int j) {
-      const Item it = item_at(min(j, nloc - 1));
+      const Item it = item_at(min(j, t_last));
       ks_real = steps_of(it);
       step0 = SPLIT ? it.split * KS : 0;
       const int T = it.mb * FT + i;
@@ -234,7 +252,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         }
       // output geometry of the item's tiles, for the MFMA waves' epilogue (not for the
       // stream's overrun: item j - 4's table may still be in use)
-      if (ch == 0 && j < nloc) {
+      if (ch == 0 && j <= t_last) {
         int* gt = geo + ((j & 3) * FT + i) * 8;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -255,7 +273,8 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     Patch pa, pb, pc;
     // issue the patch loads of the next step of the stream (steps are loaded in order)
     auto load = [&](Patch& P) {
-      if (ls == 0) enter_item(lj);
+      if (ls == 0 || (SK && first)) enter_item(lj);
+      first = false;
       // split-K padding step: every load is out of range (num_records 0) and reads zeros, and
       // the BN shift is dropped
       const bool live = !SPLIT || ls < ks_real;
@@ -353,33 +372,37 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   // U fragment of (item, step s, xi): ((xi * NB16 + nb16) * KST + step) KiB + 16 lane; the
   // xi term is a uniform stride, the rest is the item's base + its clamped step
   const int XS = NB16 * KST * 1024;
-  auto ubase = [&](int j) {  // byte offset of (item j, its first step, xi 0)
-    const Item it = item_at(min(j, nloc - 1));
+  auto ubase = [&](int j) {  // byte offset of (item j, step 0 of its K range, xi 0)
+    const Item it = item_at(min(j, t_last));
     return (min(it.nb * 4 + w, NB16 - 1) * KST + (SPLIT ? it.split * KS : 0)) * 1024;
   };
   auto ulast = [&](int j) {  // last real K-step of item j (split-K: the short last split)
-    return SPLIT ? steps_of(item_at(min(j, nloc - 1))) - 1 : KST - 1;
+    return SPLIT ? steps_of(item_at(min(j, t_last))) - 1 : KST - 1;
   };
+  // segments of the stream: MODE 0/1 item j (local) steps [0, KS); SK item j (global) steps
+  // [s0, s1) -- only the first and the last segment of a workgroup's range can be partial
+  int j = SK ? t_first : 0, s_beg = SK ? u_lo - t_first * KST : 0;
   f4 uring[URING];
-  int ub = ubase(0), ul = ulast(0);
+  int ub = ubase(j), ul = ulast(j);
 #pragma unroll
-  for (int r = 0; r < URING; ++r) uring[r] = ld4(ur, lo, r * XS + ub);
+  for (int r = 0; r < URING; ++r) uring[r] = ld4(ur, lo, r * XS + ub + s_beg * 1024);
   const float* vrd = ring + vslot(lane) * 4;
   int g = 0;
-  for (int j = 0; j < nloc; ++j) {
+  for (; SK ? g < G : j < nloc; ++j) {
     const Item it = item_at(j);
+    const int s0 = s_beg, s1 = SK ? min(KST, s0 + (G - g)) : KS;
     const bool live = it.nb * 64 + w * 16 < Cout;  // Cout % 64 != 0: idle quarter of the last block
     const int ub_next = ubase(j + 1);               // the next item's first step (prefetched
                                                     // during this item's last one)
     f4 acc[NXI];
 #pragma unroll
     for (int x = 0; x < NXI; ++x) acc[x] = f4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < KS; ++s, ++g) {
+    for (int s = s0; s < s1; ++s, ++g) {
       lds_barrier();  // barrier g: ring slot g % 4 holds step g
       const float* vb = vrd + (g % NBUF) * VSTEP;
       // U refills: xi + URING of this step, or xi + URING - 36 of the next step (or item)
       const int cur = ub + min(s, ul) * 1024;
-      const int nxt = s + 1 < KS ? ub + min(s + 1, ul) * 1024 : ub_next;
+      const int nxt = s + 1 < s1 ? ub + min(s + 1, ul) * 1024 : ub_next;
       // xi in pairs: the two accumulation chains interleave (a 16x16x4 MFMA's result is not
       // ready for the next one on the same accumulator at issue rate).  A fragments one pair
       // ahead (the LDS reads of pair x + 2 are in flight during pair x's MFMAs); an idle
@@ -416,7 +439,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     }
     ub = ub_next;
     ul = ulast(j + 1);
+    s_beg = 0;
     if (!live) continue;
+    const bool partial = SK && (s0 > 0 || s1 < KST);
     // ---- epilogue (lane-local): U is the A operand, so lane (tile n, row group rg) holds
     // couts 4rg .. 4rg+3 of tile n for every xi; Y = A^T M A per (tile, cout), BN (+PReLU |
     // +residual), one 16-byte store of the 4 couts per output pixel
@@ -441,8 +466,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     // residual rows: row 0 in flight during the output transform, row y + 1 during row y
     f4 rv[2][4];
     if constexpr (RES)
+      if (!partial)
 #pragma unroll
-      for (int x = 0; x < 4; ++x) rv[0][x] = ld4(rr, oo[0][x]);
+        for (int x = 0; x < 4; ++x) rv[0][x] = ld4(rr, oo[0][x]);
     float out[4][4][4];  // [cout r][y][x]
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -461,6 +487,23 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
         for (int y = 0; y < 4; ++y) out[r][y][x] = o[y];
       }
+    }
+    if (SK && partial) {
+      // raw partial outputs of an item cut at range boundary bd (the first part ends at this
+      // workgroup's range end, the second starts at its range start): slab [bd][part][16 tiles]
+      // [16 pixels][64 couts], summed and finished by wino4_sk_fixup_kernel
+      const int bd = s0 == 0 ? bl + 1 : bl, pt = s0 == 0 ? 0 : 1;
+      const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const u32x4 bits = {__float_as_uint(out[0][y][x]), __float_as_uint(out[1][y][x]),
+                              __float_as_uint(out[2][y][x]), __float_as_uint(out[3][y][x])};
+          const int off = (((((bd * 2 + pt) * FT + n) * 16 + y * 4 + x) * FN) + w * 16 + 4 * rg) * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(bits, sr, off, 0, 0);
+        }
+      continue;
     }
     f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f}, al = {0.f, 0.f, 0.f, 0.f};
     if constexpr (!SPLIT) {
@@ -549,6 +592,49 @@ __global__ void wino4_split_reduce_kernel(const float* __restrict__ part, int S,
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
 // B-fragment order wino4_kernel reads: [xi][Cout/16][Cin/16][lane = 16 k + cout%16][m] with
 // cin % 16 = 4k + m.
+// Stream-K finish: for each range boundary bd that cuts an item, y = epilogue(part 0 + part 1)
+// at the item's in-image pixels (the two parts summed in a fixed order: deterministic).
+// Thread = (tile n, pixel, cout quad); grid (FT * 16 * FN / 4 / 256, boundaries).
+template <int EPI>
+__global__ void wino4_sk_fixup_kernel(Wino4Params p, int KST, int P) {
+  const int bd = blockIdx.y + 1;
+  const long long N = (long long)p.mblocks * p.nblocks * KST;
+  const int u = (int)(bd * N / P);
+  if (u % KST == 0) return;
+  const Item it = item_of(p, u / KST);
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = idx >> 8, px = (idx >> 4) & 15, cq = idx & 15;
+  const int cout0 = it.nb * FN + 4 * cq;
+  const int T = it.mb * FT + n;
+  if (n >= FT || cout0 >= p.Cout || T >= p.ntiles) return;
+  const int H = p.H, W = p.W;
+  const int tr = T / p.TWc, tc = T - tr * p.TWc;
+  const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
+  int rs, cs;
+  const int y = canvas_coord(4 * tr + (px >> 2), ir0, p.Pr, H, p.Pr > H, rs);
+  const int x = canvas_coord(4 * tc + (px & 3), ic0, p.Pc, W, p.Pc > W, cs);
+  if (y < 0 || rs * p.NC >= p.B || x < 0 || cs >= p.NC) return;
+  const long long pix = (long long)(rs * p.NC * H + y) * W + (long long)cs * H * W + x;
+  if (pix >= (long long)p.B * H * W) return;
+  const float4* slab = reinterpret_cast<const float4*>(p.part);
+  const long long o0 = ((((long long)bd * 2 + 0) * FT + n) * 16 + px) * (FN / 4) + cq;
+  const long long o1 = ((((long long)bd * 2 + 1) * FT + n) * 16 + px) * (FN / 4) + cq;
+  const float4 a = slab[o0], b = slab[o1];
+  float v[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+  const long long yo = pix * p.Cout + cout0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float t = v[r] * p.post_scale[cout0 + r] + p.post_shift[cout0 + r];
+    if constexpr (EPI == EPI_AFFINE_PRELU) t = t > 0.f ? t : t * p.prelu[cout0 + r];
+    if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) {
+      t += p.res[yo + r];
+      if constexpr (EPI == EPI_AFFINE_RES_PRELU) t = t > 0.f ? t : t * p.prelu[cout0 + r];
+    }
+    v[r] = t;
+  }
+  *reinterpret_cast<float4*>(p.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __restrict__ pre_scale,
                                     float* __restrict__ u, int Cout, int Cin) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -642,7 +728,7 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
                          reinterpret_cast<uintptr_t>(p.part)) & 15) == 0;
   int S = 1;
   p.ks_per = KST;
-  if (p.part && aligned && nT <= 128 && KST > 1) {
+  if (p.part && !p.no_split && aligned && nT <= 128 && KST > 1) {
     S = std::min(KST, 256 / nT);
     S = (int)std::min<long long>(S, std::min<long long>(p.part_floats, (1ll << 29) - 1) / elems);
     if (S > 1) {
@@ -660,14 +746,26 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  const dim3 grid(std::min(nitems, cus)), block(512);
+  // stream-K when whole items would leave a last round at least 10% empty (IR-101 at B=256:
+  // stage 3 900 items = 3.52 rounds of 256, stage 2 6.13); each workgroup then runs an equal
+  // share of the item-steps and cut items are finished by wino4_sk_fixup_kernel
   const bool split = p.ksplit > 1;
+  const double rounds = (double)nT / cus;
+  const bool sk = !split && p.sk_mode && p.part && aligned && nT > cus && cus % 8 == 0 &&
+                  std::ceil(rounds) - rounds > 0.1 &&
+                  (long long)(cus + 1) * 2 * FT * 16 * FN <= p.part_floats;
+  const dim3 grid(sk ? cus : std::min(nitems, cus)), block(512);
 #define FR_W4_CASE(PRE_, EPI_)                                                                            \
   if (pre == PRE_ && epi == EPI_) {                                                                       \
     if (split)                                                                                            \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, true>), grid, block, 0, s, p);                         \
+      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, 1>), grid, block, 0, s, p);                            \
+    else if (sk)                                                                                          \
+      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, 2>), grid, block, 0, s, p);                            \
     else                                                                                                  \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, false>), grid, block, 0, s, p);                        \
+      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, 0>), grid, block, 0, s, p);                            \
+    if (sk)                                                                                               \
+      hipLaunchKernelGGL((wino4_sk_fixup_kernel<EPI_>), dim3(FT * 16 * FN / 4 / 256, cus - 1), dim3(256),  \
+                         0, s, p, KST, cus);                                                              \
     if (split) {                                                                                          \
       const long long n4 = elems / 4;                                                                     \
       hipLaunchKernelGGL((wino4_split_reduce_kernel<EPI_>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), \

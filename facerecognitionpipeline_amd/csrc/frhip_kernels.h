@@ -118,6 +118,10 @@ struct Wino4Params {
   long long part_floats;
   int ksplit, ks_per;      // set by launch_wino4
   long long part_stride;   // set by launch_wino4
+  // 1: stream-K over the item-steps when whole items leave the last round >= 10% empty (uses
+  // part for the cut items' two raw partials); 0: whole items only
+  int sk_mode;
+  int no_split;  // 1: never split-K (tests compare the two schedules)
 };
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16
 size_t wino4_weight_floats(int Cout, int Cin);

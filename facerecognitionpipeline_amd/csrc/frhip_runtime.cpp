@@ -263,6 +263,9 @@ struct ProfScope {
   }
 };
 
+// F(4x4) stream-K schedule for large layers (frt_set_wino4_streamk: A/B and tests)
+static int g_wino4_streamk = 1;
+
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s) {
   ConvParams p{};
@@ -328,6 +331,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.Cout = cw.cout;
     wp.part = h->w4part;
     wp.part_floats = h->w4part ? fr_handle::W4PART_FLOATS : 0;
+    wp.sk_mode = g_wino4_streamk;
     Wino4Params cv = wp;
     wino4_canvas(cv);
     // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
@@ -1485,6 +1489,10 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 }
 
 static int g_frt_wino4_split = 1;
+int frt_set_wino4_streamk(int on) {
+  g_wino4_streamk = on != 0;
+  return FR_OK;
+}
 int frt_set_wino4_split(int on) {
   g_frt_wino4_split = on != 0;
   return FR_OK;
@@ -1526,8 +1534,11 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.W = W;
     p.Cin = cin;
     p.Cout = cout;
-    if (g_frt_wino4_split) {  // split-K workspace: small grids take the split path
-      p.part_floats = (long long)B * H * W * cout * std::min(cin / 16, 16);
+    p.sk_mode = g_wino4_streamk;
+    p.no_split = !g_frt_wino4_split;
+    if (g_frt_wino4_split || g_wino4_streamk) {  // split-K / stream-K partial workspace
+      p.part_floats = g_frt_wino4_split ? (long long)B * H * W * cout * std::min(cin / 16, 16) : 0;
+      if (g_wino4_streamk) p.part_floats = std::max<long long>(p.part_floats, 257ll * 2 * 16 * 16 * 64);
       if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;
       p.part = part;
     }

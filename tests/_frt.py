@@ -20,6 +20,8 @@ def lib():
         L.frt_conv2d_winograd4.argtypes = [_P, _P, _P] + [_I] * 5 + [_P] * 6 + [_I, _P]
         L.frt_set_wino4_split.restype = _I
         L.frt_set_wino4_split.argtypes = [_I]
+        L.frt_set_wino4_streamk.restype = _I
+        L.frt_set_wino4_streamk.argtypes = [_I]
         L.frt_stem.restype = _I
         L.frt_stem.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P, _P]
         L.frt_topk.restype = _I

@@ -115,6 +115,31 @@ def test_winograd4_pre_bn_partial_canvas_row(B, H, W):
     _close(got, ref, rel=REL[4])
 
 
+@pytest.mark.parametrize("B,H,cin,cout", [
+    (128, 14, 256, 256),  # 456 items = 1.78 rounds of 256 workgroups
+    (96, 28, 64, 128),    # Cin = 64: 4 K-steps per item, ranges span several items
+    (160, 7, 512, 512),   # 40 * 8 = 320 items, 32 K-steps each
+])
+@pytest.mark.parametrize("epi", [1, 2])
+def test_winograd4_stream_k(B, H, cin, cout, epi):
+    """Large grids whose items leave the last round part-empty run stream-K: equal item-step
+    ranges per workgroup, cut items finished from two raw partials by wino4_sk_fixup_kernel.
+    Matches the CPU conv, the whole-item schedule to the same bar, and is deterministic."""
+    L = _frt.lib()
+    outs = {}
+    try:
+        for mode in (1, 0):
+            L.frt_set_wino4_streamk(mode)
+            got, ref = _wino_case(B, H, cin, cout, epi, seed=1300 + H + cin + epi, m=4)
+            _close(got, ref, rel=REL[4])
+            outs[mode] = got
+    finally:
+        L.frt_set_wino4_streamk(1)
+    _close(outs[1], outs[0], rel=REL[4])
+    again, _ = _wino_case(B, H, cin, cout, epi, seed=1300 + H + cin + epi, m=4)
+    assert torch.equal(again, outs[1]), "stream-K result is not run-to-run deterministic"
+
+
 def test_winograd4_small_cin():
     """Cin = 32: one transform-pass channel group, two 16-channel K-steps."""
     got, ref = _wino_case(2, 12, 32, 32, 1, seed=420, m=4)

@@ -62,6 +62,13 @@ int main(int argc, char** argv) {
   p.post_shift = qsh;
   p.prelu = al;
   p.res = epi == 2 ? res : nullptr;
+  // stream-K (argv[7] = 1, default) needs the partial workspace
+  float* part = nullptr;
+  const long long part_floats = 257ll * 2 * 16 * 16 * 64;
+  CK(hipMalloc((void**)&part, part_floats * sizeof(float)));
+  p.part = part;
+  p.part_floats = part_floats;
+  p.sk_mode = argc > 7 ? atoi(argv[7]) : 1;
   p.B = B;
   p.H = H;
   p.W = H;

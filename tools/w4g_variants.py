@@ -86,12 +86,13 @@ def main():
             print(list(ex.map(build, names)))
     else:
         for n in names:
-            for shp in SHAPES:
-                r = subprocess.run(["timeout", "-k", "5", "60", os.path.join(OUT, f"w4g_{n}")] + [str(x) for x in shp] + ["20"],
-                                   capture_output=True, text=True)
-                print(f"{n:9s} {r.stdout.strip()} {r.stderr.strip()[-200:]}", flush=True)
-                if r.returncode:
-                    return r.returncode
+            for sk in ((1, 0) if n == "base" else (1,)):  # base: stream-K on and off
+                for shp in SHAPES:
+                    r = subprocess.run(["timeout", "-k", "5", "60", os.path.join(OUT, f"w4g_{n}")] +
+                                       [str(x) for x in shp] + ["20", str(sk)], capture_output=True, text=True)
+                    print(f"{n + ('' if sk else '/nosk'):12s} {r.stdout.strip()} {r.stderr.strip()[-200:]}", flush=True)
+                    if r.returncode:
+                        return r.returncode
     return 0
 
 
