@@ -28,7 +28,7 @@ hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, in
 
 int conv_tile_bm(ConvTile t) {
   switch (t) {
-    case TILE_256x64: case TILE_256x128: case TILE_256x128_W8: return 256;
+    case TILE_256x64: case TILE_256x128: case TILE_256x128_W8: case TILE_256x64_W8: return 256;
     case TILE_64x128: case TILE_64x256_W8: return 64;
     default: return 128;
   }
@@ -36,7 +36,7 @@ int conv_tile_bm(ConvTile t) {
 
 int conv_tile_bn(ConvTile t) {
   switch (t) {
-    case TILE_256x64: case TILE_128x64: case TILE_128x64_W8: return 64;
+    case TILE_256x64: case TILE_128x64: case TILE_128x64_W8: case TILE_256x64_W8: return 64;
     case TILE_128x256: case TILE_64x256_W8: return 256;
     default: return 128;
   }

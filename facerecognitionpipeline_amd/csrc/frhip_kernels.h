@@ -58,7 +58,8 @@ enum ConvTile : int {
   TILE_256x128_W8 = 7,
   TILE_128x64_W8 = 8,
   TILE_64x256_W8 = 9,
-  TILE_COUNT = 10
+  TILE_256x64_W8 = 10,
+  TILE_COUNT = 11
 };
 
 // Arithmetic of the conv GEMM: exact-f32 MFMA (default, the parity path) or the opt-in

@@ -17,7 +17,7 @@ from facerecognitionpipeline_amd.arch import block_specs  # noqa: E402
 from tests import _frt  # noqa: E402
 
 TILES = {0: "256x64", 1: "128x128", 2: "128x64", 3: "64x128", 4: "256x128", 5: "128x256", 6: "128x128w8",
-         7: "256x128w8", 8: "128x64w8", 9: "64x256w8"}
+         7: "256x128w8", 8: "128x64w8", 9: "64x256w8", 10: "256x64w8"}
 
 
 def shapes(arch):
