@@ -61,7 +61,9 @@ namespace frhip {
 namespace {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int NXI = 36;              // transform elements
 constexpr int FT = 16;               // 4x4 output tiles per item (MFMA M)
@@ -136,6 +138,19 @@ __device__ __forceinline__ void bt6(const float (&d)[6], float (&t)[6]) {
   t[5] = __builtin_fmaf(-4.f, u, d[5] - d[3]);
 }
 
+// the same on two channels (packed f32)
+__device__ __forceinline__ void bt6v(const f2 (&d)[6], f2 (&t)[6]) {
+  const f2 c4 = {4.f, 4.f}, m4 = {-4.f, -4.f}, c2 = {2.f, 2.f}, m2 = {-2.f, -2.f};
+  const f2 r = d[4] - d[2], u = d[3] - d[1];
+  const f2 pp = __builtin_elementwise_fma(m4, d[2], d[4]), q = __builtin_elementwise_fma(m4, d[1], d[3]);
+  t[0] = __builtin_elementwise_fma(c4, d[0] - d[2], r);
+  t[1] = pp + q;
+  t[2] = pp - q;
+  t[3] = __builtin_elementwise_fma(c2, u, r);
+  t[4] = __builtin_elementwise_fma(m2, u, r);
+  t[5] = __builtin_elementwise_fma(m4, u, d[5] - d[3]);
+}
+
 // 1-D output transform A^T m (6 -> 4)
 __device__ __forceinline__ void at6(const float (&m)[6], float (&o)[4]) {
   const float p12 = m[1] + m[2], m12 = m[1] - m[2];
@@ -144,6 +159,17 @@ __device__ __forceinline__ void at6(const float (&m)[6], float (&o)[4]) {
   o[1] = m12 + 2.f * m34;
   o[2] = p12 + 4.f * p34;
   o[3] = m12 + 8.f * m34 + m[5];
+}
+
+// the same on two couts (packed f32)
+__device__ __forceinline__ void at6v(const f2 (&m)[6], f2 (&o)[4]) {
+  const f2 c2 = {2.f, 2.f}, c4 = {4.f, 4.f}, c8 = {8.f, 8.f};
+  const f2 p12 = m[1] + m[2], m12 = m[1] - m[2];
+  const f2 p34 = m[3] + m[4], m34 = m[3] - m[4];
+  o[0] = m[0] + p12 + p34;
+  o[1] = __builtin_elementwise_fma(c2, m34, m12);
+  o[2] = __builtin_elementwise_fma(c4, p34, p12);
+  o[3] = __builtin_elementwise_fma(c8, m34, m12 + m[5]);
 }
 
 // item index -> (tile block mb, cout block nb, K split): one XCD's contiguous run of items
@@ -201,24 +227,30 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [4 items][16 tiles][8]
   if (wid >= 4) {
     // ---- transform waves: every K-step, wave t transforms tiles 4t .. 4t+3 of the item for
-    // the step's 16 channels: lane (ii, ch) = channel ch of tile 4t + ii, one 6x6 patch per
-    // lane (a patch row's loads cover 4 runs of 64 contiguous bytes).  Step g + 2 is written
-    // during the period between barriers g and g + 1 (its ring slot last held step g - 2, read
-    // before barrier g - 1); its patch loads were issued one period earlier, so they have a
-    // whole MFMA step to land.
+    // the step's 16 channels in packed f32, two channels per lane and half a patch per lane:
+    // lane (half h, tile 4t + ii, channel pair pr) loads patch columns 3h .. 3h+2 of channels
+    // 2pr, 2pr+1 (18 8-byte loads; a wave's load covers 8 runs of 64 contiguous bytes), adds
+    // the folded pre-BN shift, applies B^T down its 3 columns, trades 9 values with its partner
+    // lane (v_permlane32_swap: half 0 keeps patch rows 0-2, half 1 rows 3-5), applies B^T
+    // along its 3 rows and writes them (18 ds_write_b64).  Step g + 2 is written during the
+    // period between barriers g and g + 1 (its ring slot last held step g - 2, read before
+    // barrier g - 1); its patch loads were issued two periods earlier.
     const int t = wid - 4;
-    const int ch = lane & 15, i = 4 * t + (lane >> 4);
+    const int half = lane >> 5, ii = (lane >> 3) & 3, pr = lane & 7;
+    const int i = 4 * t + ii, ch = 2 * pr;
     const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
     const __amdgpu_buffer_rsrc_t xr_none = uniform_rsrc(p.x, 0);
     const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
     // the item's patch geometry, recomputed when the load stream enters a new item: byte
-    // offset of every patch pixel (channel ch of step 0; BIGOFF sums for padding)
-    int poff[6][6];
-    // PRE: in-image masks of the patch rows / columns (1 or 0).  Separable: a patch pixel of an
-    // image past B (partial last canvas row) is never inside the 3x3 window of a stored output
-    // (a separator row / column lies between; launch_wino4 forces one below every image row
-    // when such a canvas row exists), so it may take the shift like an in-image pixel.
-    float rowm[6], colm[6];
+    // offset of every patch pixel of the lane's 3 columns (channel ch of step 0; BIGOFF sums
+    // for padding)
+    int poff[6][3];
+    // PRE: in-image masks of the patch rows / the lane's columns (1 or 0).  Separable: a patch
+    // pixel of an image past B (partial last canvas row) is never inside the 3x3 window of a
+    // stored output (a separator row / column lies between; launch_wino4 forces one below
+    // every image row when such a canvas row exists), so it may take the shift like an
+    // in-image pixel.
+    float rowm[6], colm[3];
     int lj = SK ? t_first : 0, ls = SK ? u_lo - t_first * KST : 0, ks_real = KS, step0 = 0;
     bool first = true;
     auto enter_item = [&](int j) {
@@ -228,31 +260,35 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       const int T = it.mb * FT + i;
       const int tr = T / p.TWc, tc = T - tr * p.TWc;
       const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
-      int roff[6], coff[6];
-      bool rin[6], cin[6];
+      int roff[6], coff[3];
+      bool rin[6], cin[3];
 #pragma unroll
       for (int e = 0; e < 6; ++e) {
-        int rs, cs;
+        int rs;
         const int y = canvas_coord(4 * tr - 1 + e, ir0, p.Pr, H, sep_r, rs);
-        const int x = canvas_coord(4 * tc - 1 + e, ic0, p.Pc, W, sep_c, cs);
         rin[e] = y >= 0 && rs * p.NC < p.B && T < p.ntiles;
-        cin[e] = x >= 0 && cs < p.NC;
         roff[e] = rin[e] ? (rs * p.NC * H + y) * W * Cin * 4 : BIGOFF;
+      }
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        int cs;
+        const int x = canvas_coord(4 * tc - 1 + 3 * half + e, ic0, p.Pc, W, sep_c, cs);
+        cin[e] = x >= 0 && cs < p.NC;
         coff[e] = cin[e] ? ((cs * H * W + x) * Cin + ch) * 4 : BIGOFF;
       }
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
-        for (int b = 0; b < 6; ++b) poff[a][b] = (int)((unsigned)roff[a] + (unsigned)coff[b]);
-      if constexpr (PRE)
+        for (int b = 0; b < 3; ++b) poff[a][b] = (int)((unsigned)roff[a] + (unsigned)coff[b]);
+      if constexpr (PRE) {
 #pragma unroll
-        for (int e = 0; e < 6; ++e) {
-          rowm[e] = rin[e] ? 1.f : 0.f;
-          colm[e] = cin[e] ? 1.f : 0.f;
-        }
+        for (int e = 0; e < 6; ++e) rowm[e] = rin[e] ? 1.f : 0.f;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) colm[e] = cin[e] ? 1.f : 0.f;
+      }
       // output geometry of the item's tiles, for the MFMA waves' epilogue (not for the
       // stream's overrun: item j - 4's table may still be in use)
-      if (ch == 0 && j <= t_last) {
+      if (half == 0 && pr == 0 && j <= t_last) {
         int* gt = geo + ((j & 3) * FT + i) * 8;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -264,11 +300,12 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         }
       }
     };
-    // a patch buffer: the 6x6 values and, for PRE, the folded shift t = shift / scale of its
-    // channel at its item's in-image rows (trow) and columns (colm)
+    // a patch buffer: the lane's 6x3 values (2 channels each) and, for PRE, the folded shift
+    // t = shift / scale of its channels at its item's in-image rows (trow) and columns (colm)
     struct Patch {
-      float d[6][6];
-      float trow[6], colm[6];
+      f2 d[6][3];
+      f2 trow[6];
+      float colm[3];
     };
     Patch pa, pb, pc;
     // issue the patch loads of the next step of the stream (steps are loaded in order)
@@ -277,57 +314,75 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       first = false;
       // split-K padding step: every load is out of range (num_records 0) and reads zeros, and
       // the BN shift is dropped
-      const bool live = !SPLIT || ls < ks_real;
+      // (readfirstlane: the stream counters are wave-uniform, but the compiler loses track of
+      // that through the unrolled loop's phis and would wrap every load in a waterfall loop)
+      const bool live = !SPLIT || __builtin_amdgcn_readfirstlane(ls < ks_real ? 1 : 0);
       const __amdgpu_buffer_rsrc_t r = live ? xr : xr_none;
-      const int step = step0 + min(ls, ks_real - 1);
+      const int step = __builtin_amdgcn_readfirstlane(step0 + min(ls, ks_real - 1));
       const int soff = step * KC * 4;
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
-        for (int b = 0; b < 6; ++b)
-          P.d[a][b] = __uint_as_float(
-              __builtin_amdgcn_raw_buffer_load_b32(r, poff[a][b], soff, 0));
-      if constexpr (PRE) {
-        const float t = live ? p.pre_t[step * KC + ch] : 0.f;
-#pragma unroll
-        for (int e = 0; e < 6; ++e) {
-          P.trow[e] = t * rowm[e];
-          P.colm[e] = colm[e];
+        for (int b = 0; b < 3; ++b) {
+          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);
+          P.d[a][b] = f2{__uint_as_float(v.x), __uint_as_float(v.y)};
         }
+      if constexpr (PRE) {
+        const f2 tt = live ? *reinterpret_cast<const f2*>(p.pre_t + step * KC + ch) : f2{0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 6; ++e) P.trow[e] = tt * rowm[e];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) P.colm[e] = colm[e];
       }
       if (++ls == KS) {
         ls = 0;
         ++lj;
       }
     };
+    // the ring address of (tile i, channels ch, ch+1): A-fragment slot lane 16 k + i
+    // (k = ch / 4), elements ch % 4 .. +1, at 16-byte slot vslot(16 k + i); half h writes the
+    // transform rows 3h .. 3h+2, i.e. xi from 18 h
+    const int dst_off = vslot(16 * (ch >> 2) + i) * 4 + (ch & 3) + half * 18 * 256;
     // transform a loaded patch and write it into ring slot g % NBUF
     auto store = [&](Patch& P, int g) {
-      float (&d)[6][6] = P.d;
+      f2 (&d)[6][3] = P.d;
       if constexpr (PRE)
         // BN(x) = scale (x + t) with the scale folded into U: add t at in-image pixels only,
         // the conv's zero padding and the canvas separators stay 0 (BN -> zero-padded Conv2d)
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
-          for (int b = 0; b < 6; ++b) d[a][b] = __builtin_fmaf(P.trow[a], P.colm[b], d[a][b]);
+          for (int b = 0; b < 3; ++b) d[a][b] = __builtin_elementwise_fma(P.trow[a], f2{P.colm[b], P.colm[b]}, d[a][b]);
 #pragma unroll
-      for (int b = 0; b < 6; ++b) {  // columns: d[.][b] <- (B^T d)[.][b]
-        float c[6], o[6];
+      for (int b = 0; b < 3; ++b) {  // the lane's columns: d[.][b] <- (B^T d)[.][b]
+        f2 c[6], o[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) c[a] = d[a][b];
-        bt6(c, o);
+        bt6v(c, o);
 #pragma unroll
         for (int a = 0; a < 6; ++a) d[a][b] = o[a];
       }
-      // A-fragment slot of (tile i, channel ch): lane 16 k + i (k = ch / 4), element ch % 4,
-      // stored at 16-byte slot 16 k + (i ^ 4k) (vslot) so a wave's 64 stores hit 64 banks
-      float* dst = ring + (g % NBUF) * VSTEP + vslot(16 * (ch >> 2) + i) * 4 + (ch & 3);
+      // partner exchange: swap(upper half of d[k][b], lower half of d[3+k][b]) leaves, in both
+      // halves, transform row 3h + k with column b in d[k][b] and column 3 + b in d[3+k][b]
 #pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        float v[6];
-        bt6(d[a], v);
+      for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int b = 0; b < 6; ++b) dst[(6 * a + b) * 256] = v[b];
+        for (int b = 0; b < 3; ++b)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(d[k][b][e]),
+                                                            __float_as_uint(d[3 + k][b][e]), false, false);
+            d[k][b][e] = __uint_as_float(r[0]);
+            d[3 + k][b][e] = __uint_as_float(r[1]);
+          }
+      float* dst = ring + (g % NBUF) * VSTEP + dst_off;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const f2 row[6] = {d[k][0], d[k][1], d[k][2], d[3 + k][0], d[3 + k][1], d[3 + k][2]};
+        f2 v[6];
+        bt6v(row, v);
+#pragma unroll
+        for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(dst + (6 * k + b) * 256) = v[b];
       }
     };
     // prologue: steps 0 and 1 written before the first barrier, steps 2 and 3 in flight (the
@@ -361,6 +416,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       store(pc, b + 4);
       if (b + 3 >= G) break;
     }
+    lds_barrier();  // barrier G: the MFMA waves close their last K-step with it
     return;
   }
 
@@ -387,6 +443,10 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
   for (int r = 0; r < URING; ++r) uring[r] = ld4(ur, lo, r * XS + ub + s_beg * 1024);
   const float* vrd = ring + vslot(lane) * 4;
+  // A fragments (V) of the next xi pair, carried across K-steps: step g + 1's slot was written
+  // before barrier g, so its first pair is read during step g's last MFMAs
+  lds_barrier();  // barrier 0: steps 0 and 1 are in the ring
+  f4 a0n = *reinterpret_cast<const f4*>(vrd), a1n = *reinterpret_cast<const f4*>(vrd + 256);
   int g = 0;
   for (; SK ? g < G : j < nloc; ++j) {
     const Item it = item_at(j);
@@ -397,9 +457,11 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     f4 acc[NXI];
 #pragma unroll
     for (int x = 0; x < NXI; ++x) acc[x] = f4{0.f, 0.f, 0.f, 0.f};
-    for (int s = s0; s < s1; ++s, ++g) {
-      lds_barrier();  // barrier g: ring slot g % 4 holds step g
+    auto kstep = [&](int s) {
+      // between barriers g and g + 1: ring slot g % 4 holds step g (barrier g closed the
+      // previous K-step, or is the stream's first)
       const float* vb = vrd + (g % NBUF) * VSTEP;
+      const float* vn = vrd + ((g + 1) % NBUF) * VSTEP;
       // U refills: xi + URING of this step, or xi + URING - 36 of the next step (or item)
       const int cur = ub + min(s, ul) * 1024;
       const int nxt = s + 1 < s1 ? ub + min(s + 1, ul) * 1024 : ub_next;
@@ -407,14 +469,12 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       // ready for the next one on the same accumulator at issue rate).  A fragments one pair
       // ahead (the LDS reads of pair x + 2 are in flight during pair x's MFMAs); an idle
       // quarter (!live) computes on a clamped U block and is never stored.
-      f4 a0n = *reinterpret_cast<const f4*>(vb), a1n = *reinterpret_cast<const f4*>(vb + 256);
 #pragma unroll
       for (int x = 0; x < NXI; x += 2) {
         const f4 a0 = a0n, a1 = a1n;
-        if (x + 2 < NXI) {
-          a0n = *reinterpret_cast<const f4*>(vb + (x + 2) * 256);
-          a1n = *reinterpret_cast<const f4*>(vb + (x + 3) * 256);
-        }
+        const float* nb = x + 2 < NXI ? vb + (x + 2) * 256 : vn;
+        a0n = *reinterpret_cast<const f4*>(nb);
+        a1n = *reinterpret_cast<const f4*>(nb + 256);
         const f4 u0 = uring[x % URING], u1 = uring[(x + 1) % URING];
         acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0.x, a0.x, acc[x], 0, 0, 0);
         acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1.x, a1.x, acc[x + 1], 0, 0, 0);
@@ -431,22 +491,31 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
                                              : ld4(ur, lo, (y + URING - NXI) * XS + nxt);
         }
         // pin the slot's order: LDS reads of the next pair, the 8 MFMAs, the 2 U refills
-        if (x + 2 < NXI) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
         __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
-    }
+      ++g;
+      lds_barrier();  // barrier g + 1
+    };
+    // the item's first K-step is peeled off the loop: it follows the previous item's epilogue
+    // in straight-line code, so the wait for its U fragments counts exactly the epilogue's
+    // stores in between (a merged loop header made the compiler wait for every outstanding
+    // load and store, vmcnt(0), at every K-step)
+    kstep(s0);
+    for (int s = s0 + 1; s < s1; ++s) kstep(s);
     ub = ub_next;
     ul = ulast(j + 1);
     s_beg = 0;
-    if (!live) continue;
+    // an idle quarter (!live, Cout % 64 != 0) runs the epilogue too, with every store dropped
+    // (no branch: a merge here costs the next K-step a full wait for stores)
     const bool partial = SK && (s0 > 0 || s1 < KST);
     // ---- epilogue (lane-local): U is the A operand, so lane (tile n, row group rg) holds
     // couts 4rg .. 4rg+3 of tile n for every xi; Y = A^T M A per (tile, cout), BN (+PReLU |
     // +residual), one 16-byte store of the 4 couts per output pixel
     const int n = lane & 15, rg = lane >> 4;
-    const int cout0 = it.nb * 64 + w * 16 + 4 * rg;
+    const int cout0 = min(it.nb * 64 + w * 16, Cout - 16) + 4 * rg;  // (clamped for an idle quarter)
     const __amdgpu_buffer_rsrc_t yr =
         uniform_rsrc(SPLIT ? p.part + it.split * p.part_stride : p.y, p.B * H * W * Cout * 4);
     constexpr bool RES = !SPLIT && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
@@ -461,33 +530,45 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       for (int x = 0; x < 4; ++x) {
         const int orow = gt[y], ocol = gt[4 + x], pix = orow + ocol;
         const bool ok = orow >= 0 && ocol >= 0 && pix < p.B * H * W;
-        oo[y][x] = ok ? (pix * Cout + cout0) * 4 : BIGOFF;
+        oo[y][x] = ok && live ? (pix * Cout + cout0) * 4 : BIGOFF;
       }
-    // residual rows: row 0 in flight during the output transform, row y + 1 during row y
-    f4 rv[2][4];
-    if constexpr (RES)
-      if (!partial)
+    // residual rows 0-1 in flight during the output transform of couts 2-3, rows 2-3 while rows
+    // 0-1 are stored (issued earlier they would spill beside the 144 accumulators)
+    f4 rv[4][4];
+    auto load_res = [&](int y0) {
+      if constexpr (RES)
+        if (!partial)
 #pragma unroll
-        for (int x = 0; x < 4; ++x) rv[0][x] = ld4(rr, oo[0][x]);
-    float out[4][4][4];  // [cout r][y][x]
+          for (int y = y0; y < y0 + 2; ++y)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float z[6][4];
+            for (int x = 0; x < 4; ++x) rv[y][x] = ld4(rr, oo[y][x]);
+    };
+    // (stream-K carries more live registers: there row y + 1 goes out while row y is stored)
+    f2 outv[2][4][4];  // [cout pair q][y][x]: couts 2q, 2q + 1 (packed f32)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (!SK && q == 1) load_res(0);
+      f2 z[6][4];
 #pragma unroll
       for (int a = 0; a < 6; ++a) {  // rows: A^T along b
-        const float m6[6] = {acc[6 * a][r], acc[6 * a + 1][r], acc[6 * a + 2][r],
-                             acc[6 * a + 3][r], acc[6 * a + 4][r], acc[6 * a + 5][r]};
-        at6(m6, z[a]);
+        f2 m6[6];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) m6[b] = f2{acc[6 * a + b][2 * q], acc[6 * a + b][2 * q + 1]};
+        at6v(m6, z[a]);
       }
 #pragma unroll
       for (int x = 0; x < 4; ++x) {  // columns: A^T along a
-        const float c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
-        float o[4];
-        at6(c6, o);
+        const f2 c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
+        f2 o[4];
+        at6v(c6, o);
 #pragma unroll
-        for (int y = 0; y < 4; ++y) out[r][y][x] = o[y];
+        for (int y = 0; y < 4; ++y) outv[q][y][x] = o[y];
       }
     }
+    if constexpr (!SK) load_res(2);
+    auto out4 = [&](int y, int x) {
+      return f4{outv[0][y][x].x, outv[0][y][x].y, outv[1][y][x].x, outv[1][y][x].y};
+    };
     if (SK && partial) {
       // raw partial outputs of an item cut at range boundary bd (the first part ends at this
       // workgroup's range end, the second starts at its range start): slab [bd][part][16 tiles]
@@ -498,8 +579,8 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       for (int y = 0; y < 4; ++y)
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
-          const u32x4 bits = {__float_as_uint(out[0][y][x]), __float_as_uint(out[1][y][x]),
-                              __float_as_uint(out[2][y][x]), __float_as_uint(out[3][y][x])};
+          const f4 v = out4(y, x);
+          const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
           const int off = (((((bd * 2 + pt) * FT + n) * 16 + y * 4 + x) * FN) + w * 16 + 4 * rg) * 4;
           __builtin_amdgcn_raw_buffer_store_b128(bits, sr, off, 0, 0);
         }
@@ -513,23 +594,27 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     if constexpr (PRELU) al = *reinterpret_cast<const f4*>(p.prelu + cout0);
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
-      if constexpr (RES)
+      if constexpr (SK && RES) {
+        if (y == 0)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) rv[0][x] = ld4(rr, oo[0][x]);
         if (y + 1 < 4)
 #pragma unroll
-          for (int x = 0; x < 4; ++x) rv[(y + 1) & 1][x] = ld4(rr, oo[y + 1][x]);
+          for (int x = 0; x < 4; ++x) rv[y + 1][x] = ld4(rr, oo[y + 1][x]);
+      }
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
-        f4 v = {out[0][y][x], out[1][y][x], out[2][y][x], out[3][y][x]};
+        f4 v = out4(y, x);
         if constexpr (!SPLIT) {
+          v = __builtin_elementwise_fma(v, sc, sh);
+          if constexpr (EPI == EPI_AFFINE_PRELU)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float t = v[r] * sc[r] + sh[r];
-            if constexpr (EPI == EPI_AFFINE_PRELU) t = t > 0.f ? t : t * al[r];
-            if constexpr (RES) {
-              t += rv[y & 1][x][r];
-              if constexpr (EPI == EPI_AFFINE_RES_PRELU) t = t > 0.f ? t : t * al[r];
-            }
-            v[r] = t;
+            for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * al[r];
+          if constexpr (RES) {
+            v += rv[y][x];
+            if constexpr (EPI == EPI_AFFINE_RES_PRELU)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * al[r];
           }
         }
         const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
@@ -746,13 +831,19 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  // stream-K when whole items would leave a last round at least 10% empty (IR-101 at B=256:
-  // stage 3 900 items = 3.52 rounds of 256, stage 2 6.13); each workgroup then runs an equal
-  // share of the item-steps and cut items are finished by wino4_sk_fixup_kernel
+  // stream-K when whole items would leave a last round at least 10% empty; each workgroup then
+  // runs an equal share of the item-steps and cut items are finished by wino4_sk_fixup_kernel.
+  // Whole items keep every workgroup on the same K-step of its item, so an XCD's workgroups
+  // read the same U slice at a time; stream-K ranges start at arbitrary steps and read all of
+  // U at once, which pays only while U fits an XCD's 4 MB L2 (measured, IR-101 B=256: stage 2
+  // 128->128, U 2.4 MB, 258 -> 249 us; stage 3 256->256, U 9.4 MB, 238 -> 324 us).  With fewer
+  // than 8 K-steps per item the two partial epilogues and the fixup outweigh the round
+  // (stage 1 64->64: 297 -> 314 us).
   const bool split = p.ksplit > 1;
   const double rounds = (double)nT / cus;
   const bool sk = !split && p.sk_mode && p.part && aligned && nT > cus && cus % 8 == 0 &&
-                  std::ceil(rounds) - rounds > 0.1 &&
+                  (p.sk_mode == 2 || (KST >= 8 && (long long)NXI * p.Cin * p.Cout * 4 <= (3ll << 20) &&
+                                      std::ceil(rounds) - rounds > 0.1)) &&
                   (long long)(cus + 1) * 2 * FT * 16 * FN <= p.part_floats;
   const dim3 grid(sk ? cus : std::min(nitems, cus)), block(512);
 #define FR_W4_CASE(PRE_, EPI_)                                                                            \

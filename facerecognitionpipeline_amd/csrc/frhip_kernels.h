@@ -119,8 +119,9 @@ struct Wino4Params {
   long long part_floats;
   int ksplit, ks_per;      // set by launch_wino4
   long long part_stride;   // set by launch_wino4
-  // 1: stream-K over the item-steps when whole items leave the last round >= 10% empty (uses
-  // part for the cut items' two raw partials); 0: whole items only
+  // 1: stream-K over the item-steps when whole items leave the last round >= 10% empty and U
+  // fits an XCD's L2 (uses part for the cut items' two raw partials); 2: stream-K whenever the
+  // grid has more items than CUs (experiments); 0: whole items only
   int sk_mode;
   int no_split;  // 1: never split-K (tests compare the two schedules)
 };

@@ -263,8 +263,10 @@ struct ProfScope {
   }
 };
 
-// F(4x4) stream-K schedule for large layers (frt_set_wino4_streamk: A/B and tests)
-static int g_wino4_streamk = 1;
+// F(4x4) stream-K schedule for large layers (frt_set_wino4_streamk: A/B and tests).  Off by
+// default: measured neutral on the IR-101 layers where its policy applies (stage 2, B=256:
+// 241-246 vs 239-243 us whole items), DESIGN.md §4.
+static int g_wino4_streamk = 0;
 
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s) {
@@ -1490,7 +1492,7 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 
 static int g_frt_wino4_split = 1;
 int frt_set_wino4_streamk(int on) {
-  g_wino4_streamk = on != 0;
+  g_wino4_streamk = on < 0 ? 0 : (on > 2 ? 2 : on);
   return FR_OK;
 }
 int frt_set_wino4_split(int on) {

@@ -39,8 +39,9 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
  * cin % 16 == 0, cout % 16 == 0.  frt_conv2d_winograd4 gives launch_wino4 a split-K workspace
  * (small grids then split the K loop over items + a reduce pass) unless frt_set_wino4_split(0). */
 int frt_set_wino4_split(int on);
-/* F(4x4) stream-K schedule for large layers (default on; also the handle's default).  Off: whole
- * items round-robin over the persistent grid. */
+/* F(4x4) stream-K schedule for large layers (default off, for handles too): 1 = by policy
+ * (last round >= 10% empty, U fits an XCD's L2, >= 8 K-steps per item), 2 = whenever the grid
+ * has more items than CUs, 0 = whole items round-robin over the persistent grid. */
 int frt_set_wino4_streamk(int on);
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                          const float* pre_scale, const float* pre_shift, const float* post_scale,

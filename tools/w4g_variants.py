@@ -18,7 +18,7 @@ OUT = os.path.join(REPO, "tools", "wv")
 SHAPES = [(256, 14, 256, 256, 2), (256, 14, 256, 256, 1), (256, 28, 128, 128, 2), (256, 56, 64, 64, 2),
           (256, 7, 512, 512, 2)]
 
-EPI_START = "    if (!live) continue;\n"
+EPI_START = "    // an idle quarter (!live, Cout % 64 != 0) runs the epilogue too"
 EPI_END = "\n  }\n}\n\n// Split-K finish"
 MFMA8 = "".join(f"        acc[x{o}] = __builtin_amdgcn_mfma_f32_16x16x4f32(a{e}.{c}, u{e}.{c}, acc[x{o}], 0, 0, 0);\n"
                 for c in "xyzw" for e, o in ((0, ""), (1, " + 1")))
@@ -54,11 +54,17 @@ VARIANTS = {
     "base": lambda s: s,
     "noepi": noepi,
     "notrans": notrans,
-    "noload": lambda s: s.replace("""          d[a][b] = __uint_as_float(
-              __builtin_amdgcn_raw_buffer_load_b32(r, poff[a][b], soff, 0));""", "          d[a][b] = __int_as_float(poff[a][b] + soff);"),
+    "noload": lambda s: s.replace("""          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);""",
+                                  """          const u32x2 v = {(unsigned)(poff[a][b] + soff), 0u};"""),
     "nomfma": lambda s: s.replace(MFMA8, "        acc[x][0] += a0.x * u0.x + a1.w * u1.w;\n"),
     "nouload": nouload,
     "mfmaonly": lambda s: nouload(notrans(noepi(s))),
+    "nores": lambda s: s.replace("rv[y][x] = ld4(rr, oo[y][x]);", "rv[y][x] = f4{0.f, 0.f, 0.f, 0.f};"),
+    "nostore": lambda s: s.replace("__builtin_amdgcn_raw_buffer_store_b128(bits, yr, oo[y][x], 0, 0);",
+                                   "if (bits.x == 0x7fc00001u) __builtin_amdgcn_raw_buffer_store_b128(bits, yr, oo[y][x], 0, 0);"),
+    "smallstore": lambda s: s.replace("__builtin_amdgcn_raw_buffer_store_b128(bits, yr, oo[y][x], 0, 0);",
+                                      "__builtin_amdgcn_raw_buffer_store_b128(bits, yr, oo[y][x] & 0xfff0, 0, 0);"),
+    "smallres": lambda s: s.replace("rv[y][x] = ld4(rr, oo[y][x]);", "rv[y][x] = ld4(rr, oo[y][x] & 0xfff0);"),
     "nomfma_noload": lambda s: VARIANTS["noload"](VARIANTS["nomfma"](s)),
     "nomfma_notrans": lambda s: notrans(VARIANTS["nomfma"](s)),
     "nomfma_noepi": lambda s: noepi(VARIANTS["nomfma"](s)),
@@ -86,11 +92,11 @@ def main():
             print(list(ex.map(build, names)))
     else:
         for n in names:
-            for sk in ((1, 0) if n == "base" else (1,)):  # base: stream-K on and off
+            for sk in ((1, 0, 2) if n == "base" else (1,)):  # base: stream-K auto, off, forced
                 for shp in SHAPES:
                     r = subprocess.run(["timeout", "-k", "5", "60", os.path.join(OUT, f"w4g_{n}")] +
                                        [str(x) for x in shp] + ["20", str(sk)], capture_output=True, text=True)
-                    print(f"{n + ('' if sk else '/nosk'):12s} {r.stdout.strip()} {r.stderr.strip()[-200:]}", flush=True)
+                    print(f"{n + ['/nosk', '', '/skall'][sk]:12s} {r.stdout.strip()} {r.stderr.strip()[-200:]}", flush=True)
                     if r.returncode:
                         return r.returncode
     return 0
