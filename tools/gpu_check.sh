@@ -21,6 +21,6 @@ if [ "${PROF:-0}" = "1" ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1
   echo "rocprof rc=$?"
-  python3 tools/prof_summary.py gpurun_out/prof/*/ > gpurun_out/layers.txt 2>&1 || true
+  python3 tools/prof_summary.py gpurun_out/prof/ > gpurun_out/layers.txt 2>&1 || true
   head -5 gpurun_out/prof/*/run_kernel_stats.csv 2>/dev/null | cut -c1-200
 fi

@@ -20,7 +20,7 @@ SHAPES = [(256, 14, 256, 256, 2), (256, 14, 256, 256, 1), (256, 28, 128, 128, 2)
 
 EPI_START = "    // an idle quarter (!live, Cout % 64 != 0) runs the epilogue too"
 EPI_END = "\n  }\n}\n\n// Split-K finish"
-MFMA8 = "".join(f"        acc[x{o}] = __builtin_amdgcn_mfma_f32_16x16x4f32(a{e}.{c}, u{e}.{c}, acc[x{o}], 0, 0, 0);\n"
+MFMA8 = "".join(f"        acc[x{o}] = __builtin_amdgcn_mfma_f32_16x16x4f32(u{e}.{c}, a{e}.{c}, acc[x{o}], 0, 0, 0);\n"
                 for c in "xyzw" for e, o in ((0, ""), (1, " + 1")))
 ULOAD = """          uring[y % URING] = y + URING < NXI ? ld4(ur, lo, (y + URING) * XS + cur)
                                              : ld4(ur, lo, (y + URING - NXI) * XS + nxt);"""
@@ -31,8 +31,7 @@ def nouload(s):
     return s.replace(ULOAD, "")
 
 
-TRANS_TURNS = ["      store(pa, sc_a, sh_a, mask_a, b + 2);", "      store(pb, sc_b, sh_b, mask_b, b + 3);",
-               "      store(pc, sc_c, sh_c, mask_c, b + 4);"]
+TRANS_TURNS = ["      store(pa, b + 2);", "      store(pb, b + 3);", "      store(pc, b + 4);"]
 
 
 def notrans(s):
@@ -56,7 +55,7 @@ VARIANTS = {
     "notrans": notrans,
     "noload": lambda s: s.replace("""          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);""",
                                   """          const u32x2 v = {(unsigned)(poff[a][b] + soff), 0u};"""),
-    "nomfma": lambda s: s.replace(MFMA8, "        acc[x][0] += a0.x * u0.x + a1.w * u1.w;\n"),
+    "nomfma": lambda s: (s.replace(MFMA8, "        acc[x][0] += a0.x * u0.x + a1.w * u1.w;\n") if MFMA8 in s else s + "#error MFMA8"),
     "nouload": nouload,
     "mfmaonly": lambda s: nouload(notrans(noepi(s))),
     "nores": lambda s: s.replace("rv[y][x] = ld4(rr, oo[y][x]);", "rv[y][x] = f4{0.f, 0.f, 0.f, 0.f};"),
