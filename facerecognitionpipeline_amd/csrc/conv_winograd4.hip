@@ -176,26 +176,30 @@ __device__ __forceinline__ void at6v(const f2 (&m)[6], f2 (&o)[4]) {
 // covers GM tile blocks x all cout blocks, so the patches and U blocks it streams are shared
 // in its L2
 struct Item {
-  int mb, nb, split;
+  int mb, nb;  // tile block, cout block
+  int split;   // K part (split-K launches)
+  int li;      // item index within the launch's item range
 };
-__device__ __forceinline__ Item item_of(const Wino4Params& p, int t) {
-  const int NB = p.nblocks, nT = p.mblocks * NB;
+// global item index gi (0 .. mblocks * nblocks - 1) -> (tile block, cout block)
+__device__ __forceinline__ Item item_of(const Wino4Params& p, int gi) {
+  const int NB = p.nblocks;
   Item it;
-  it.split = t / nT;
-  t -= it.split * nT;
   const int GM = p.nbg;
-  const int grp = t / (GM * NB), rem = t - grp * GM * NB;
+  const int grp = gi / (GM * NB), rem = gi - grp * GM * NB;
   const int gm = min(GM, p.mblocks - grp * GM);
   it.nb = rem / gm;
   it.mb = grp * GM + (rem - it.nb * gm);
+  it.split = 0;
+  it.li = 0;
   return it;
 }
 
-// MODE: 0 = whole items round-robin over the persistent grid; 1 = split-K (small grids: every
-// item's K loop cut into ksplit parts, raw partial outputs + wino4_split_reduce_kernel);
-// 2 = stream-K (large grids whose items do not fill whole rounds: the item-step space is cut
-// into equal contiguous ranges, one per workgroup; an item cut at a range boundary leaves two raw
-// partial outputs in a compact slab, summed by wino4_sk_fixup_kernel).
+// A launch covers the items [item0, item0 + nitem) of the layer's item order.
+// MODE: 0 = whole items round-robin over the persistent grid; 1 = split-K (every item's K loop
+// cut into ksplit parts, raw partial outputs into compact slots [item][part][16 tiles]
+// [16 pixels][64 couts], summed in part order by wino4_part_fixup_kernel: small grids);
+// 2 = stream-K (the item-step space cut into equal contiguous ranges, one per workgroup; an item
+// cut at a range boundary leaves two parts).
 template <bool PRE, int EPI, int MODE>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   constexpr bool SPLIT = MODE == 1, SK = MODE == 2;
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout;
   const int KST = Cin / KC;                       // K-steps of the whole reduction
   const int KS = SPLIT ? p.ks_per : KST;          // stream steps per item
-  const int nitems = p.mblocks * p.nblocks * p.ksplit;
+  const int nitems = p.nitem * p.ksplit;
   // MODE 0/1: this workgroup's items are blockIdx.x, blockIdx.x + gridDim.x, ... of the
   // XCD-remapped order (item_at(j), j local).  SK: it owns item-steps [u_lo, u_hi) of the
   // nT * KST space (its logical index XCD-remapped, so an XCD's workgroups hold one contiguous
@@ -217,7 +221,13 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   const int u_hi = SK ? (int)((long long)(bl + 1) * nT * KST / gridDim.x) : 0;
   const int t_first = u_lo / KST, t_last = SK ? (u_hi - 1) / KST : nloc - 1;
   auto item_at = [&](int j) {
-    return SK ? item_of(p, j) : item_of(p, xcd_remap(blockIdx.x + j * gridDim.x, nitems));
+    if (SK) return item_of(p, j);
+    const int t = xcd_remap(blockIdx.x + j * gridDim.x, nitems);
+    const int sp = t / p.nitem, li = t - sp * p.nitem;
+    Item it = item_of(p, p.item0 + li);
+    it.split = sp;
+    it.li = li;
+    return it;
   };
   // K-steps item `it` really has (split-K: the last split may be short; its stream is padded
   // with steps whose patches load as zeros, so every item is KS stream steps long)
@@ -516,8 +526,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     // +residual), one 16-byte store of the 4 couts per output pixel
     const int n = lane & 15, rg = lane >> 4;
     const int cout0 = min(it.nb * 64 + w * 16, Cout - 16) + 4 * rg;  // (clamped for an idle quarter)
-    const __amdgpu_buffer_rsrc_t yr =
-        uniform_rsrc(SPLIT ? p.part + it.split * p.part_stride : p.y, p.B * H * W * Cout * 4);
+    const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(p.y, p.B * H * W * Cout * 4);
     constexpr bool RES = !SPLIT && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
     constexpr bool PRELU = !SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU);
     const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, RES ? p.B * H * W * Cout * 4 : 0);
@@ -569,11 +578,12 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     auto out4 = [&](int y, int x) {
       return f4{outv[0][y][x].x, outv[0][y][x].y, outv[1][y][x].x, outv[1][y][x].y};
     };
-    if (SK && partial) {
-      // raw partial outputs of an item cut at range boundary bd (the first part ends at this
-      // workgroup's range end, the second starts at its range start): slab [bd][part][16 tiles]
-      // [16 pixels][64 couts], summed and finished by wino4_sk_fixup_kernel
-      const int bd = s0 == 0 ? bl + 1 : bl, pt = s0 == 0 ? 0 : 1;
+    if (SPLIT || (SK && partial)) {
+      // raw partial outputs into compact slot [16 tiles][16 pixels][64 couts]: split-K part
+      // it.split of launch item it.li, or (stream-K) part 0 / 1 of the item cut at range
+      // boundary bd (the first part ends at this workgroup's range end, the second starts at its
+      // range start); summed in part order and finished by wino4_part_fixup_kernel
+      const int slot = SPLIT ? it.li * p.ksplit + it.split : (s0 == 0 ? bl + 1 : bl) * 2 + (s0 == 0 ? 0 : 1);
       const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
 #pragma unroll
       for (int y = 0; y < 4; ++y)
@@ -581,7 +591,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         for (int x = 0; x < 4; ++x) {
           const f4 v = out4(y, x);
           const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-          const int off = (((((bd * 2 + pt) * FT + n) * 16 + y * 4 + x) * FN) + w * 16 + 4 * rg) * 4;
+          const int off = ((((slot * FT + n) * 16 + y * 4 + x) * FN) + w * 16 + 4 * rg) * 4;
           __builtin_amdgcn_raw_buffer_store_b128(bits, sr, off, 0, 0);
         }
       continue;
@@ -624,69 +634,31 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   }
 }
 
-// Split-K finish: y = epilogue(sum over splits of the raw partial outputs), summed in split
-// order (deterministic).  Pixels outside the images were never stored by any split, and none
-// of them is read here (n4 covers exactly the B*H*W*Cout outputs).
-template <int EPI>
-__global__ void wino4_split_reduce_kernel(const float* __restrict__ part, int S, long long stride, long long n4,
-                                           int Cout, const float* __restrict__ sc, const float* __restrict__ sh,
-                                           const float* __restrict__ prelu, const float* __restrict__ res,
-                                           float* __restrict__ y) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  float4 w[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s)
-    if (s < S) w[s] = reinterpret_cast<const float4*>(part + s * stride)[i];
-  float4 v = w[0];
-#pragma unroll
-  for (int s = 1; s < 16; ++s)
-    if (s < S) {
-      v.x += w[s].x;
-      v.y += w[s].y;
-      v.z += w[s].z;
-      v.w += w[s].w;
-    }
-  for (int s = 16; s < S; ++s) {
-    const float4 u = reinterpret_cast<const float4*>(part + s * stride)[i];
-    v.x += u.x;
-    v.y += u.y;
-    v.z += u.z;
-    v.w += u.w;
-  }
-  const int c0 = (int)((i * 4) % Cout);
-  float o[4] = {v.x, v.y, v.z, v.w};
-  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-  if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) r = reinterpret_cast<const float4*>(res)[i];
-  const float rv[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = c0 + j;
-    float t = o[j] * sc[c] + sh[c];
-    if constexpr (EPI == EPI_AFFINE_PRELU) t = t > 0.f ? t : t * prelu[c];
-    if constexpr (EPI == EPI_AFFINE_RES) t += rv[j];
-    if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
-      t += rv[j];
-      t = t > 0.f ? t : t * prelu[c];
-    }
-    o[j] = t;
-  }
-  reinterpret_cast<float4*>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
-}
-
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
 // B-fragment order wino4_kernel reads: [xi][Cout/16][Cin/16][lane = 16 k + cout%16][m] with
 // cin % 16 = 4k + m.
-// Stream-K finish: for each range boundary bd that cuts an item, y = epilogue(part 0 + part 1)
-// at the item's in-image pixels (the two parts summed in a fixed order: deterministic).
-// Thread = (tile n, pixel, cout quad); grid (FT * 16 * FN / 4 / 256, boundaries).
-template <int EPI>
-__global__ void wino4_sk_fixup_kernel(Wino4Params p, int KST, int P) {
-  const int bd = blockIdx.y + 1;
-  const long long N = (long long)p.mblocks * p.nblocks * KST;
-  const int u = (int)(bd * N / P);
-  if (u % KST == 0) return;
-  const Item it = item_of(p, u / KST);
+// Split-K / stream-K finish: y = epilogue(sum of an item's raw partial outputs, in part order:
+// deterministic) at the item's in-image pixels.  Thread = (tile n, pixel, cout quad); grid
+// (FT * 16 * FN / 4 / 256, items).  SKF: blockIdx.y + 1 is a stream-K range boundary (the item
+// it cuts has parts in slots 2 bd, 2 bd + 1; an uncut boundary returns); else blockIdx.y is the
+// launch item li with parts in slots li * S .. li * S + S - 1.
+template <int EPI, bool SKF>
+__global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
+  int gi, slot0, S;
+  if (SKF) {
+    const int bd = blockIdx.y + 1;
+    const long long N = (long long)p.mblocks * p.nblocks * KST;
+    const int u = (int)(bd * N / P);
+    if (u % KST == 0) return;
+    gi = u / KST;
+    slot0 = 2 * bd;
+    S = 2;
+  } else {
+    gi = p.item0 + blockIdx.y;
+    slot0 = blockIdx.y * p.ksplit;
+    S = p.ksplit;
+  }
+  const Item it = item_of(p, gi);
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = idx >> 8, px = (idx >> 4) & 15, cq = idx & 15;
   const int cout0 = it.nb * FN + 4 * cq;
@@ -702,10 +674,14 @@ __global__ void wino4_sk_fixup_kernel(Wino4Params p, int KST, int P) {
   const long long pix = (long long)(rs * p.NC * H + y) * W + (long long)cs * H * W + x;
   if (pix >= (long long)p.B * H * W) return;
   const float4* slab = reinterpret_cast<const float4*>(p.part);
-  const long long o0 = ((((long long)bd * 2 + 0) * FT + n) * 16 + px) * (FN / 4) + cq;
-  const long long o1 = ((((long long)bd * 2 + 1) * FT + n) * 16 + px) * (FN / 4) + cq;
-  const float4 a = slab[o0], b = slab[o1];
-  float v[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < S; ++sp) {
+    const float4 a = slab[((((long long)slot0 + sp) * FT + n) * 16 + px) * (FN / 4) + cq];
+    v[0] += a.x;
+    v[1] += a.y;
+    v[2] += a.z;
+    v[3] += a.w;
+  }
   const long long yo = pix * p.Cout + cout0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -804,66 +780,93 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   p.mblocks = (p.ntiles + FT - 1) / FT;
   p.nblocks = (p.Cout + FN - 1) / FN;
   p.nbg = std::max(1, std::min(p.mblocks, 32 / p.nblocks));  // tile blocks per XCD group (32 items)
-  // split-K when the items leave most CUs idle (serving batches): as many splits as fit one
-  // round of 256 workgroups, bounded by the K-steps and the partial-output workspace
   const int KST = p.Cin / KC;
   const int nT = p.mblocks * p.nblocks;
-  const long long elems = (long long)p.B * p.H * p.W * p.Cout;
+  constexpr long long SLOT = (long long)FT * 16 * FN;  // floats of one compact partial slot
   const bool aligned = ((reinterpret_cast<uintptr_t>(p.y) | reinterpret_cast<uintptr_t>(p.res) |
                          reinterpret_cast<uintptr_t>(p.part)) & 15) == 0;
-  int S = 1;
-  p.ks_per = KST;
-  if (p.part && !p.no_split && aligned && nT <= 128 && KST > 1) {
-    S = std::min(KST, 256 / nT);
-    S = (int)std::min<long long>(S, std::min<long long>(p.part_floats, (1ll << 29) - 1) / elems);
-    if (S > 1) {
-      p.ks_per = (KST + S - 1) / S;
-      S = (KST + p.ks_per - 1) / p.ks_per;
-    }
-  }
-  p.ksplit = S > 1 ? S : 1;
-  if (p.ksplit == 1) p.ks_per = KST;
-  p.part_stride = elems;
-  const int nitems = nT * p.ksplit;
   int cus = 256;
   {
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  // stream-K when whole items would leave a last round at least 10% empty; each workgroup then
-  // runs an equal share of the item-steps and cut items are finished by wino4_sk_fixup_kernel.
-  // Whole items keep every workgroup on the same K-step of its item, so an XCD's workgroups
-  // read the same U slice at a time; stream-K ranges start at arbitrary steps and read all of
-  // U at once, which pays only while U fits an XCD's 4 MB L2 (measured, IR-101 B=256: stage 2
-  // 128->128, U 2.4 MB, 258 -> 249 us; stage 3 256->256, U 9.4 MB, 238 -> 324 us).  With fewer
-  // than 8 K-steps per item the two partial epilogues and the fixup outweigh the round
-  // (stage 1 64->64: 297 -> 314 us).
-  const bool split = p.ksplit > 1;
+  const bool can_split = p.part && !p.no_split && aligned && KST > 1;
+  // K parts for a split-K launch of n items: as many as fit one round of workgroups, bounded by
+  // the K-steps and the slot workspace; ks_per steps each
+  auto split_of = [&](int n, int& ks_per) {
+    int S = (int)std::min<long long>(std::min(KST, cus / n), p.part_floats / (SLOT * n));
+    ks_per = KST;
+    if (S > 1) {
+      ks_per = (KST + S - 1) / S;
+      S = (KST + ks_per - 1) / ks_per;
+    }
+    return std::max(S, 1);
+  };
+  // stream-K (opt-in, p.sk_mode): each workgroup runs an equal share of the item-steps; cut items
+  // are finished by wino4_part_fixup_kernel.  Whole items keep every workgroup on the same K-step
+  // of its item, so an XCD's workgroups read the same U slice at a time; stream-K ranges start
+  // at arbitrary steps and read all of U at once, which pays only while U fits an XCD's 4 MB L2
+  // (measured, IR-101 B=256: stage 2 128->128, U 2.4 MB, neutral; stage 3 256->256, U 9.4 MB,
+  // 238 -> 324 us).  With fewer than 8 K-steps per item the two partial epilogues and the fixup
+  // outweigh the round (stage 1 64->64: 297 -> 314 us).
   const double rounds = (double)nT / cus;
-  const bool sk = !split && p.sk_mode && p.part && aligned && nT > cus && cus % 8 == 0 &&
+  const bool sk = p.sk_mode && p.part && aligned && nT > cus && cus % 8 == 0 &&
                   (p.sk_mode == 2 || (KST >= 8 && (long long)NXI * p.Cin * p.Cout * 4 <= (3ll << 20) &&
                                       std::ceil(rounds) - rounds > 0.1)) &&
-                  (long long)(cus + 1) * 2 * FT * 16 * FN <= p.part_floats;
-  const dim3 grid(sk ? cus : std::min(nitems, cus)), block(512);
-#define FR_W4_CASE(PRE_, EPI_)                                                                            \
-  if (pre == PRE_ && epi == EPI_) {                                                                       \
-    if (split)                                                                                            \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, 1>), grid, block, 0, s, p);                            \
-    else if (sk)                                                                                          \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, 2>), grid, block, 0, s, p);                            \
-    else                                                                                                  \
-      hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, 0>), grid, block, 0, s, p);                            \
-    if (sk)                                                                                               \
-      hipLaunchKernelGGL((wino4_sk_fixup_kernel<EPI_>), dim3(FT * 16 * FN / 4 / 256, cus - 1), dim3(256),  \
-                         0, s, p, KST, cus);                                                              \
-    if (split) {                                                                                          \
-      const long long n4 = elems / 4;                                                                     \
-      hipLaunchKernelGGL((wino4_split_reduce_kernel<EPI_>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), \
-                         0, s, p.part, p.ksplit, p.part_stride, n4, p.Cout, p.post_scale, p.post_shift,     \
-                         p.prelu, p.res, p.y);                                                             \
-    }                                                                                                     \
-    return hipGetLastError();                                                                             \
+                  (long long)(cus + 1) * 2 * SLOT <= p.part_floats;
+  // Whole-item launch of n items from item0 (MODE 0), or split-K launch (MODE 1) + fixup
+  Wino4Params pw = p;
+  auto whole = [&](int item0, int n) {
+    pw = p;
+    pw.item0 = item0;
+    pw.nitem = n;
+    pw.ksplit = 1;
+    pw.ks_per = KST;
+  };
+  auto splitk = [&](int item0, int n, int S, int ks_per) {
+    pw = p;
+    pw.item0 = item0;
+    pw.nitem = n;
+    pw.ksplit = S;
+    pw.ks_per = ks_per;
+  };
+#define FR_W4_LAUNCH(PRE_, EPI_, MODE_)                                                                     \
+  {                                                                                                         \
+    const int nit = MODE_ == 2 ? nT : pw.nitem * pw.ksplit;                                                 \
+    hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, MODE_>), dim3(MODE_ == 2 ? cus : std::min(nit, cus)),      \
+                       dim3(512), 0, s, pw);                                                                \
+    if (MODE_ == 1)                                                                                         \
+      hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_, false>), dim3(FT * 16 * FN / 4 / 256, pw.nitem),    \
+                         dim3(256), 0, s, pw, KST, cus);                                                    \
+    if (MODE_ == 2)                                                                                         \
+      hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_, true>), dim3(FT * 16 * FN / 4 / 256, cus - 1),      \
+                         dim3(256), 0, s, pw, KST, cus);                                                    \
+  }
+#define FR_W4_CASE(PRE_, EPI_)                                                                              \
+  if (pre == PRE_ && epi == EPI_) {                                                                         \
+    int ks_per = KST;                                                                                       \
+    if (can_split && nT <= cus / 2) {                                                                       \
+      /* small grid (serving batches): every item's K loop split */                                         \
+      const int S = split_of(nT, ks_per);                                                                   \
+      if (S > 1) {                                                                                          \
+        splitk(0, nT, S, ks_per);                                                                           \
+        FR_W4_LAUNCH(PRE_, EPI_, 1)                                                                         \
+      } else {                                                                                              \
+        whole(0, nT);                                                                                       \
+        FR_W4_LAUNCH(PRE_, EPI_, 0)                                                                         \
+      }                                                                                                     \
+    } else if (sk) {                                                                                        \
+      whole(0, nT);                                                                                         \
+      FR_W4_LAUNCH(PRE_, EPI_, 2)                                                                           \
+    } else {                                                                                                \
+      /* whole items.  (Running a part-empty last round as a split-K launch of its own was      */          \
+      /* measured neutral: stage 2, 6 rounds + 32 items, 244.6 -> 245.8 us; the short launch and  */          \
+      /* its fixup cost about the round they save.)                                               */          \
+      whole(0, nT);                                                                                         \
+      FR_W4_LAUNCH(PRE_, EPI_, 0)                                                                           \
+    }                                                                                                       \
+    return hipGetLastError();                                                                               \
   }
   FR_W4_CASE(true, EPI_AFFINE_PRELU)       // IR conv1: pre-BN (in the transform), BN, PReLU
   FR_W4_CASE(false, EPI_AFFINE_RES)        // IR conv2: BN + identity shortcut
@@ -871,6 +874,7 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   FR_W4_CASE(false, EPI_AFFINE)            // SCRFD conv + BN / bias
   FR_W4_CASE(false, EPI_AFFINE_RES_PRELU)  // SCRFD BasicBlock conv2 + BN + add + ReLU
 #undef FR_W4_CASE
+#undef FR_W4_LAUNCH
   return hipErrorInvalidValue;
 }
 

@@ -113,12 +113,13 @@ struct Wino4Params {
   int B, H, W, Cin, Cout;
   int Pr, Pc, NC, TWc, ntiles, mblocks, nblocks;  // set by launch_wino4 (wino4_canvas)
   int nbg;  // tile blocks per XCD group of items (set by launch_wino4)
-  // split-K workspace (optional): raw partial outputs [ksplit][B*H*W*Cout]; launch_wino4 splits
-  // the K loop over items when the grid is small and part_floats holds the slabs
+  // split-K / stream-K workspace (optional): compact raw partial outputs, one 16-tile x 16-pixel
+  // x 64-cout slot (64 KiB) per item part; launch_wino4 splits the K loop of a small grid's items
+  // when part_floats holds the slots
   float* part;
   long long part_floats;
   int ksplit, ks_per;      // set by launch_wino4
-  long long part_stride;   // set by launch_wino4
+  int item0, nitem;        // set by launch_wino4: the launch's range of the layer's item order
   // 1: stream-K over the item-steps when whole items leave the last round >= 10% empty and U
   // fits an XCD's L2 (uses part for the cut items' two raw partials); 2: stream-K whenever the
   // grid has more items than CUs (experiments); 0: whole items only

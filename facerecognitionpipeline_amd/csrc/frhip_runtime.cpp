@@ -1538,9 +1538,8 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.Cout = cout;
     p.sk_mode = g_wino4_streamk;
     p.no_split = !g_frt_wino4_split;
-    if (g_frt_wino4_split || g_wino4_streamk) {  // split-K / stream-K partial workspace
-      p.part_floats = g_frt_wino4_split ? (long long)B * H * W * cout * std::min(cin / 16, 16) : 0;
-      if (g_wino4_streamk) p.part_floats = std::max<long long>(p.part_floats, 257ll * 2 * 16 * 16 * 64);
+    if (g_frt_wino4_split || g_wino4_streamk) {  // split-K / stream-K partial slots (64 KiB each)
+      p.part_floats = 257ll * 2 * 16 * 16 * 64;
       if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;
       p.part = part;
     }

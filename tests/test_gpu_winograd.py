@@ -87,9 +87,9 @@ def test_winograd4_multi_round(B, H, cin, cout):
 ])
 @pytest.mark.parametrize("epi", [1, 2])
 def test_winograd4_split_k_small_grids(B, H, cin, cout, epi):
-    """Small grids split the F(4x4) K loop over workgroups (raw partial outputs, one split
-    carrying the pre-BN correction); wino4_split_reduce_kernel sums the slabs in split order
-    and applies the epilogue.  Both paths match the CPU conv, and each other to the same bar."""
+    """Small grids split the F(4x4) K loop over workgroups (raw partial outputs in compact
+    slots); wino4_part_fixup_kernel sums them in split order and applies the epilogue.  Both
+    paths match the CPU conv, and each other to the same bar."""
     L = _frt.lib()
     outs = {}
     try:

@@ -69,6 +69,7 @@ int main(int argc, char** argv) {
   p.part = part;
   p.part_floats = part_floats;
   p.sk_mode = argc > 7 ? atoi(argv[7]) : 1;
+  p.no_split = argc > 8 ? atoi(argv[8]) : 0;  // 1: whole items only (no tail split-K)
   p.B = B;
   p.H = H;
   p.W = H;

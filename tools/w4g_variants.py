@@ -91,11 +91,12 @@ def main():
             print(list(ex.map(build, names)))
     else:
         for n in names:
-            for sk in ((1, 0, 2) if n == "base" else (1,)):  # base: stream-K auto, off, forced
+            # base: the default schedule (whole items + tail split-K), whole items only, stream-K
+            for tag, sk, ns in ((("", 0, 0), ("/whole", 0, 1), ("/sk", 2, 0)) if n == "base" else (("", 0, 0),)):
                 for shp in SHAPES:
                     r = subprocess.run(["timeout", "-k", "5", "60", os.path.join(OUT, f"w4g_{n}")] +
-                                       [str(x) for x in shp] + ["20", str(sk)], capture_output=True, text=True)
-                    print(f"{n + ['/nosk', '', '/skall'][sk]:12s} {r.stdout.strip()} {r.stderr.strip()[-200:]}", flush=True)
+                                       [str(x) for x in shp] + ["20", str(sk), str(ns)], capture_output=True, text=True)
+                    print(f"{n + tag:12s} {r.stdout.strip()} {r.stderr.strip()[-200:]}", flush=True)
                     if r.returncode:
                         return r.returncode
     return 0
