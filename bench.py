@@ -61,6 +61,8 @@ def parse():
                     help="conv arithmetic: exact f32 MFMA (default, parity path) or opt-in split bf16x3")
     ap.add_argument("--conv-algorithm", choices=["winograd4", "winograd", "direct"], default="winograd4",
                     help="stride-1 3x3 convs: Winograd F(4x4,3x3), F(2x2,3x3) or the direct implicit GEMM (all f32)")
+    ap.add_argument("--lanes-min", type=int, default=None,
+                    help="forwards of n >= this many crops run as two half-batch lanes (0: one lane; default: library's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=None,
@@ -217,7 +219,7 @@ def main():
     from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
     sd = W.synthetic_state_dict(args.arch, model_type=args.model_type)
     emb = FaceEmbedder(architecture=args.arch, model_type=args.model_type, state_dict=sd, device=dev, max_batch=args.batch,
-                       precision=args.precision, conv_algorithm=args.conv_algorithm)
+                       precision=args.precision, conv_algorithm=args.conv_algorithm, lanes_min=args.lanes_min)
 
     # gallery: rank 0 embeds min(G, 1000) synthetic gallery crops on its GPU and grows them to G
     # rows as normalize(e + 0.0214 z); RCCL broadcast to the other ranks

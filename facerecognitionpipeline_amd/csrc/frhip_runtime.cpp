@@ -269,7 +269,11 @@ struct ProfScope {
 static int g_wino4_streamk = 0;
 
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
-             const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s) {
+             const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
+             const LaneWs* L) {
+  float* const sk_ws = L ? L->sk_ws : h->sk_ws;
+  int* const sk_cnt = L ? L->sk_cnt : h->sk_cnt;
+  float* const w4part = L ? L->w4part : h->w4part;
   ConvParams p{};
   p.x = x;
   p.w = cw.w;
@@ -297,12 +301,12 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   p.steps_total = cw.kh * cw.kw * cw.cin / 32;
   p.steps_per_split = (p.steps_total + nsplit - 1) / nsplit;
   p.split_stride = split_stride;
-  if (h->stream_k && nsplit == 1 && h->sk_ws) {
+  if (h->stream_k && nsplit == 1 && sk_ws) {
     p.sk_cus = h->cus;
-    p.sk_ws = h->sk_ws;
-    p.sk_ws_floats = h->sk_ws_floats;
-    p.sk_cnt = h->sk_cnt;
-    p.sk_cnt_cap = h->sk_cnt_cap;
+    p.sk_ws = sk_ws;
+    p.sk_ws_floats = L ? L->sk_ws_floats : h->sk_ws_floats;
+    p.sk_cnt = sk_cnt;
+    p.sk_cnt_cap = L ? L->sk_cnt_cap : h->sk_cnt_cap;
   }
   const double flop = 2.0 * p.M * (double)p.Cout * cw.kh * cw.kw * cw.cin;
   // Tile per layer shape, from tools/conv_sweep.py on MI355X at B=256 with the stream-K
@@ -331,8 +335,8 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.W = W;
     wp.Cin = cw.cin;
     wp.Cout = cw.cout;
-    wp.part = h->w4part;
-    wp.part_floats = h->w4part ? fr_handle::W4PART_FLOATS : 0;
+    wp.part = w4part;
+    wp.part_floats = w4part ? fr_handle::W4PART_FLOATS : 0;
     wp.sk_mode = g_wino4_streamk;
     Wino4Params cv = wp;
     wino4_canvas(cv);
@@ -385,43 +389,127 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   return FR_OK;
 }
 
-// One forward of up to max_batch crops: rgb (device) -> out (device) [n][512].
-int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int normalize, hipStream_t s) {
-  {
-    ProfScope ps(h, s, 2.0 * n * 112.0 * 112.0 * 64 * 27, 0);
-    hipError_t e = launch_stem(rgb, n, h->lut, h->stem_w, h->stem_scale, h->stem_shift, h->stem_prelu, h->act[0], s);
+// The handle's own workspace as lane 0.
+LaneWs lane0_ws(fr_handle* h) {
+  LaneWs L;
+  for (int i = 0; i < 3; ++i) L.act[i] = h->act[i];
+  L.sc_buf = h->sc_buf;
+  L.partial = h->partial;
+  L.w4part = h->w4part;
+  L.sk_ws = h->sk_ws;
+  L.sk_ws_floats = h->sk_ws_floats;
+  L.sk_cnt = h->sk_cnt;
+  L.sk_cnt_cap = h->sk_cnt_cap;
+  return L;
+}
+
+// Lane 1's workspace for up to `batch` crops, its stream and the fork / join events.
+int ensure_lane1(fr_handle* h, int batch) {
+  LaneWs& L = h->lane1;
+  if (h->lane1_batch < batch) {
+    for (auto& a : L.act) {
+      if (a) FR_HIP(h, hipFree(a));
+      a = nullptr;
+    }
+    if (L.sc_buf) FR_HIP(h, hipFree(L.sc_buf));
+    if (L.partial) FR_HIP(h, hipFree(L.partial));
+    L.sc_buf = L.partial = nullptr;
+    h->lane1_batch = 0;
+    const size_t mb = batch;
+    for (auto& a : L.act) FR_HIP(h, hipMalloc((void**)&a, mb * 112 * 112 * 64 * sizeof(float)));
+    FR_HIP(h, hipMalloc((void**)&L.sc_buf, mb * 56 * 56 * 64 * sizeof(float)));
+    FR_HIP(h, hipMalloc((void**)&L.partial, (size_t)h->head_split * mb * 512 * sizeof(float)));
+    h->lane1_batch = batch;
+  }
+  if (!L.w4part) FR_HIP(h, hipMalloc((void**)&L.w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
+  if (ensure_stream_k(h->device, &h->cus, &L.sk_ws, &L.sk_ws_floats, &L.sk_cnt, &L.sk_cnt_cap) != FR_OK)
+    return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
+  if (!h->lane_stream) FR_HIP(h, hipStreamCreateWithFlags(&h->lane_stream, hipStreamNonBlocking));
+  if (!h->lane_fork) FR_HIP(h, hipEventCreateWithFlags(&h->lane_fork, hipEventDisableTiming));
+  if (!h->lane_join) FR_HIP(h, hipEventCreateWithFlags(&h->lane_join, hipEventDisableTiming));
+  return FR_OK;
+}
+
+// One forward of up to max_batch crops: rgb (device) -> out (device) [n][512], as nl lanes
+// (lane l: crops [off[l], off[l] + cnt[l]) on stream st[l] with workspace L[l]).  Every launch is
+// issued for each lane in turn, so while one lane's layer runs its last, part-empty round the
+// other lane's launch of the same layer is already queued.
+int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* cnt, int nl, float* out,
+                  int normalize, const hipStream_t* st, const LaneWs* L) {
+  for (int l = 0; l < nl; ++l) {
+    const int n = cnt[l];
+    ProfScope ps(h, st[l], 2.0 * n * 112.0 * 112.0 * 64 * 27, 0);
+    hipError_t e = launch_stem(rgb + (size_t)off[l] * 112 * 112 * 3, n, h->lut, h->stem_w, h->stem_scale,
+                               h->stem_shift, h->stem_prelu, L[l].act[0], st[l]);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("stem launch: ") + hipGetErrorString(e));
   }
   int cur = 0, HW = 112;
   for (const auto& b : h->blocks) {
     const int nxt = cur == 0 ? 1 : 0;
-    float* x = h->act[cur];
-    float* r = h->act[2];
-    float* y = h->act[nxt];
-    int rc = run_conv(h, b.conv1, x, r, n, HW, HW, EPI_AFFINE_PRELU, nullptr, 0, 0, 1, 0, s);
-    if (rc) return rc;
     const int Ho = HW / b.spec.stride;
-    if (b.has_sc_conv) {
-      rc = run_conv(h, b.sc, x, h->sc_buf, n, HW, HW, EPI_AFFINE, nullptr, 0, 0, 1, 0, s);
+    for (int l = 0; l < nl; ++l) {
+      int rc = run_conv(h, b.conv1, L[l].act[cur], L[l].act[2], cnt[l], HW, HW, EPI_AFFINE_PRELU, nullptr, 0, 0, 1,
+                        0, st[l], &L[l]);
       if (rc) return rc;
-      rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES, h->sc_buf, Ho, Ho, 1, 0, s);
-    } else if (b.spec.stride == 1) {
-      rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES, x, HW, HW, 1, 0, s);
-    } else {
-      rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES_SUB, x, HW, HW, 1, 0, s);
     }
-    if (rc) return rc;
+    for (int l = 0; l < nl; ++l) {
+      float* x = L[l].act[cur];
+      float* r = L[l].act[2];
+      float* y = L[l].act[nxt];
+      const int n = cnt[l];
+      int rc;
+      if (b.has_sc_conv) {
+        rc = run_conv(h, b.sc, x, L[l].sc_buf, n, HW, HW, EPI_AFFINE, nullptr, 0, 0, 1, 0, st[l], &L[l]);
+        if (rc) return rc;
+        rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES, L[l].sc_buf, Ho, Ho, 1, 0, st[l], &L[l]);
+      } else if (b.spec.stride == 1) {
+        rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES, x, HW, HW, 1, 0, st[l], &L[l]);
+      } else {
+        rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES_SUB, x, HW, HW, 1, 0, st[l], &L[l]);
+      }
+      if (rc) return rc;
+    }
     cur = nxt;
     HW = Ho;
   }
-  const long long split_stride = (long long)n * 512;
-  int rc = run_conv(h, h->head, h->act[cur], h->partial, n, 7, 7, EPI_RAW, nullptr, 0, 0, h->head_split,
-                    split_stride, s);
+  for (int l = 0; l < nl; ++l) {
+    const int n = cnt[l];
+    const long long split_stride = (long long)n * 512;
+    int rc = run_conv(h, h->head, L[l].act[cur], L[l].partial, n, 7, 7, EPI_RAW, nullptr, 0, 0, h->head_split,
+                      split_stride, st[l], &L[l]);
+    if (rc) return rc;
+    ProfScope ps(h, st[l], 0.0, 0);
+    hipError_t e = launch_head_reduce(L[l].partial, h->head_split, split_stride, h->fc_bias, h->bn1d_scale,
+                                      h->bn1d_shift, out + (size_t)off[l] * 512, n, normalize, !h->arcface, st[l]);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("head launch: ") + hipGetErrorString(e));
+  }
+  return FR_OK;
+}
+
+// One forward of up to max_batch crops: rgb (device) -> out (device) [n][512].  With lanes on
+// (fr_set_lanes) and n >= lane_min, the batch runs as two halves: lane 1 forks from s and joins
+// back into it, so the call is stream-ordered on s like a single forward.  Profiled forwards stay
+// one lane (their per-launch events would overlap).
+int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int normalize, hipStream_t s) {
+  const LaneWs L0 = lane0_ws(h);
+  if (h->lane_min <= 0 || n < h->lane_min || n < 2 || h->prof) {
+    const int off = 0;
+    return forward_lanes(h, rgb, &off, &n, 1, out, normalize, &s, &L0);
+  }
+  const int n0 = n / 2, n1 = n - n0;
+  int rc = ensure_lane1(h, std::max(n1, (h->max_batch + 1) / 2));
   if (rc) return rc;
-  ProfScope ps(h, s, 0.0, 0);
-  hipError_t e = launch_head_reduce(h->partial, h->head_split, split_stride, h->fc_bias, h->bn1d_scale,
-                                    h->bn1d_shift, out, n, normalize, !h->arcface, s);
-  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("head launch: ") + hipGetErrorString(e));
+  const int off[2] = {0, n0}, cnt[2] = {n0, n1};
+  const hipStream_t st[2] = {s, h->lane_stream};
+  const LaneWs L[2] = {L0, h->lane1};
+  FR_HIP(h, hipEventRecord(h->lane_fork, s));
+  FR_HIP(h, hipStreamWaitEvent(h->lane_stream, h->lane_fork, 0));
+  rc = forward_lanes(h, rgb, off, cnt, 2, out, normalize, st, L);
+  // join even after a failed launch, so that nothing of this call is left unordered behind s
+  const hipError_t e1 = hipEventRecord(h->lane_join, h->lane_stream);
+  const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(s, h->lane_join, 0) : e1;
+  if (rc) return rc;
+  FR_HIP(h, e2);
   return FR_OK;
 }
 
@@ -702,6 +790,7 @@ int fr_create(const char* architecture, const char* model_type, int device, int 
   h->arcface = mt == "arcface";
   h->device = device;
   h->max_batch = max_batch;
+  h->lane_min = detector ? 0 : FR_LANES_DEFAULT;
   h->specs = specs;
   h->detector = detector;
   h->expected = detector ? detector_schema() : h->arcface ? schema_arcface(specs) : schema(specs);
@@ -1336,6 +1425,15 @@ int fr_set_graph_batch(fr_handle* h, int max_n) {
   DeviceGuard dg(h->device);
   h->graph_max_n = max_n;
   clear_graphs(h);
+  return FR_OK;
+}
+
+int fr_set_lanes(fr_handle* h, int min_n) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (h->detector) return fail(h, FR_ERR_STATE, "this handle is a detector (scrfd_10g)");
+  if (min_n < 0) return fail(h, FR_ERR_INVALID_ARGUMENT, "min_n must be >= 0 (0: one lane)");
+  h->lane_min = min_n;
   return FR_OK;
 }
 

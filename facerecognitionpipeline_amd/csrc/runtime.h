@@ -45,6 +45,21 @@ struct ProfEvent {
   int kind;
 };
 
+// The buffers one running forward writes (a lane).  Lane 0 is the handle's own workspace; lane 1
+// (fr_set_lanes) is a second set, so the two halves of a large batch run as two concurrent
+// forwards on two streams and one half's part-empty last round of a layer fills with the other
+// half's work.
+struct LaneWs {
+  float* act[3] = {nullptr, nullptr, nullptr};
+  float* sc_buf = nullptr;
+  float* partial = nullptr;
+  float* w4part = nullptr;
+  float* sk_ws = nullptr;
+  long long sk_ws_floats = 0;
+  int* sk_cnt = nullptr;
+  int sk_cnt_cap = 0;
+};
+
 struct Detector;  // detector.cpp
 void detector_destroy(Detector* d);
 // every conv of the detector (for the Winograd filter builds); no-op for d == nullptr
@@ -128,6 +143,14 @@ struct fr_handle {
   float* w4part = nullptr;         // F(4x4) split-K partial outputs (small batches), W4PART_FLOATS
   static constexpr long long W4PART_FLOATS = 16ll << 20;
 
+  // lanes (fr_set_lanes): forwards of n >= lane_min crops run as two concurrent half batches,
+  // lane 0 on the caller's stream with the workspace above, lane 1 on lane_stream with lane1
+  int lane_min = 0;
+  frhip_rt::LaneWs lane1;
+  int lane1_batch = 0;  // crops lane 1's buffers hold
+  hipStream_t lane_stream = nullptr;
+  hipEvent_t lane_fork = nullptr, lane_join = nullptr;
+
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
   frhip_rt::Detector* det = nullptr;
 
@@ -157,6 +180,15 @@ struct fr_handle {
     for (auto e : pool) (void)hipEventDestroy(e);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
+    if (lane_stream) (void)hipStreamDestroy(lane_stream);
+    if (lane_fork) (void)hipEventDestroy(lane_fork);
+    if (lane_join) (void)hipEventDestroy(lane_join);
+    for (auto p : lane1.act) (void)hipFree(p);
+    (void)hipFree(lane1.sc_buf);
+    (void)hipFree(lane1.partial);
+    (void)hipFree(lane1.w4part);
+    (void)hipFree(lane1.sk_ws);
+    (void)hipFree(lane1.sk_cnt);
     (void)hipFree(arena);
     (void)hipFree(wino_arena);
     (void)hipFree(wino4_arena);
@@ -224,8 +256,10 @@ void bn_fold(const std::vector<float>* gamma, const std::vector<float>* beta, co
 std::vector<float> repack_oihw(const std::vector<float>& w, int O, int I, int kh, int kw);
 int ensure_buf(fr_handle* h, void** p, size_t* cap, size_t bytes);
 int ensure_stream_k(int device, int* cus, float** ws, long long* ws_floats, int** cnt, int* cnt_cap);
+// L: the lane whose stream-K / split-K workspace the launch uses (nullptr: the handle's own)
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, frhip::Epi epi,
-             const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s);
+             const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
+             const LaneWs* L = nullptr);
 const std::vector<float>* getp(fr_handle* h, const std::string& k);
 
 // detector.cpp

@@ -54,7 +54,7 @@ class FaceEmbedder:
     def __init__(self, architecture: str = "ir_101", model_path: Optional[str] = None,
                  model_type: str = "adaface", device=None, max_batch: int = 256,
                  state_dict=None, weight_seed: Optional[int] = None, precision: str = "fp32",
-                 conv_algorithm: str = "winograd4", graph_batch: int = 16):
+                 conv_algorithm: str = "winograd4", graph_batch: int = 16, lanes_min: Optional[int] = None):
         self.device = _as_device(device)
         self.model_type = model_type
         self.architecture = architecture
@@ -87,6 +87,10 @@ class FaceEmbedder:
         # captured hipGraph instead of ~100 individual launches (bit-identical results)
         self.graph_batch = min(int(graph_batch), max_batch)
         self.model.set_graph_batch(self.graph_batch)
+        # forwards of n >= lanes_min crops run as two concurrent half-batch lanes (fr_set_lanes;
+        # None keeps the library default, 0 = one lane)
+        if lanes_min is not None:
+            self.model.set_lanes(lanes_min)
         self.input_size = INPUT_SIZE
         # face_embedder.py:60-61 (AdaFace) and :86-87 (ArcFace)
         self.mean, self.std = (0.5, 0.5) if model_type == "adaface" else (127.5, 127.5)

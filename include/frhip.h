@@ -162,8 +162,7 @@ int fr_set_precision(fr_handle* h, int mode);
  * instead of 144, filters transformed once (on selection / at fr_finalize), pre-BN folded
  * into them; embeddings within 1e-5 of the CPU reference (tests).  FR_CONV_WINOGRAD:
  * F(2x2,3x3), 16 products per 2x2 tile instead of 36.  FR_CONV_DIRECT: the implicit-GEMM
- * kernel for every conv.  FR_PRECISION_BF16X3 runs the direct split-bf16 kernel (faster there than
- * the split-bf16 F(4x4) variant, which FRHIP_WINO4_BF=1 selects for experiments). */
+ * kernel for every conv.  FR_PRECISION_BF16X3 runs the direct split-bf16 kernel. */
 #define FR_CONV_DIRECT 0
 #define FR_CONV_WINOGRAD 1
 #define FR_CONV_WINOGRAD4 2
@@ -175,6 +174,16 @@ int fr_set_conv_algorithm(fr_handle* h, int algo);
  * arguments, so bit-identical results).  0 (default) disables; changing the precision, the conv
  * algorithm or the weights drops the captured graphs.  fr_graph_count reports how many exist. */
 int fr_set_graph_batch(fr_handle* h, int max_n);
+
+/* Lanes of a large forward.  With min_n > 0, every forward of n >= min_n crops runs as two
+ * concurrent half batches: the first half on the call's stream, the second on an internal stream
+ * forked from it and joined back before the call returns, each with its own activation and
+ * split-K workspace (allocated on first use, ~1.7 GB for max_batch 256).  Launches alternate
+ * between the halves, so the last, part-empty round of one half's layer runs beside the other
+ * half's launch of the same layer.  Embeddings are those of two forwards of n/2 crops (batch-
+ * invariant to ~1e-6).  0 = one lane.  fr_create's default: FR_LANES_DEFAULT. */
+#define FR_LANES_DEFAULT 128
+int fr_set_lanes(fr_handle* h, int min_n);
 int fr_graph_count(fr_handle* h, int* count);
 
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).

@@ -132,3 +132,38 @@ def test_small_batches_match_oracle(embedder):
     for n in (1, 2, 5):
         got = embedder.embed_tensor(dev[:n].contiguous()).cpu().numpy()
         assert np.abs(got - ref[:n]).max() <= 1e-5, n
+
+
+def test_lanes_equal_two_half_batch_forwards(embedder):
+    """fr_set_lanes: a forward of n >= min_n crops runs as two concurrent half batches, each with
+    its own workspace and stream.  Each half must be bit-identical to a one-lane forward of the
+    same crops, for even and odd n, and the call must stay ordered on the caller's stream."""
+    h = embedder.model
+    crops = torch.from_numpy(W.synthetic_crops(61, seed=W.CROP_SEED_GALLERY)).cuda()
+    try:
+        for n in (40, 61):
+            h.set_lanes(0)
+            n0 = n // 2
+            a = embedder.embed_tensor(crops[:n0]).clone()
+            b = embedder.embed_tensor(crops[n0:n]).clone()
+            h.set_lanes(32)
+            for _ in range(3):  # lane 1's workspace is reused across calls
+                got = embedder.embed_tensor(crops[:n])
+                assert torch.equal(got[:n0], a) and torch.equal(got[n0:], b), n
+        # below min_n: one lane, the same result as with lanes off
+        h.set_lanes(0)
+        one = embedder.embed_tensor(crops[:20]).clone()
+        h.set_lanes(32)
+        assert torch.equal(embedder.embed_tensor(crops[:20]), one)
+        # stream order: a consumer on the caller's stream sees the whole result
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            out = embedder.embed_tensor(crops[:61])
+            total = out.sum()
+        s.synchronize()
+        ref = embedder.embed_tensor(crops[:61])
+        assert torch.equal(out, ref) and total.item() == ref.sum().item()
+        with pytest.raises(ValueError):
+            h.set_lanes(-1)
+    finally:
+        h.set_lanes(0)

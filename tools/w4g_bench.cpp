@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -70,18 +71,52 @@ int main(int argc, char** argv) {
   p.part_floats = part_floats;
   p.sk_mode = argc > 7 ? atoi(argv[7]) : 1;
   p.no_split = argc > 8 ? atoi(argv[8]) : 0;  // 1: whole items only (no tail split-K)
+  // argv[9] lanes: 1 one stream; 2 two streams of B/2 each, launches interleaved (fr_set_lanes)
+  const int nl = argc > 9 ? atoi(argv[9]) : 1;
   p.B = B;
   p.H = H;
   p.W = H;
   p.Cin = Cin;
   p.Cout = Cout;
+  hipStream_t st[2] = {nullptr, nullptr};
+  Wino4Params pl[2] = {p, p};
+  if (nl == 2) {
+    CK(hipStreamCreateWithFlags(&st[0], hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&st[1], hipStreamNonBlocking));
+    const int hb = B / 2;
+    for (int l = 0; l < 2; ++l) {
+      pl[l].B = l ? B - hb : hb;
+      pl[l].x = x + (size_t)l * hb * H * H * Cin;
+      pl[l].y = y + (size_t)l * hb * H * H * Cout;
+      pl[l].res = p.res ? res + (size_t)l * hb * H * H * Cout : nullptr;
+      pl[l].part = nullptr;  // no split-K schedules in the lane experiment
+      pl[l].part_floats = 0;
+    }
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) CK(launch_wino4(p, pre, (Epi)epi, nullptr));
+  auto run = [&](int n) {
+    for (int i = 0; i < n; ++i)
+      for (int l = 0; l < nl; ++l) CK(launch_wino4(pl[l], pre, (Epi)epi, st[l]));
+  };
+  run(3);
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, nullptr));
-  for (int i = 0; i < iters; ++i) CK(launch_wino4(p, pre, (Epi)epi, nullptr));
+  if (nl == 2) {  // fork both streams from the null stream's event, join back
+    CK(hipStreamWaitEvent(st[0], e0, 0));
+    CK(hipStreamWaitEvent(st[1], e0, 0));
+  }
+  run(iters);
+  if (nl == 2) {
+    hipEvent_t j0, j1;
+    CK(hipEventCreate(&j0));
+    CK(hipEventCreate(&j1));
+    CK(hipEventRecord(j0, st[0]));
+    CK(hipEventRecord(j1, st[1]));
+    CK(hipStreamWaitEvent(nullptr, j0, 0));
+    CK(hipStreamWaitEvent(nullptr, j1, 0));
+  }
   CK(hipEventRecord(e1, nullptr));
   CK(hipEventSynchronize(e1));
   float t = 0;
@@ -89,7 +124,7 @@ int main(int argc, char** argv) {
   Wino4Params c = p;
   wino4_canvas(c);
   const double exec = 2.0 * 36.0 * c.ntiles * (double)Cin * Cout;
-  printf("B=%d H=%d %d->%d epi=%d: %.1f us (%.1f TF executed)\n", B, H, Cin, Cout, epi, 1e3 * t / iters,
+  printf("B=%d H=%d %d->%d epi=%d lanes=%d: %.1f us (%.1f TF executed)\n", B, H, Cin, Cout, epi, nl, 1e3 * t / iters,
          exec / (1e-3 * t / iters) / 1e12);
   return 0;
 }

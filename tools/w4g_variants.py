@@ -19,7 +19,7 @@ SHAPES = [(256, 14, 256, 256, 2), (256, 14, 256, 256, 1), (256, 28, 128, 128, 2)
           (256, 7, 512, 512, 2)]
 
 EPI_START = "    // an idle quarter (!live, Cout % 64 != 0) runs the epilogue too"
-EPI_END = "\n  }\n}\n\n// Split-K finish"
+EPI_END = "\n  }\n}\n\n// G g G^T"
 MFMA8 = "".join(f"        acc[x{o}] = __builtin_amdgcn_mfma_f32_16x16x4f32(u{e}.{c}, a{e}.{c}, acc[x{o}], 0, 0, 0);\n"
                 for c in "xyzw" for e, o in ((0, ""), (1, " + 1")))
 ULOAD = """          uring[y % URING] = y + URING < NXI ? ld4(ur, lo, (y + URING) * XS + cur)
