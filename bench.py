@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--conv-algorithm", choices=["winograd4", "winograd", "direct"], default="winograd4",
                     help="stride-1 3x3 convs: Winograd F(4x4,3x3), F(2x2,3x3) or the direct implicit GEMM (all f32)")
     ap.add_argument("--lanes-min", type=int, default=None,
-                    help="forwards of n >= this many crops run as two half-batch lanes (0: one lane; default: library's)")
+                    help="a forward of n >= 2x this many crops runs as two concurrent halves (0: one lane; default: library's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=None,

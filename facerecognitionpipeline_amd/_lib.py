@@ -50,7 +50,7 @@ _SIGNATURES = {
     "fr_set_precision": (_I, [_P, _I]),
     "fr_set_conv_algorithm": (_I, [_P, _I]),
     "fr_set_graph_batch": (_I, [_P, _I]),
-    "fr_set_lanes": (_I, [_P, _I]),
+    "fr_set_lanes": (_I, [_P, _I, _I]),
     "fr_graph_count": (_I, [_P, ctypes.POINTER(ctypes.c_int)]),
     "fr_profile_enable": (_I, [_P, _I]),
     "fr_profile_kernel": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -272,9 +272,9 @@ class Handle:
         """Replay forwards of n <= max_n crops as captured hipGraphs (0 disables)."""
         check(self._lib.fr_set_graph_batch(self.h, int(max_n)), self.h)
 
-    def set_lanes(self, min_n: int) -> None:
-        """Run forwards of n >= min_n crops as two concurrent half-batch lanes (0: one lane)."""
-        check(self._lib.fr_set_lanes(self.h, int(min_n)), self.h)
+    def set_lanes(self, min_n: int, max_lanes: int = 2) -> None:
+        """Run a forward of n crops as min(max_lanes, n // min_n) concurrent parts (0: one lane)."""
+        check(self._lib.fr_set_lanes(self.h, int(min_n), int(max_lanes)), self.h)
 
     def graph_count(self) -> int:
         c = ctypes.c_int()

@@ -403,10 +403,10 @@ LaneWs lane0_ws(fr_handle* h) {
   return L;
 }
 
-// Lane 1's workspace for up to `batch` crops, its stream and the fork / join events.
-int ensure_lane1(fr_handle* h, int batch) {
-  LaneWs& L = h->lane1;
-  if (h->lane1_batch < batch) {
+// Lane l's (>= 1) workspace for up to `batch` crops, its stream and its join event.
+int ensure_lane(fr_handle* h, int l, int batch) {
+  LaneWs& L = h->lane_ws[l];
+  if (h->lane_batch[l] < batch) {
     for (auto& a : L.act) {
       if (a) FR_HIP(h, hipFree(a));
       a = nullptr;
@@ -414,19 +414,19 @@ int ensure_lane1(fr_handle* h, int batch) {
     if (L.sc_buf) FR_HIP(h, hipFree(L.sc_buf));
     if (L.partial) FR_HIP(h, hipFree(L.partial));
     L.sc_buf = L.partial = nullptr;
-    h->lane1_batch = 0;
+    h->lane_batch[l] = 0;
     const size_t mb = batch;
     for (auto& a : L.act) FR_HIP(h, hipMalloc((void**)&a, mb * 112 * 112 * 64 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&L.sc_buf, mb * 56 * 56 * 64 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&L.partial, (size_t)h->head_split * mb * 512 * sizeof(float)));
-    h->lane1_batch = batch;
+    h->lane_batch[l] = batch;
   }
   if (!L.w4part) FR_HIP(h, hipMalloc((void**)&L.w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
   if (ensure_stream_k(h->device, &h->cus, &L.sk_ws, &L.sk_ws_floats, &L.sk_cnt, &L.sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
-  if (!h->lane_stream) FR_HIP(h, hipStreamCreateWithFlags(&h->lane_stream, hipStreamNonBlocking));
+  if (!h->lane_stream[l]) FR_HIP(h, hipStreamCreateWithFlags(&h->lane_stream[l], hipStreamNonBlocking));
   if (!h->lane_fork) FR_HIP(h, hipEventCreateWithFlags(&h->lane_fork, hipEventDisableTiming));
-  if (!h->lane_join) FR_HIP(h, hipEventCreateWithFlags(&h->lane_join, hipEventDisableTiming));
+  if (!h->lane_join[l]) FR_HIP(h, hipEventCreateWithFlags(&h->lane_join[l], hipEventDisableTiming));
   return FR_OK;
 }
 
@@ -487,29 +487,44 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
 }
 
 // One forward of up to max_batch crops: rgb (device) -> out (device) [n][512].  With lanes on
-// (fr_set_lanes) and n >= lane_min, the batch runs as two halves: lane 1 forks from s and joins
-// back into it, so the call is stream-ordered on s like a single forward.  Profiled forwards stay
-// one lane (their per-launch events would overlap).
+// (fr_set_lanes), the batch runs as nl = min(lane_max, n / lane_min) near-equal parts: lanes
+// 1 .. nl - 1 fork from s and join back into it, so the call is stream-ordered on s like a single
+// forward.  Profiled forwards stay one lane (their per-launch events would overlap).
 int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int normalize, hipStream_t s) {
   const LaneWs L0 = lane0_ws(h);
-  if (h->lane_min <= 0 || n < h->lane_min || n < 2 || h->prof) {
+  const int nl = (h->lane_min <= 0 || h->prof) ? 1 : std::max(1, std::min(h->lane_max, n / h->lane_min));
+  if (nl == 1) {
     const int off = 0;
     return forward_lanes(h, rgb, &off, &n, 1, out, normalize, &s, &L0);
   }
-  const int n0 = n / 2, n1 = n - n0;
-  int rc = ensure_lane1(h, std::max(n1, (h->max_batch + 1) / 2));
-  if (rc) return rc;
-  const int off[2] = {0, n0}, cnt[2] = {n0, n1};
-  const hipStream_t st[2] = {s, h->lane_stream};
-  const LaneWs L[2] = {L0, h->lane1};
+  int off[MAX_LANES], cnt[MAX_LANES];
+  hipStream_t st[MAX_LANES];
+  LaneWs L[MAX_LANES];
+  // lane buffers sized for the largest part of a max_batch forward, so they are made once
+  const int cap = (h->max_batch + nl - 1) / nl;
+  for (int l = 0, o = 0; l < nl; ++l) {
+    cnt[l] = n / nl + (l < n % nl ? 1 : 0);
+    off[l] = o;
+    o += cnt[l];
+    if (l > 0) {
+      const int rc = ensure_lane(h, l, std::max(cnt[l], cap));
+      if (rc) return rc;
+    }
+    st[l] = l ? h->lane_stream[l] : s;
+    L[l] = l ? h->lane_ws[l] : L0;
+  }
   FR_HIP(h, hipEventRecord(h->lane_fork, s));
-  FR_HIP(h, hipStreamWaitEvent(h->lane_stream, h->lane_fork, 0));
-  rc = forward_lanes(h, rgb, off, cnt, 2, out, normalize, st, L);
+  for (int l = 1; l < nl; ++l) FR_HIP(h, hipStreamWaitEvent(st[l], h->lane_fork, 0));
+  const int rc = forward_lanes(h, rgb, off, cnt, nl, out, normalize, st, L);
   // join even after a failed launch, so that nothing of this call is left unordered behind s
-  const hipError_t e1 = hipEventRecord(h->lane_join, h->lane_stream);
-  const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(s, h->lane_join, 0) : e1;
+  hipError_t e = hipSuccess;
+  for (int l = 1; l < nl; ++l) {
+    hipError_t e1 = hipEventRecord(h->lane_join[l], st[l]);
+    if (e1 == hipSuccess) e1 = hipStreamWaitEvent(s, h->lane_join[l], 0);
+    if (e == hipSuccess) e = e1;
+  }
   if (rc) return rc;
-  FR_HIP(h, e2);
+  FR_HIP(h, e);
   return FR_OK;
 }
 
@@ -790,7 +805,8 @@ int fr_create(const char* architecture, const char* model_type, int device, int 
   h->arcface = mt == "arcface";
   h->device = device;
   h->max_batch = max_batch;
-  h->lane_min = detector ? 0 : FR_LANES_DEFAULT;
+  h->lane_min = detector ? 0 : FR_LANES_MIN_DEFAULT;
+  h->lane_max = FR_LANES_MAX_DEFAULT;
   h->specs = specs;
   h->detector = detector;
   h->expected = detector ? detector_schema() : h->arcface ? schema_arcface(specs) : schema(specs);
@@ -1428,12 +1444,14 @@ int fr_set_graph_batch(fr_handle* h, int max_n) {
   return FR_OK;
 }
 
-int fr_set_lanes(fr_handle* h, int min_n) {
+int fr_set_lanes(fr_handle* h, int min_n, int max_lanes) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
   if (h->detector) return fail(h, FR_ERR_STATE, "this handle is a detector (scrfd_10g)");
   if (min_n < 0) return fail(h, FR_ERR_INVALID_ARGUMENT, "min_n must be >= 0 (0: one lane)");
+  if (max_lanes < 1 || max_lanes > MAX_LANES) return fail(h, FR_ERR_INVALID_ARGUMENT, "max_lanes must be in [1, 4]");
   h->lane_min = min_n;
+  h->lane_max = max_lanes;
   return FR_OK;
 }
 

@@ -45,10 +45,10 @@ struct ProfEvent {
   int kind;
 };
 
-// The buffers one running forward writes (a lane).  Lane 0 is the handle's own workspace; lane 1
-// (fr_set_lanes) is a second set, so the two halves of a large batch run as two concurrent
-// forwards on two streams and one half's part-empty last round of a layer fills with the other
-// half's work.
+// The buffers one running forward writes (a lane).  Lane 0 is the handle's own workspace; lanes
+// 1 .. MAX_LANES - 1 (fr_set_lanes) are further sets, so the parts of a large batch run as
+// concurrent forwards on their own streams and one part's part-empty last round of a layer fills
+// with another part's work.
 struct LaneWs {
   float* act[3] = {nullptr, nullptr, nullptr};
   float* sc_buf = nullptr;
@@ -59,6 +59,7 @@ struct LaneWs {
   int* sk_cnt = nullptr;
   int sk_cnt_cap = 0;
 };
+constexpr int MAX_LANES = 4;
 
 struct Detector;  // detector.cpp
 void detector_destroy(Detector* d);
@@ -143,13 +144,15 @@ struct fr_handle {
   float* w4part = nullptr;         // F(4x4) split-K partial outputs (small batches), W4PART_FLOATS
   static constexpr long long W4PART_FLOATS = 16ll << 20;
 
-  // lanes (fr_set_lanes): forwards of n >= lane_min crops run as two concurrent half batches,
-  // lane 0 on the caller's stream with the workspace above, lane 1 on lane_stream with lane1
-  int lane_min = 0;
-  frhip_rt::LaneWs lane1;
-  int lane1_batch = 0;  // crops lane 1's buffers hold
-  hipStream_t lane_stream = nullptr;
-  hipEvent_t lane_fork = nullptr, lane_join = nullptr;
+  // lanes (fr_set_lanes): a forward of n crops runs as min(lane_max, n / lane_min) concurrent
+  // parts, lane 0 on the caller's stream with the workspace above, lane l >= 1 on lane_stream[l]
+  // with lane_ws[l]
+  int lane_min = 0, lane_max = 1;
+  frhip_rt::LaneWs lane_ws[frhip_rt::MAX_LANES];
+  int lane_batch[frhip_rt::MAX_LANES] = {0, 0, 0, 0};  // crops lane l's buffers hold
+  hipStream_t lane_stream[frhip_rt::MAX_LANES] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t lane_fork = nullptr;
+  hipEvent_t lane_join[frhip_rt::MAX_LANES] = {nullptr, nullptr, nullptr, nullptr};
 
   // SCRFD detector (arch "scrfd_10g"): layers, workspace (detector.cpp)
   frhip_rt::Detector* det = nullptr;
@@ -180,15 +183,18 @@ struct fr_handle {
     for (auto e : pool) (void)hipEventDestroy(e);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
-    if (lane_stream) (void)hipStreamDestroy(lane_stream);
     if (lane_fork) (void)hipEventDestroy(lane_fork);
-    if (lane_join) (void)hipEventDestroy(lane_join);
-    for (auto p : lane1.act) (void)hipFree(p);
-    (void)hipFree(lane1.sc_buf);
-    (void)hipFree(lane1.partial);
-    (void)hipFree(lane1.w4part);
-    (void)hipFree(lane1.sk_ws);
-    (void)hipFree(lane1.sk_cnt);
+    for (int l = 1; l < frhip_rt::MAX_LANES; ++l) {
+      if (lane_stream[l]) (void)hipStreamDestroy(lane_stream[l]);
+      if (lane_join[l]) (void)hipEventDestroy(lane_join[l]);
+      frhip_rt::LaneWs& L = lane_ws[l];
+      for (auto p : L.act) (void)hipFree(p);
+      (void)hipFree(L.sc_buf);
+      (void)hipFree(L.partial);
+      (void)hipFree(L.w4part);
+      (void)hipFree(L.sk_ws);
+      (void)hipFree(L.sk_cnt);
+    }
     (void)hipFree(arena);
     (void)hipFree(wino_arena);
     (void)hipFree(wino4_arena);

@@ -87,7 +87,7 @@ class FaceEmbedder:
         # captured hipGraph instead of ~100 individual launches (bit-identical results)
         self.graph_batch = min(int(graph_batch), max_batch)
         self.model.set_graph_batch(self.graph_batch)
-        # forwards of n >= lanes_min crops run as two concurrent half-batch lanes (fr_set_lanes;
+        # a forward of n >= 2 * lanes_min crops runs as two concurrent halves (fr_set_lanes;
         # None keeps the library default, 0 = one lane)
         if lanes_min is not None:
             self.model.set_lanes(lanes_min)

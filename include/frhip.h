@@ -175,15 +175,20 @@ int fr_set_conv_algorithm(fr_handle* h, int algo);
  * algorithm or the weights drops the captured graphs.  fr_graph_count reports how many exist. */
 int fr_set_graph_batch(fr_handle* h, int max_n);
 
-/* Lanes of a large forward.  With min_n > 0, every forward of n >= min_n crops runs as two
- * concurrent half batches: the first half on the call's stream, the second on an internal stream
- * forked from it and joined back before the call returns, each with its own activation and
- * split-K workspace (allocated on first use, ~1.7 GB for max_batch 256).  Launches alternate
- * between the halves, so the last, part-empty round of one half's layer runs beside the other
- * half's launch of the same layer.  Embeddings are those of two forwards of n/2 crops (batch-
- * invariant to ~1e-6).  0 = one lane.  fr_create's default: FR_LANES_DEFAULT. */
-#define FR_LANES_DEFAULT 128
-int fr_set_lanes(fr_handle* h, int min_n);
+/* Lanes of a large forward.  With min_n > 0, a forward of n crops runs as
+ * min(max_lanes, n / min_n) concurrent parts of near-equal size (n < 2 * min_n: one part;
+ * max_lanes in [1, 4]): the first
+ * part on the call's stream, the others on internal streams forked from it and joined back
+ * before the call returns, each with its own activation and split-K workspace (allocated on first
+ * use, ~1 GB per extra lane of 64 crops).  Launches alternate between the parts, so the last,
+ * part-empty round of one part's layer runs beside another part's launch of the same layer.
+ * Embeddings are those of separate forwards of the parts (batch-invariant to ~1e-6).
+ * min_n 0 = one lane.  fr_create's default: FR_LANES_MIN_DEFAULT crops per lane, at most
+ * FR_LANES_MAX_DEFAULT lanes (measured on MI355X, IR-101 C3: batch 256 as 2 x 128 +6%, as 3 or 4
+ * parts -1..-2%; batch 128 as 2 x 64 +8%; batch 64 as 2 x 32 -6%). */
+#define FR_LANES_MIN_DEFAULT 64
+#define FR_LANES_MAX_DEFAULT 2
+int fr_set_lanes(fr_handle* h, int min_n, int max_lanes);
 int fr_graph_count(fr_handle* h, int* count);
 
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).

@@ -134,26 +134,27 @@ def test_small_batches_match_oracle(embedder):
         assert np.abs(got - ref[:n]).max() <= 1e-5, n
 
 
-def test_lanes_equal_two_half_batch_forwards(embedder):
-    """fr_set_lanes: a forward of n >= min_n crops runs as two concurrent half batches, each with
-    its own workspace and stream.  Each half must be bit-identical to a one-lane forward of the
-    same crops, for even and odd n, and the call must stay ordered on the caller's stream."""
+def test_lanes_equal_separate_part_forwards(embedder):
+    """fr_set_lanes(min_n): a forward of n crops runs as min(4, n // min_n) concurrent parts of
+    near-equal size, each with its own workspace and stream.  Each part must be bit-identical to
+    a one-lane forward of the same crops, and the call must stay ordered on the caller's stream."""
     h = embedder.model
-    crops = torch.from_numpy(W.synthetic_crops(61, seed=W.CROP_SEED_GALLERY)).cuda()
+    crops = torch.from_numpy(W.synthetic_crops(64, seed=W.CROP_SEED_GALLERY)).cuda()
     try:
-        for n in (40, 61):
+        for n, nl in ((40, 2), (61, 3), (64, 4)):
+            cnt = [n // nl + (1 if l < n % nl else 0) for l in range(nl)]
+            offs = np.cumsum([0] + cnt)
             h.set_lanes(0)
-            n0 = n // 2
-            a = embedder.embed_tensor(crops[:n0]).clone()
-            b = embedder.embed_tensor(crops[n0:n]).clone()
-            h.set_lanes(32)
-            for _ in range(3):  # lane 1's workspace is reused across calls
+            parts = [embedder.embed_tensor(crops[offs[l]:offs[l + 1]]).clone() for l in range(nl)]
+            h.set_lanes(16, 4)
+            for _ in range(3):  # the lanes' workspaces are reused across calls
                 got = embedder.embed_tensor(crops[:n])
-                assert torch.equal(got[:n0], a) and torch.equal(got[n0:], b), n
-        # below min_n: one lane, the same result as with lanes off
+                for l in range(nl):
+                    assert torch.equal(got[offs[l]:offs[l + 1]], parts[l]), (n, l)
+        # fewer than 2 * min_n crops: one lane, the same result as with lanes off
         h.set_lanes(0)
         one = embedder.embed_tensor(crops[:20]).clone()
-        h.set_lanes(32)
+        h.set_lanes(16, 4)
         assert torch.equal(embedder.embed_tensor(crops[:20]), one)
         # stream order: a consumer on the caller's stream sees the whole result
         s = torch.cuda.Stream()
@@ -165,5 +166,7 @@ def test_lanes_equal_two_half_batch_forwards(embedder):
         assert torch.equal(out, ref) and total.item() == ref.sum().item()
         with pytest.raises(ValueError):
             h.set_lanes(-1)
+        with pytest.raises(ValueError):
+            h.set_lanes(16, 5)
     finally:
         h.set_lanes(0)

@@ -49,7 +49,43 @@ def noepi(s):
     return s[:a] + dummy + s[b:]
 
 
+STORE = "__builtin_amdgcn_raw_buffer_store_b128(bits, yr, oo[y][x], 0, 0);"
+GEO_LINE = "      const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;\n      int roff[6], coff[3];"
+WARM = """
+      // warm L2 with this item's residual rows (one pixel = 64 couts = two 128-B lines per lane)
+      if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU)
+        if (!SPLIT && j <= t_last) {
+          const int px = half * 8 + pr, yy = px >> 2, xx = px & 3;
+          int rs2, cs2;
+          const int y2 = canvas_coord(4 * tr + yy, ir0, p.Pr, H, sep_r, rs2);
+          const int x2 = canvas_coord(4 * tc + xx, ic0, p.Pc, W, sep_c, cs2);
+          if (y2 >= 0 && rs2 * p.NC < p.B && T < p.ntiles && x2 >= 0 && cs2 < p.NC) {
+            const int pix = (rs2 * p.NC * H + y2) * W + cs2 * H * W + x2;
+            const int off = (pix * Cout + it.nb * 64) * 4;
+            sink += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, off, 0, 0)) +
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, off + 128, 0, 0));
+          }
+        }
+"""
+
+
+def reswarm(s):
+    assert GEO_LINE in s
+    s = s.replace(GEO_LINE, GEO_LINE.replace("\n      int roff", WARM + "      int roff"), 1)
+    a = "    float rowm[6], colm[3];\n"
+    assert a in s
+    s = s.replace(a, a + "    float sink = 0.f;\n    const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(p.res, p.res ? p.B * H * W * Cout * 4 : 0);\n", 1)
+    a = "    lds_barrier();  // barrier G: the MFMA waves close their last K-step with it\n    return;"
+    assert a in s
+    return s.replace(a, "    lds_barrier();  // barrier G: the MFMA waves close their last K-step with it\n"
+                        "    if (sink == 1234.5f) ring[tid] = sink;\n    return;")
+
+
 VARIANTS = {
+    "st_nt": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 2);")),
+    "st_sc1": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 16);")),
+    "st_sc01": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 17);")),
+    "reswarm": reswarm,
     "base": lambda s: s,
     "noepi": noepi,
     "notrans": notrans,
