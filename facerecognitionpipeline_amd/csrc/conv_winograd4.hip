@@ -97,11 +97,18 @@ __device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, int off, int soff = 
   return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
 }
 
-// 16-byte slot of A-fragment lane l = 16 k + i in a ring plane: tile bits 2-3 XOR k.  The
-// fragment reads stay one permuted 16-lane row per k (conflict-free ds_read_b128); the
-// transform waves' scalar stores (4 tiles x 16 channels per wave) spread over all 64 banks
-// instead of 16.
-__device__ __forceinline__ int vslot(int l) { return l ^ ((l >> 4) << 2); }
+// 16-byte slot of fragment lane l = 16 k + i (k: channel quad, i: tile) in a ring plane:
+// i XOR c(k), c = 0, 2, 12, 14.  ds_read_b128 serves a wave in four 16-lane groups
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) over 64 banks: c(k) keeps bits 3 and 2 of i
+// equal-or-opposite as they were, so each group still reads 16 distinct slot columns.
+// ds_write_b64 serves 16 contiguous lanes at a time over 32 banks: a transform wave's group is
+// 2 tiles x 4 channel quads x 2 channel pairs, and c(k) gives the 4 quads distinct bits 1-2 of
+// the slot, so its 32 dwords hit 32 banks (i XOR 4k, the previous map, left 2-way conflicts on
+// both sides: SQ_LDS_BANK_CONFLICT ~10% of the kernel's cycles).
+__device__ __forceinline__ int vslot(int l) {
+  const int k = l >> 4;
+  return l ^ ((k & 1) * 2 + (k >> 1) * 12);
+}
 
 // Workgroup barrier that waits for this wave's LDS operations only: global loads issued ahead
 // (U fragments, the next turn's patches) stay in flight across it.
