@@ -38,6 +38,8 @@
 // Numerics: exact f32 products, f32 accumulation (MFMA = fmaf chain), only the
 // k summation order differs from the CPU reference.
 #pragma once
+#include <type_traits>
+
 #include "frhip_kernels.h"
 
 namespace frhip {
@@ -163,35 +165,43 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
       b_base[j] = n < p.Cout ? (n * Ktot + 4 * k4) * 4 : OOB;
     }
 
+    // counters of the next step to load
     int tap = s_begin % taps;
     int cc = s_begin / taps;
     int ky = tap / p.KW;
     int kx = tap - ky * p.KW;
-    float4 ra[A_IT], rb[B_IT];
-    float4 psc = make_float4(1.f, 1.f, 1.f, 1.f), psh = make_float4(0.f, 0.f, 0.f, 0.f);
-    unsigned a_okm = 0;
+    // DEEP (tiles with <= 32 accumulators per lane, where the registers are there): global loads
+    // run two K-steps ahead of the MFMAs: step t is loaded into register set (t - s_begin) & 1
+    // two iterations before it is computed and written to LDS buffer (t - s_begin) & 1 at the end
+    // of the iteration before (the layers with the largest inputs stream them from HBM, whose
+    // latency under load is more than one step of MFMAs).  Otherwise one set, one step ahead.
+    constexpr bool DEEP = ACC <= 32;
+    float4 ra[2][A_IT], rb[2][B_IT];
+    float4 psc[2] = {make_float4(1.f, 1.f, 1.f, 1.f), make_float4(1.f, 1.f, 1.f, 1.f)};
+    float4 psh[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    unsigned a_okm[2] = {0, 0};
 
-    auto load_step = [&](bool live) {
+    auto load_step = [&](int r, bool live) {
       const int c0 = cc * BK;
       const int tap_off = ((ky * W + kx) * Cin + c0) * 4;
-      a_okm = 0;
+      a_okm[r] = 0;
 #pragma unroll
       for (int i = 0; i < A_IT; ++i) {
         const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
         const unsigned ok =
             (unsigned)live & (unsigned)((unsigned)iy < (unsigned)H) & (unsigned)((unsigned)ix < (unsigned)W);
-        a_okm |= ok << i;
-        ra[i] = ld4(xr, ok ? a_base[i] + tap_off : OOB);
+        a_okm[r] |= ok << i;
+        ra[r][i] = ld4(xr, ok ? a_base[i] + tap_off : OOB);
       }
       const int koff = (tap * Cin + c0) * 4;
 #pragma unroll
-      for (int j = 0; j < B_IT; ++j) rb[j] = ld4(wr, (b_base[j] == OOB || !live) ? OOB : b_base[j] + koff);
+      for (int j = 0; j < B_IT; ++j) rb[r][j] = ld4(wr, (b_base[j] == OOB || !live) ? OOB : b_base[j] + koff);
       if constexpr (PRE) {
-        psc = *reinterpret_cast<const float4*>(p.pre_scale + c0 + 4 * k4);
-        psh = *reinterpret_cast<const float4*>(p.pre_shift + c0 + 4 * k4);
+        psc[r] = *reinterpret_cast<const float4*>(p.pre_scale + c0 + 4 * k4);
+        psh[r] = *reinterpret_cast<const float4*>(p.pre_shift + c0 + 4 * k4);
       }
     };
-    // counters of step s+1; frozen on the last step (its loads are OOB no-ops)
+    // counters of the next step; frozen past the segment's end (those loads are OOB no-ops)
     auto advance = [&](bool live) {
       const int kx1 = kx + 1 == p.KW ? 0 : kx + 1;
       const int ky1 = kx + 1 == p.KW ? (ky + 1 == p.KH ? 0 : ky + 1) : ky;
@@ -202,19 +212,19 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
       tap = live ? tap1 : tap;
       cc = live ? cc1 : cc;
     };
-    auto store_step = [&](int buf) {
+    auto store_step = [&](int r, int buf) {
       float* As = As0 + buf * BUF;
       float* Bs = Bs0 + buf * BUF;
 #pragma unroll
       for (int i = 0; i < A_IT; ++i) {
-        float4 v = ra[i];
+        float4 v = ra[r][i];
         if constexpr (PRE) {
           // BN(x) only where the tap is inside the image: padded zeros stay zero.
-          if (a_okm & (1u << i)) {
-            v.x = v.x * psc.x + psh.x;
-            v.y = v.y * psc.y + psh.y;
-            v.z = v.z * psc.z + psh.z;
-            v.w = v.w * psc.w + psh.w;
+          if (a_okm[r] & (1u << i)) {
+            v.x = v.x * psc[r].x + psh[r].x;
+            v.y = v.y * psc[r].y + psh[r].y;
+            v.z = v.z * psc[r].z + psh[r].z;
+            v.w = v.w * psc[r].w + psh[r].w;
           }
         }
         if constexpr (SPLIT)
@@ -225,23 +235,35 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
 #pragma unroll
       for (int j = 0; j < B_IT; ++j) {
         if constexpr (SPLIT)
-          split_store(Bs + (rsub + RPP * j) * ROWF, k4, rb[j]);
+          split_store(Bs + (rsub + RPP * j) * ROWF, k4, rb[r][j]);
         else
-          *reinterpret_cast<float4*>(Bs + (rsub + RPP * j) * LDK + 4 * k4) = rb[j];
+          *reinterpret_cast<float4*>(Bs + (rsub + RPP * j) * LDK + 4 * k4) = rb[r][j];
       }
     };
 
-    load_step(true);
-    store_step(0);
+    load_step(0, true);  // step s_begin
+    advance(s_begin + 1 < s_end);
+    if constexpr (DEEP) {
+      load_step(1, s_begin + 1 < s_end);  // step s_begin + 1
+      advance(s_begin + 2 < s_end);
+    }
+    store_step(0, 0);
     __syncthreads();
-    int buf = 0;
-    for (int s = s_begin; s < s_end; ++s) {
-      const bool live = (s + 1) < s_end;
-      advance(live);
-      load_step(live);
+    // iteration for step s from LDS buffer `buf`; DEEP: register set R = buf = (s - s_begin) & 1
+    // (compile time), else set 0
+    auto iteration = [&](auto Rc, int s, int buf) {
+      constexpr int R = decltype(Rc)::value;
+      const int cb = DEEP ? R : buf;
+      if constexpr (DEEP) {
+        load_step(R, s + 2 < s_end);  // step s + 2 into the set step s was staged from
+        advance(s + 3 < s_end);
+      } else {
+        load_step(0, s + 1 < s_end);
+        advance(s + 2 < s_end);
+      }
       if constexpr (!SPLIT) {
-        const float* Ab = As0 + buf * BUF + (wm * TM * 32 + frag_row) * LDK + frag_k;
-        const float* Bb = Bs0 + buf * BUF + (wn * TN * 32 + frag_row) * LDK + frag_k;
+        const float* Ab = As0 + cb * BUF + (wm * TM * 32 + frag_row) * LDK + frag_k;
+        const float* Bb = Bs0 + cb * BUF + (wn * TN * 32 + frag_row) * LDK + frag_k;
         float4 fa[BK / 8][TM], fb[BK / 8][TN];
 #pragma unroll
         for (int g = 0; g < BK / 8; ++g) {
@@ -263,9 +285,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
       } else {
         // bf16x3: x = hi + lo (bf16 each); x.y ~= hi.hi + hi.lo + lo.hi, f32 accumulation.
         // Lane (r, h) reads 8 consecutive k (16 B) of hi and of lo for each 16-k group.
-        const char* Ab = reinterpret_cast<const char*>(As0 + buf * BUF + (wm * TM * 32 + frag_row) * ROWF) +
+        const char* Ab = reinterpret_cast<const char*>(As0 + cb * BUF + (wm * TM * 32 + frag_row) * ROWF) +
                          16 * (lane >> 5);
-        const char* Bb = reinterpret_cast<const char*>(Bs0 + buf * BUF + (wn * TN * 32 + frag_row) * ROWF) +
+        const char* Bb = reinterpret_cast<const char*>(Bs0 + cb * BUF + (wn * TN * 32 + frag_row) * ROWF) +
                          16 * (lane >> 5);
         bf16x8 ah[BK / 16][TM], al[BK / 16][TM], bh[BK / 16][TN], bl[BK / 16][TN];
 #pragma unroll
@@ -300,10 +322,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
               acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[g][a], bh[g][b], acc[a][b], 0, 0, 0);
         }
       }
-      store_step(buf ^ 1);
+      // step s + 1 (loaded one iteration ago) into the other LDS buffer, free since the barrier
+      // that closed step s - 1
+      store_step(DEEP ? R ^ 1 : 0, cb ^ 1);
       // Schedule (MFMA f32 = 64 pipe cycles; other instructions issue in its shadow):
       //   fragments of groups 0-1 | 1 MFMA + 1 global load, x loads | fragments of groups 2-3 |
-      //   MFMAs | 2 MFMA + 1 LDS write, x writes (the loads had the whole step to land)
+      //   MFMAs | 2 MFMA + 1 LDS write, x writes (the loads have two steps to land)
       constexpr int NMFMA = SPLIT ? (BK / 16) * 3 * TM * TN : (BK / 2) * TM * TN;
       constexpr int NLD = A_IT + B_IT + (PRE ? 2 : 0);
       constexpr int NDSR = SPLIT ? (BK / 16) * 2 * (TM + TN) : (BK / 8) * (TM + TN);
@@ -326,7 +350,18 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
         }
       }
       __syncthreads();
-      buf ^= 1;
+    };
+    if constexpr (DEEP) {
+      for (int s = s_begin; s < s_end; s += 2) {
+        iteration(std::integral_constant<int, 0>(), s, 0);
+        if (s + 1 < s_end) iteration(std::integral_constant<int, 1>(), s + 1, 1);
+      }
+    } else {
+      int buf = 0;
+      for (int s = s_begin; s < s_end; ++s) {
+        iteration(std::integral_constant<int, 0>(), s, buf);
+        buf ^= 1;
+      }
     }
   };
 

@@ -372,11 +372,15 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd launch: ") + hipGetErrorString(e));
     return FR_OK;
   }
+  // Round-2 sweep with loads two K-steps ahead on the <= 32-accumulator tiles
+  // (profiles/r02/sweep_s2.txt): 128x64/W8 also for the 256-channel stride-2 conv2 (111.9 ->
+  // 115.6 TF/s) and 256x128/W8 for the 512-channel shortcut (49.4 -> 63.2).
   ConvTile tile = TILE_256x128_W8;
-  if (cw.cout <= 64 || (cw.cout == 128 && epi == EPI_AFFINE_RES && cw.kh == 3))
+  if (cw.cout <= 64 || (cw.cout == 128 && epi == EPI_AFFINE_RES && cw.kh == 3) ||
+      (cw.cout == 256 && epi == EPI_AFFINE_RES && cw.kh == 3 && cw.stride == 2))
     tile = TILE_128x64_W8;
   else if (cw.kh == 1 && cw.kw == 1 && p.H > 1)
-    tile = TILE_128x128_W8;
+    tile = cw.cout >= 512 ? TILE_256x128_W8 : TILE_128x128_W8;
   else if (p.H == 1)
     tile = TILE_64x128;  // gallery scores (1x1 GEMM)
   // embedding serving batches (M = B*Ho*Wo <= 4096: the stride-2 / 1x1 convs at batch <= ~20):
