@@ -109,13 +109,16 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
 
   const int H = p.H, W = p.W, Cin = p.Cin;
   const int taps = p.KH * p.KW;
-  const int Ktot = taps * Cin;
+  const int Ktot = taps * Cin + p.Cin2;  // weight row length (fused shortcut columns last)
+  const int ncc = Cin / BK;              // channel chunks of the main conv
   const int HoWo = p.Ho * p.Wo;
 
   // Buffer descriptors: an out-of-range offset returns zeros, so padding taps,
   // rows past M and columns past N need no branches (OOB = 0x80000000).
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.B * H * W * Cin * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr2 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.Cin2 ? p.x2 : p.x), (short)0, p.Cin2 ? p.B * H * W * p.Cin2 * 4 : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.Cout * Ktot * 4, 0x00020000);
   constexpr int OOB = 0x80000000;
@@ -140,7 +143,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
     if (s_begin >= s_end) return;
 
     // per-row im2col bases (bytes) for the A rows this thread stages
-    int a_base[A_IT], a_iy[A_IT], a_ix[A_IT];
+    int a_base[A_IT], a_iy[A_IT], a_ix[A_IT], a_base2[A_IT];
+    unsigned a_row = 0;  // rows inside M
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       const int m = m0 + rsub + RPP * i;
@@ -152,10 +156,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
         a_iy[i] = oy * p.stride - p.pad;
         a_ix[i] = ox * p.stride - p.pad;
         a_base[i] = (((b * H + a_iy[i]) * W + a_ix[i]) * Cin + 4 * k4) * 4;
+        a_base2[i] = (((b * H + oy * p.stride) * W + ox * p.stride) * p.Cin2 + 4 * k4) * 4;
+        a_row |= 1u << i;
       } else {
         a_iy[i] = -(1 << 20);
         a_ix[i] = 0;
         a_base[i] = 0;
+        a_base2[i] = 0;
       }
     }
     int b_base[B_IT];
@@ -165,9 +172,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
       b_base[j] = n < p.Cout ? (n * Ktot + 4 * k4) * 4 : OOB;
     }
 
-    // counters of the next step to load
-    int tap = s_begin % taps;
-    int cc = s_begin / taps;
+    // counters of the next step to load (cc >= ncc: fused shortcut chunk cc - ncc, tap 0)
+    const bool in_sc = p.Cin2 > 0 && s_begin >= p.steps1;
+    int tap = in_sc ? 0 : s_begin % taps;
+    int cc = in_sc ? ncc + (s_begin - p.steps1) : s_begin / taps;
     int ky = tap / p.KW;
     int kx = tap - ky * p.KW;
     // DEEP (tiles with <= 32 accumulators per lane, where the registers are there): global loads
@@ -182,6 +190,20 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
     unsigned a_okm[2] = {0, 0};
 
     auto load_step = [&](int r, bool live) {
+      if (p.Cin2 > 0 && cc >= ncc) {  // fused shortcut step: x2 at the output's stride
+        const int c2 = (cc - ncc) * BK;
+        a_okm[r] = 0;
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) {
+          const unsigned ok = (unsigned)live & ((a_row >> i) & 1u);
+          a_okm[r] |= ok << i;
+          ra[r][i] = ld4(xr2, ok ? a_base2[i] + c2 * 4 : OOB);
+        }
+        const int koff2 = (taps * Cin + c2) * 4;
+#pragma unroll
+        for (int j = 0; j < B_IT; ++j) rb[r][j] = ld4(wr, (b_base[j] == OOB || !live) ? OOB : b_base[j] + koff2);
+        return;
+      }
       const int c0 = cc * BK;
       const int tap_off = ((ky * W + kx) * Cin + c0) * 4;
       a_okm[r] = 0;
@@ -203,10 +225,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
     };
     // counters of the next step; frozen past the segment's end (those loads are OOB no-ops)
     auto advance = [&](bool live) {
-      const int kx1 = kx + 1 == p.KW ? 0 : kx + 1;
-      const int ky1 = kx + 1 == p.KW ? (ky + 1 == p.KH ? 0 : ky + 1) : ky;
-      const int tap1 = tap + 1 == taps ? 0 : tap + 1;
-      const int cc1 = tap + 1 == taps ? cc + 1 : cc;
+      const bool sc = p.Cin2 > 0 && cc >= ncc;  // shortcut chunks: one step each, tap 0
+      const int kx1 = sc ? 0 : kx + 1 == p.KW ? 0 : kx + 1;
+      const int ky1 = sc ? 0 : kx + 1 == p.KW ? (ky + 1 == p.KH ? 0 : ky + 1) : ky;
+      const int tap1 = sc ? 0 : tap + 1 == taps ? 0 : tap + 1;
+      const int cc1 = sc || tap + 1 == taps ? cc + 1 : cc;
       kx = live ? kx1 : kx;
       ky = live ? ky1 : ky;
       tap = live ? tap1 : tap;

@@ -44,6 +44,12 @@ struct ConvParams {
   long long sk_ws_floats;
   int* sk_cnt;           // per stream-K tile arrival counters, zero at allocation
   int sk_cnt_cap;
+  // fused 1x1 shortcut (Cin2 > 0): K-steps [steps1, steps_total) read x2 [B][H][W][Cin2] at the
+  // output's stride and no padding, 32 channels per step, against weight columns
+  // KH*KW*Cin .. + Cin2 (w rows are KH*KW*Cin + Cin2 long): conv2 and the block's conv
+  // shortcut as one GEMM (both BN scales folded into the weights, the shifts into post_shift)
+  const float* x2;
+  int Cin2, steps1;
 };
 
 // Tile family of a conv launch.

@@ -270,7 +270,7 @@ static int g_wino4_streamk = 0;
 
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
-             const LaneWs* L) {
+             const LaneWs* L, const float* x2) {
   float* const sk_ws = L ? L->sk_ws : h->sk_ws;
   int* const sk_cnt = L ? L->sk_cnt : h->sk_cnt;
   float* const w4part = L ? L->w4part : h->w4part;
@@ -299,6 +299,12 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   p.res_W = res_W;
   p.M = B * p.Ho * p.Wo;
   p.steps_total = cw.kh * cw.kw * cw.cin / 32;
+  if (cw.cin2 > 0) {
+    p.x2 = x2;
+    p.Cin2 = cw.cin2;
+    p.steps1 = p.steps_total;
+    p.steps_total += cw.cin2 / 32;
+  }
   p.steps_per_split = (p.steps_total + nsplit - 1) / nsplit;
   p.split_stride = split_stride;
   if (h->stream_k && nsplit == 1 && sk_ws) {
@@ -308,7 +314,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     p.sk_cnt = sk_cnt;
     p.sk_cnt_cap = L ? L->sk_cnt_cap : h->sk_cnt_cap;
   }
-  const double flop = 2.0 * p.M * (double)p.Cout * cw.kh * cw.kw * cw.cin;
+  const double flop = 2.0 * p.M * (double)p.Cout * (cw.kh * cw.kw * cw.cin + cw.cin2);
   // Tile per layer shape, from tools/conv_sweep.py on MI355X at B=256 with the stream-K
   // schedule (profiles/r01/sweep.txt): 8-wave 128x64 for the 64-channel
   // stage and the 128-channel residual convs, 8-wave 128x128 for the 1x1 shortcuts,
@@ -462,7 +468,9 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
       float* y = L[l].act[nxt];
       const int n = cnt[l];
       int rc;
-      if (b.has_sc_conv) {
+      if (b.has_sc_conv && h->fuse_shortcut && b.conv2_sc.w) {
+        rc = run_conv(h, b.conv2_sc, r, y, n, HW, HW, EPI_AFFINE, nullptr, 0, 0, 1, 0, st[l], &L[l], x);
+      } else if (b.has_sc_conv) {
         rc = run_conv(h, b.sc, x, L[l].sc_buf, n, HW, HW, EPI_AFFINE, nullptr, 0, 0, 1, 0, st[l], &L[l]);
         if (rc) return rc;
         rc = run_conv(h, b.conv2, r, y, n, HW, HW, EPI_AFFINE_RES, L[l].sc_buf, Ho, Ho, 1, 0, st[l], &L[l]);
@@ -1015,8 +1023,10 @@ int fr_finalize(fr_handle* h) {
     b.conv2.kh = b.conv2.kw = 3;
     b.conv2.stride = s.stride;
     b.conv2.pad = 1;
-    pk.put(&b.conv2.w, repack_oihw(P(k.conv2), s.depth, s.depth, 3, 3));
+    const std::vector<float> w2 = repack_oihw(P(k.conv2), s.depth, s.depth, 3, 3);
+    pk.put(&b.conv2.w, w2);
     bn(k.out_bn, &b.conv2.post_scale, &b.conv2.post_shift);
+    const std::vector<float> sc2 = sc, sh2 = sh;
     // AdaFace: conv shortcut only where the width changes (MaxPool2d(1,2) in stage 1);
     // ArcFace: a conv1x1 downsample on every strided unit
     if (af ? s.stride == 2 : s.cin != s.depth) {
@@ -1028,6 +1038,22 @@ int fr_finalize(fr_handle* h) {
       b.sc.pad = 0;
       pk.put(&b.sc.w, P(k.sc_conv));  // [O][I][1][1] == [O][1][1][I]
       bn(k.sc_bn, &b.sc.post_scale, &b.sc.post_shift);
+      if (s.stride == 2 && s.depth % 32 == 0 && s.cin % 32 == 0) {
+        // fused conv2 + shortcut: y = sum (w2 * s2) r + sum (wsc * s_sc) x + (b2 + b_sc)
+        const auto& wsc = P(k.sc_conv);
+        const int K2 = 9 * s.depth, Kf = K2 + s.cin;
+        std::vector<float> wf((size_t)s.depth * Kf), one(s.depth, 1.f), shf(s.depth);
+        for (int o = 0; o < s.depth; ++o) {
+          for (int q = 0; q < K2; ++q) wf[(size_t)o * Kf + q] = w2[(size_t)o * K2 + q] * sc2[o];
+          for (int c = 0; c < s.cin; ++c) wf[(size_t)o * Kf + K2 + c] = wsc[(size_t)o * s.cin + c] * sc[o];
+          shf[o] = sh2[o] + sh[o];
+        }
+        b.conv2_sc = b.conv2;
+        b.conv2_sc.cin2 = s.cin;
+        pk.put(&b.conv2_sc.w, wf);
+        pk.put(&b.conv2_sc.post_scale, one);
+        pk.put(&b.conv2_sc.post_shift, shf);
+      }
     }
   }
   // head: BN2d(512) as pre-affine; Linear(25088,512) with NCHW-flatten columns
@@ -1613,6 +1639,14 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 static int g_frt_wino4_split = 1;
 int frt_set_wino4_streamk(int on) {
   g_wino4_streamk = on < 0 ? 0 : (on > 2 ? 2 : on);
+  return FR_OK;
+}
+int frt_set_fuse_shortcut(fr_handle* h, int on) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  DeviceGuard dg(h->device);
+  h->fuse_shortcut = on != 0;
+  clear_graphs(h);
   return FR_OK;
 }
 int frt_set_wino4_split(int on) {

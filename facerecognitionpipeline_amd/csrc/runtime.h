@@ -29,12 +29,16 @@ struct ConvW {
   float* wino4 = nullptr; // F(4x4,3x3) transformed filters G (g * pre_scale) G^T (built on demand), or null
   float* wino4_t = nullptr;  // F(4x4) folded pre-BN: pre_shift / pre_scale per input channel
   int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
+  int cin2 = 0;  // fused 1x1 shortcut input channels (w rows KH*KW*cin + cin2 long), else 0
 };
 
 struct BlockW {
   BlockSpec spec;
   ConvW conv1, conv2, sc;
   bool has_sc_conv = false;
+  // conv2 and the conv shortcut as one GEMM (stride-2 blocks with a conv shortcut): both BN
+  // scales folded into the weights [Cout][3][3][Cout | Cin], the two BN shifts summed
+  ConvW conv2_sc;
 };
 
 // kind: 0 other launch, 1 direct implicit-GEMM conv, 2 Winograd conv (frhip.h FR_PROF_*)
@@ -136,6 +140,7 @@ struct fr_handle {
   int* sk_cnt = nullptr;
   int sk_cnt_cap = 0;
   bool stream_k = true;
+  bool fuse_shortcut = true;  // conv2 + conv shortcut as one launch (frt_set_fuse_shortcut: A/B)
   frhip::Precision prec = frhip::PREC_F32;
   bool winograd = true;          // FR_CONV_WINOGRAD / _WINOGRAD4 for stride-1 3x3 convs
   int wino_m = 4;                // output tile of the Winograd algorithm: 4 = F(4x4,3x3) (default), 2 = F(2x2,3x3)
@@ -263,9 +268,10 @@ std::vector<float> repack_oihw(const std::vector<float>& w, int O, int I, int kh
 int ensure_buf(fr_handle* h, void** p, size_t* cap, size_t bytes);
 int ensure_stream_k(int device, int* cus, float** ws, long long* ws_floats, int** cnt, int* cnt_cap);
 // L: the lane whose stream-K / split-K workspace the launch uses (nullptr: the handle's own)
+// x2: the fused shortcut's input (cw.cin2 > 0)
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, frhip::Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
-             const LaneWs* L = nullptr);
+             const LaneWs* L = nullptr, const float* x2 = nullptr);
 const std::vector<float>* getp(fr_handle* h, const std::string& k);
 
 // detector.cpp

@@ -43,6 +43,10 @@ int frt_set_wino4_split(int on);
  * (last round >= 10% empty, U fits an XCD's L2, >= 8 K-steps per item), 2 = whenever the grid
  * has more items than CUs, 0 = whole items round-robin over the persistent grid. */
 int frt_set_wino4_streamk(int on);
+/* Handle h runs the stride-2 conv2 of a block with a conv shortcut and that shortcut as one
+ * GEMM (on = 1, default: BN scales folded into the weights, extra K-steps over the block input)
+ * or as two launches (0).  Drops captured graphs. */
+int frt_set_fuse_shortcut(fr_handle* h, int on);
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                          const float* pre_scale, const float* pre_shift, const float* post_scale,
                          const float* post_shift, const float* prelu, const float* res, int epi, void* stream);

@@ -300,3 +300,22 @@ def test_resize_branch_embeddings_vs_reference(golden_dir):
     # 224x224 float crops with integer values give the same result (face_embedder.py:100 computes on them)
     # (batch of 1 vs batch of 8: equal to the forward's batch invariance, 1e-6)
     assert np.abs(emb.extract_embeddings_batch([crops[0].astype(np.float64)]) - got[:1]).max() <= 1e-6
+
+
+def test_fused_shortcut_matches_two_launches(arch_embedder):
+    """The stride-2 conv2 of a block with a conv shortcut runs with that shortcut as one GEMM
+    (BN scales folded into the weights, extra K-steps over the block input).  It must agree with
+    the two-launch form (conv2 + BN + residual of the separately computed BN(conv1x1)) within the
+    embedding bar; the default path's parity vs the reference is pinned by the tests above."""
+    from tests import _frt
+    arch, emb = arch_embedder
+    crops = torch.from_numpy(W.synthetic_crops(24, seed=W.CROP_SEED_GALLERY)).cuda()
+    L = _frt.lib()
+    fused = emb.embed_tensor(crops).clone()
+    assert L.frt_set_fuse_shortcut(emb.model.h, 0) == 0
+    try:
+        two = emb.embed_tensor(crops).clone()
+    finally:
+        assert L.frt_set_fuse_shortcut(emb.model.h, 1) == 0
+    assert (fused - two).abs().max().item() <= EMB_TOL
+    assert torch.equal(emb.embed_tensor(crops), fused)

@@ -21,8 +21,10 @@ from facerecognitionpipeline_amd.arch import block_specs  # noqa: E402
 PEAK = 157.3
 
 
-def layers(arch, B):
-    """(name, algorithmic FLOP, algorithmic HBM bytes) per launch of one B-image forward."""
+def layers(arch, B, fused=True):
+    """(name, algorithmic FLOP, algorithmic HBM bytes) per launch of one B-image forward.
+    fused: the stride-2 conv2 of a block with a conv shortcut runs that shortcut as extra K-steps
+    (one launch, frt_set_fuse_shortcut default)."""
     f4 = 4.0
     out = [("stem", 2.0 * B * 112 * 112 * 64 * 27, B * 112 * 112 * 3 + f4 * B * 112 * 112 * 64)]
     hw = 112
@@ -33,12 +35,15 @@ def layers(arch, B):
                     x_b + f4 * d * 9 * cin + f4 * B * hw * hw * d))
         ho = hw // s
         y_b = f4 * B * ho * ho * d
-        if cin != d:
-            out.append((f"s{st}.shortcut1x1.{cin}->{d}@{ho}", 2.0 * B * ho * ho * d * cin,
-                        x_b / (s * s) + f4 * d * cin + y_b))
-        # conv2 reads r (B*hw*hw*d), weights, the residual (y-sized) and writes y
-        out.append((f"s{st}.conv2.{d}->{d}@{ho}{'/s2' if s == 2 else ''}", 2.0 * B * ho * ho * d * 9 * d,
-                    f4 * B * hw * hw * d + f4 * d * 9 * d + 2 * y_b))
+        sc = (2.0 * B * ho * ho * d * cin, x_b / (s * s) + f4 * d * cin) if cin != d else None
+        if sc and not fused:
+            out.append((f"s{st}.shortcut1x1.{cin}->{d}@{ho}", sc[0], sc[1] + y_b))
+        if sc and fused:  # conv2 + shortcut: reads r, x at stride 2, both weights; writes y
+            out.append((f"s{st}.conv2+sc.{d}+{cin}->{d}@{ho}/s2", 2.0 * B * ho * ho * d * 9 * d + sc[0],
+                        f4 * B * hw * hw * d + f4 * d * 9 * d + sc[1] + y_b))
+        else:  # conv2 reads r (B*hw*hw*d), weights, the residual (y-sized) and writes y
+            out.append((f"s{st}.conv2.{d}->{d}@{ho}{'/s2' if s == 2 else ''}", 2.0 * B * ho * ho * d * 9 * d,
+                        f4 * B * hw * hw * d + f4 * d * 9 * d + 2 * y_b))
         hw = ho
     out.append(("head.fc7x7", 2.0 * B * 512 * 25088, f4 * B * 25088 + f4 * 512 * 25088 + f4 * 49 * B * 512))
     out.append(("head_reduce", 0.0, f4 * 49 * B * 512 + f4 * B * 512))
@@ -82,10 +87,11 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--pmc", nargs="*", default=[])
     ap.add_argument("--json", default=None)
+    ap.add_argument("--unfused-shortcut", action="store_true", help="traces taken with frt_set_fuse_shortcut(h, 0)")
     a = ap.parse_args()
     rows = read_csv(glob.glob(os.path.join(a.trace_dir, "*kernel_trace.csv"))[0])
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    L = layers(a.arch, a.batch)
+    L = layers(a.arch, a.batch, fused=not a.unfused_shortcut)
     fwds = align(rows, L, a.batch)
     per = collections.defaultdict(list)
     kname = {}
