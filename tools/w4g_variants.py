@@ -81,7 +81,29 @@ def reswarm(s):
                         "    if (sink == 1234.5f) ring[tid] = sink;\n    return;")
 
 
+ENTER = "      const Item it = item_at(min(j, t_last));\n      ks_real = steps_of(it);\n      step0 = SPLIT ? it.split * KS : 0;\n"
+
+
+def noenter(s):
+    # geometry of the first item only (outputs wrong): what enter_item costs per item
+    assert ENTER in s
+    return s.replace(ENTER, ENTER + "      if (j > (SK ? t_first : 0)) return;\n", 1)
+
+
+GEOW = "        if (g < 8 && j <= t_last) geo[((j & 3) * FT + i) * 8 + g] = g < 4 ? rv : cv;"
+
+
+def samegeo(s):
+    # every item's epilogue writes (and reads its residual at) the first item's pixels: what the
+    # output stores to fresh addresses cost
+    assert GEOW in s
+    s = s.replace(GEOW, "        if (g < 8 && j <= t_last && j == 0) for (int q = 0; q < 4; ++q) geo[(q * FT + i) * 8 + g] = g < 4 ? rv : cv;")
+    return s
+
+
 VARIANTS = {
+    "noenter": noenter,
+    "samegeo": samegeo,
     "st_nt": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 2);")),
     "st_sc1": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 16);")),
     "st_sc01": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 17);")),
