@@ -501,10 +501,11 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
 // One forward of up to max_batch crops: rgb (device) -> out (device) [n][512].  With lanes on
 // (fr_set_lanes), the batch runs as nl = min(lane_max, n / lane_min) near-equal parts: lanes
 // 1 .. nl - 1 fork from s and join back into it, so the call is stream-ordered on s like a single
-// forward.  Profiled forwards stay one lane (their per-launch events would overlap).
+// forward.  Profiled and graph-captured forwards stay one lane (per-launch events would overlap;
+// a captured graph replays on one stream).
 int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int normalize, hipStream_t s) {
   const LaneWs L0 = lane0_ws(h);
-  const int nl = (h->lane_min <= 0 || h->prof) ? 1 : std::max(1, std::min(h->lane_max, n / h->lane_min));
+  const int nl = (h->lane_min <= 0 || h->prof || h->capturing) ? 1 : std::max(1, std::min(h->lane_max, n / h->lane_min));
   if (nl == 1) {
     const int off = 0;
     return forward_lanes(h, rgb, &off, &n, 1, out, normalize, &s, &L0);
@@ -553,7 +554,9 @@ void clear_graphs(fr_handle* h) {
 int capture_graph(fr_handle* h, int n, int normalize) {
   if (!h->cap_stream) FR_HIP(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
   FR_HIP(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+  h->capturing = true;
   const int rc = forward_chunk(h, h->in_stage, n, h->emb_stage, normalize, h->cap_stream);
+  h->capturing = false;
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(h->cap_stream, &g);
   if (rc != FR_OK || e != hipSuccess) {

@@ -169,6 +169,7 @@ struct fr_handle {
     hipGraphExec_t exec;
   };
   int graph_max_n = 0;
+  bool capturing = false;  // forwards captured into a graph run one lane
   hipStream_t cap_stream = nullptr;
   std::vector<GraphEntry> graphs;
 

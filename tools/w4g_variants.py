@@ -101,8 +101,20 @@ def samegeo(s):
     return s
 
 
+KBAR = "      lds_barrier();  // barrier g + 1"
+
+
+def nobar(s):
+    # MFMA waves alone and without the per-K-step barrier (the transform waves, idle, wait at
+    # their first one until the MFMA waves exit): what the barrier costs the MFMA stream
+    s = VARIANTS["mfmaonly"](s)
+    assert KBAR in s
+    return s.replace(KBAR, "      asm volatile(\"s_waitcnt lgkmcnt(0)\" ::: \"memory\");")
+
+
 VARIANTS = {
     "noenter": noenter,
+    "nobar": lambda s: nobar(s),
     "samegeo": samegeo,
     "st_nt": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 2);")),
     "st_sc1": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 16);")),
