@@ -404,6 +404,10 @@ def main():
                        "arch": args.arch, "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "gallery": G, "top_k": k, "parallelism": f"dp{world}",
                        "gallery_exchange": "rccl broadcast" if world > 1 else "none",
+                       # concurrent half-batch forwards per GPU (fr_set_lanes; library default 64 crops
+                       # per lane, at most 2 lanes); the roofline pass always runs one lane
+                       "lanes": (1 if args.lanes_min == 0 else
+                                 max(1, min(2, args.batch // (64 if args.lanes_min is None else args.lanes_min)))),
                        **({"frames_per_step": int(frames.shape[0]),
                            "detector_gflop_per_frame": round(2 * detector_macs() / 1e9, 3),
                            "aligned_from_detections": det_stats["detected"],

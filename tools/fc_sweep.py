@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Head FC (Linear 25088 -> 512 as a 7x7 valid conv over [B][7][7][512], raw split-K slabs)
+under every tile and a few split counts (GPU).  usage: python tools/fc_sweep.py [--batch 256]"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tests import _frt  # noqa: E402
+from tools.conv_sweep import TILES  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    B, dev = a.batch, torch.device("cuda", 0)
+    x = torch.randn(B, 7, 7, 512, device=dev)
+    w = torch.randn(512, 7, 7, 512, device=dev) / 25088 ** 0.5
+    flop = 2.0 * B * 512 * 25088
+    for ns in (49, 98, 196):
+        row = []
+        for t in range(11):
+            try:
+                _frt.conv2d(x, w, B, 7, 7, 512, 512, 7, 7, 1, 0, epi=4, nsplit=ns, tile=t)
+            except Exception:  # noqa: BLE001
+                row.append(f"{TILES[t]}:ERR")
+                continue
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.reps):
+                _frt.conv2d(x, w, B, 7, 7, 512, 512, 7, 7, 1, 0, epi=4, nsplit=ns, tile=t)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.reps
+            row.append(f"{TILES[t]}:{us:.1f}us/{flop / us / 1e6:.0f}TF")
+        print(f"split {ns:3d}: " + " ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
