@@ -112,8 +112,38 @@ def nobar(s):
     return s.replace(KBAR, "      asm volatile(\"s_waitcnt lgkmcnt(0)\" ::: \"memory\");")
 
 
+BT6V = """  const f2 c4 = {4.f, 4.f}, m4 = {-4.f, -4.f}, c2 = {2.f, 2.f}, m2 = {-2.f, -2.f};
+  const f2 r = d[4] - d[2], u = d[3] - d[1];
+  const f2 pp = __builtin_elementwise_fma(m4, d[2], d[4]), q = __builtin_elementwise_fma(m4, d[1], d[3]);
+  t[0] = __builtin_elementwise_fma(c4, d[0] - d[2], r);
+  t[1] = pp + q;
+  t[2] = pp - q;
+  t[3] = __builtin_elementwise_fma(c2, u, r);
+  t[4] = __builtin_elementwise_fma(m2, u, r);
+  t[5] = __builtin_elementwise_fma(m4, u, d[5] - d[3]);"""
+BT6S = """  float a[6], b[6], ta[6], tb[6];
+#pragma unroll
+  for (int e = 0; e < 6; ++e) {
+    a[e] = d[e].x;
+    b[e] = d[e].y;
+  }
+  bt6(a, ta);
+  bt6(b, tb);
+#pragma unroll
+  for (int e = 0; e < 6; ++e) t[e] = f2{ta[e], tb[e]};"""
+PREFMA = "d[a][b] = __builtin_elementwise_fma(P.trow[a], f2{P.colm[b], P.colm[b]}, d[a][b]);"
+PRES = "d[a][b] = f2{__builtin_fmaf(P.trow[a].x, P.colm[b], d[a][b].x), __builtin_fmaf(P.trow[a].y, P.colm[b], d[a][b].y)};"
+
+
+def scalartr(s):
+    # the input transform's math in scalar f32 (same 8-byte loads and lane layout)
+    assert BT6V in s and PREFMA in s
+    return s.replace(BT6V, BT6S).replace(PREFMA, PRES)
+
+
 VARIANTS = {
     "noenter": noenter,
+    "scalartr": scalartr,
     "nobar": lambda s: nobar(s),
     "samegeo": samegeo,
     "st_nt": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 2);")),
