@@ -15,7 +15,8 @@ hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, in
   if (p.Cin % 32 != 0 || p.Cin2 < 0 || p.Cin2 % 32 != 0 || p.steps_total != main_steps + p.Cin2 / 32 || nsplit < 1 ||
       (long long)p.steps_per_split * nsplit < p.steps_total || p.M <= 0 || p.Cout <= 0 ||
       (long long)p.B * p.H * p.W * p.Cin * 4 >= (1ll << 31) ||
-      (long long)p.Cout * (p.KH * p.KW * p.Cin + p.Cin2) * 4 >= (1ll << 31) || (p.sk_cus > 0 && nsplit != 1))
+      (long long)p.Cout * (p.KH * p.KW * p.Cin + p.Cin2) * 4 >= (1ll << 31) || (p.sk_cus > 0 && nsplit != 1) ||
+      (long long)p.M * p.Cout * 4 >= (1ll << 31))  // 32-bit output offsets (the epilogue's buffer stores)
     return hipErrorInvalidValue;
   // fused 1x1 shortcut: its own input, no pre-BN, not on the detector's instances
   if (p.Cin2 > 0 && (!p.x2 || pre || p.steps1 != main_steps || (long long)p.B * p.H * p.W * p.Cin2 * 4 >= (1ll << 31) ||

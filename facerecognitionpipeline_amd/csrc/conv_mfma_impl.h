@@ -389,7 +389,19 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
   };
 
   // ---- epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  // Output (and residual) addresses are 32-bit byte offsets into buffer descriptors sized to the
+  // tensors: rows past M are dropped by the range check (no per-element branch), and a lane's
+  // 16 rows of a 32x32 block sit at compile-time row steps r_e from its first row, so each
+  // element's offset is that row's base plus a wave-uniform r_e * Cout * 4 (an SGPR operand).
+  constexpr bool RESM = EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU;
+  const __amdgpu_buffer_rsrc_t rres = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.res ? p.res : p.y), (short)0,
+      p.res ? (RESM ? p.M * p.Cout * 4 : p.B * p.res_H * p.res_W * p.Cout * 4) : 0, 0x00020000);
   auto epilogue = [&](int m0, int n0, int split) {
+    const int rowb = p.Cout * 4;  // bytes per output row
+    // the output (EPI_RAW: split-K slab `split`), M rows exactly (launch_conv: < 2 GiB)
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.y + (EPI == EPI_RAW ? (long long)split * p.split_stride : 0ll)), (short)0, p.M * rowb, 0x00020000);
 #pragma unroll
     for (int b = 0; b < TN; ++b) {
       const int n = n0 + (wn * TN + b) * 32 + (lane & 31);
@@ -402,30 +414,43 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
       if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) al = p.prelu[n];
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
+        // the lane's first row of this 32x32 block; element e is row m1 + (e & 3) + 8 (e >> 2)
+        const int m1 = m0 + (wm * TM + a) * 32 + 4 * (lane >> 5);
+        const int vb = m1 * rowb + n * 4;
+        // EPI_AFFINE_RES_SUB: (b, oy, ox) of row m1 once; the 16 rows follow by carries
+        int sb = 0, soy = 0, sox = 0;
+        if constexpr (EPI == EPI_AFFINE_RES_SUB) {
+          sb = m1 / HoWo;
+          const int rem = m1 - sb * HoWo;
+          soy = rem / p.Wo;
+          sox = rem - soy * p.Wo;
+        }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int m = m0 + (wm * TM + a) * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-          if (m >= p.M) continue;
+          const int r = (e & 3) + 8 * (e >> 2);  // compile time
+          const int so = r * rowb;               // wave-uniform
           float v = acc[a][b][e];
-          if constexpr (EPI == EPI_RAW) {
-            p.y[(long long)split * p.split_stride + (long long)m * p.Cout + n] = v;
-          } else {
+          if constexpr (EPI != EPI_RAW) {
             v = v * sc + sh;
             if constexpr (EPI == EPI_AFFINE_PRELU) v = v > 0.f ? v : v * al;
-            if constexpr (EPI == EPI_AFFINE_RES) v += p.res[(long long)m * p.Cout + n];
-            if constexpr (EPI == EPI_AFFINE_RES_PRELU) {
-              v += p.res[(long long)m * p.Cout + n];
-              v = v > 0.f ? v : v * al;
+            if constexpr (RESM) {
+              v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rres, vb, so, 0));
+              if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = v > 0.f ? v : v * al;
             }
             if constexpr (EPI == EPI_AFFINE_RES_SUB) {
-              const int bb = m / HoWo;
-              const int rem = m - bb * HoWo;
-              const int oy = rem / p.Wo;
-              const int ox = rem - oy * p.Wo;
-              v += p.res[((long long)(bb * p.res_H + 2 * oy) * p.res_W + 2 * ox) * p.Cout + n];
+              int bb = sb, oy = soy, ox = sox + r;
+              while (ox >= p.Wo) {  // once at most when Wo >= 32 (every stride-2 layer here)
+                ox -= p.Wo;
+                if (++oy == p.Ho) {
+                  oy = 0;
+                  ++bb;
+                }
+              }
+              const int ro = (((bb * p.res_H + 2 * oy) * p.res_W + 2 * ox) * p.Cout + n) * 4;
+              v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rres, bb < p.B ? ro : 0x80000000, 0, 0));
             }
-            p.y[(long long)m * p.Cout + n] = v;
           }
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), yr, vb, so, 0);
         }
       }
     }

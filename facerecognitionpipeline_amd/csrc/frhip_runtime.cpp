@@ -655,8 +655,6 @@ int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float
   if (rc) return rc;
   if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
-  rc = ensure_buf(h, (void**)&h->scores, &h->scores_cap, (size_t)n * h->G * sizeof(float));
-  if (rc) return rc;
   {
     ProfScope ps(h, s, 0.0, 0);
     hipError_t e = launch_l2norm_rows(Q, h->qn, n, 512, s);
@@ -669,11 +667,18 @@ int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float
   g.kh = g.kw = 1;
   g.stride = 1;
   g.pad = 0;
-  rc = run_conv(h, g, h->qn, h->scores, n, 1, 1, EPI_RAW, nullptr, 0, 0, 1, 0, s);
+  // score matrices below 2 GiB (the conv epilogue's 32-bit offsets): queries in chunks
+  const int nc = (int)std::max<long long>(1, std::min<long long>(n, ((1ll << 31) - 1) / ((long long)h->G * 4)));
+  rc = ensure_buf(h, (void**)&h->scores, &h->scores_cap, (size_t)nc * h->G * sizeof(float));
   if (rc) return rc;
-  ProfScope ps(h, s, 0.0, 0);
-  hipError_t e = launch_topk(h->scores, n, h->G, k, idx, score, s);
-  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("topk launch: ") + hipGetErrorString(e));
+  for (int q0 = 0; q0 < n; q0 += nc) {
+    const int qn = std::min(nc, n - q0);
+    rc = run_conv(h, g, h->qn + (size_t)q0 * 512, h->scores, qn, 1, 1, EPI_RAW, nullptr, 0, 0, 1, 0, s);
+    if (rc) return rc;
+    ProfScope ps(h, s, 0.0, 0);
+    hipError_t e = launch_topk(h->scores, qn, h->G, k, idx + (size_t)q0 * k, score + (size_t)q0 * k, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("topk launch: ") + hipGetErrorString(e));
+  }
   return FR_OK;
 }
 
