@@ -224,3 +224,22 @@ def test_batched_delete_compaction(tmp_path):
     dev = gm._get_handle().gallery_read().cpu().numpy()
     assert np.array_equal(dev, np.asarray(gm.get_gallery_embeddings()[0], np.float32))
     assert res[0][0][0] == "S1" and res[2][0][0] == "S2"
+
+
+def test_match_scores_over_2gib_are_chunked(handle):
+    """fr_match_topk keeps each score matrix below 2 GiB (the conv epilogue's 32-bit offsets): a
+    600k-row gallery and 1,000 queries (2.4 GB of scores) run in query chunks.  Queries are
+    gallery rows, so each one's top-1 is its own row at score 1 with a wide margin."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    G, n = 600_000, 1_000
+    E = torch.randn(G, 512, device="cuda", generator=g)
+    E = E / E.norm(dim=1, keepdim=True)
+    handle.gallery_set(E)
+    rows = torch.randint(0, G, (n,), device="cuda", generator=g)
+    idx = torch.empty((n, 2), dtype=torch.int32, device="cuda")
+    score = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+    handle.match(E[rows].contiguous(), 2, idx, score)
+    torch.cuda.synchronize()
+    assert torch.equal(idx[:, 0].long(), rows)
+    assert (score[:, 0] - 1).abs().max().item() < 1e-5 and score[:, 1].max().item() < 0.5
+    handle.gallery_set(torch.empty((0, 512), device="cuda"))
