@@ -71,10 +71,17 @@ constexpr int FN = 64;               // output channels per item: 4 MFMA waves x
 constexpr int KC = 16;               // input channels per K-step
 constexpr int NBUF = 4;              // LDS ring of transformed K-steps
 constexpr int VSTEP = NXI * FT * KC; // floats of one ring slot (9,216)
-constexpr int URING = 9;             // xi-slots of U in flight per MFMA wave (36 % URING == 0)
+// xi-slots of U in flight per MFMA wave (36 % URING == 0): 12 where the registers allow (no
+// residual in the epilogue: stage-3 conv1 244 -> 239 us, stage-1 263 -> 259), 9 for residual
+// epilogues (12 spills ~13 VGPRs there)
+template <int EPI>
+constexpr int uring_depth() {
+  return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 9 : 12;
+}
 constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum with it is past the range
 static_assert((NBUF * VSTEP + 4 * FT * 8) * 4 <= 160 * 1024, "LDS budget");
-static_assert(NXI % URING == 0, "U ring phase must repeat every K-step");
+static_assert(NXI % uring_depth<EPI_AFFINE_RES>() == 0 && NXI % uring_depth<EPI_AFFINE>() == 0,
+              "U ring phase must repeat every K-step");
 
 __device__ __forceinline__ int xcd_remap(int bid, int n) {
   const int xcd = bid & 7, loc = bid >> 3;
@@ -455,6 +462,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   // segments of the stream: MODE 0/1 item j (local) steps [0, KS); SK item j (global) steps
   // [s0, s1) -- only the first and the last segment of a workgroup's range can be partial
   int j = SK ? t_first : 0, s_beg = SK ? u_lo - t_first * KST : 0;
+  constexpr int URING = uring_depth<EPI>();
   f4 uring[URING];
   int ub = ubase(j), ul = ulast(j);
 #pragma unroll

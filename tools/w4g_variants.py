@@ -142,6 +142,7 @@ def scalartr(s):
 
 
 VARIANTS = {
+    "uring12": lambda s: s.replace("constexpr int URING = 9; ", "constexpr int URING = 12;"),
     "noenter": noenter,
     "scalartr": scalartr,
     "nobar": lambda s: nobar(s),
