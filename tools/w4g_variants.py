@@ -141,7 +141,19 @@ def scalartr(s):
     return s.replace(BT6V, BT6S).replace(PREFMA, PRES)
 
 
+def res12(s):
+    # 12-deep U ring for the residual epilogues too, with the residual loaded one output row ahead
+    for a, b in (("  return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 9 : 12;", "  return 12;"),
+                 ("      if (!SK && q == 1) load_res(0);", ""),
+                 ("    if constexpr (!SK) load_res(2);", ""),
+                 ("      if constexpr (SK && RES) {", "      if constexpr (RES) {")):
+        assert a in s, a
+        s = s.replace(a, b)
+    return s
+
+
 VARIANTS = {
+    "res12": res12,
     "uring12": lambda s: s.replace("constexpr int URING = 9; ", "constexpr int URING = 12;"),
     "noenter": noenter,
     "scalartr": scalartr,
