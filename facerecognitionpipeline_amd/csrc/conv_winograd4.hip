@@ -690,12 +690,23 @@ __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
   if (pix >= (long long)p.B * H * W) return;
   const float4* slab = reinterpret_cast<const float4*>(p.part);
   float v[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int sp = 0; sp < S; ++sp) {
-    const float4 a = slab[((((long long)slot0 + sp) * FT + n) * 16 + px) * (FN / 4) + cq];
-    v[0] += a.x;
-    v[1] += a.y;
-    v[2] += a.z;
-    v[3] += a.w;
+  // eight slot loads in flight at a time, summed in part order (deterministic): a loop of one
+  // load and one add per part waited out every load's latency in turn (batch 1: 7.3 us per
+  // fixup launch, 94 launches per forward)
+  for (int s0 = 0; s0 < S; s0 += 8) {
+    float4 a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      a[u] = s0 + u < S ? slab[((((long long)slot0 + s0 + u) * FT + n) * 16 + px) * (FN / 4) + cq]
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (s0 + u < S) {
+        v[0] += a[u].x;
+        v[1] += a[u].y;
+        v[2] += a[u].z;
+        v[3] += a[u].w;
+      }
   }
   const long long yo = pix * p.Cout + cout0;
 #pragma unroll
