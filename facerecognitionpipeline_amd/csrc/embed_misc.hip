@@ -118,9 +118,21 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
   const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
   float v0 = 0.f, v1 = 0.f;
   const float* p = partial + (long long)row * 512;
-  for (int s = 0; s < nsplit; ++s) {
-    v0 += p[(long long)s * split_stride + c0];
-    v1 += p[(long long)s * split_stride + c1];
+  // eight splits' loads in flight at a time, summed in split order (deterministic)
+  for (int s0 = 0; s0 < nsplit; s0 += 8) {
+    float a0[8], a1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = s0 + u < nsplit;
+      a0[u] = ok ? p[(long long)(s0 + u) * split_stride + c0] : 0.f;
+      a1[u] = ok ? p[(long long)(s0 + u) * split_stride + c1] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (s0 + u < nsplit) {
+        v0 += a0[u];
+        v1 += a1[u];
+      }
   }
   v0 += fc_bias[c0];
   v1 += fc_bias[c1];

@@ -393,6 +393,8 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // the 64x128 tile gives stream-K more, smaller tiles (batch 1: 2.28 -> 2.15 ms per forward).
   // The detector's tile set (conv_det.hip) has no 64x128 instance.
   if (!h->detector && p.M <= 4096 && nsplit == 1) tile = TILE_64x128;
+  // the head FC of a serving batch (M = n <= 64 rows, split-K over taps and K quarters)
+  if (!h->detector && p.M <= 64 && nsplit > 1 && cw.kh == 7) tile = TILE_64x128;
   ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
   hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s, h->prec);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
@@ -428,7 +430,9 @@ int ensure_lane(fr_handle* h, int l, int batch) {
     const size_t mb = batch;
     for (auto& a : L.act) FR_HIP(h, hipMalloc((void**)&a, mb * 112 * 112 * 64 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&L.sc_buf, mb * 56 * 56 * 64 * sizeof(float)));
-    FR_HIP(h, hipMalloc((void**)&L.partial, (size_t)h->head_split * mb * 512 * sizeof(float)));
+    // head partials: also a serving batch's 4x split (forward_lanes), whatever the lane's size
+    FR_HIP(h, hipMalloc((void**)&L.partial, (size_t)h->head_split * std::max<size_t>(mb, h->max_batch) * 512 *
+                                                sizeof(float)));
     h->lane_batch[l] = batch;
   }
   if (!L.w4part) FR_HIP(h, hipMalloc((void**)&L.w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
@@ -487,11 +491,16 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
   for (int l = 0; l < nl; ++l) {
     const int n = cnt[l];
     const long long split_stride = (long long)n * 512;
-    int rc = run_conv(h, h->head, L[l].act[cur], L[l].partial, n, 7, 7, EPI_RAW, nullptr, 0, 0, h->head_split,
+    // serving batches (4 n <= max_batch): the FC's 784 K-steps in 196 splits of 4 instead of 49
+    // taps of 16, so its 51 MB of weights stream through 4x the workgroups (batch 1: 78 us).
+    // Decided by n alone (every lane's partials hold head_split x max_batch rows), so a lane's
+    // part computes exactly as a one-lane forward of the same crops.
+    const int hs = 4 * n <= h->max_batch ? 4 * h->head_split : h->head_split;
+    int rc = run_conv(h, h->head, L[l].act[cur], L[l].partial, n, 7, 7, EPI_RAW, nullptr, 0, 0, hs,
                       split_stride, st[l], &L[l]);
     if (rc) return rc;
     ProfScope ps(h, st[l], 0.0, 0);
-    hipError_t e = launch_head_reduce(L[l].partial, h->head_split, split_stride, h->fc_bias, h->bn1d_scale,
+    hipError_t e = launch_head_reduce(L[l].partial, hs, split_stride, h->fc_bias, h->bn1d_scale,
                                       h->bn1d_shift, out + (size_t)off[l] * 512, n, normalize, !h->arcface, st[l]);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("head launch: ") + hipGetErrorString(e));
   }
