@@ -393,8 +393,9 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // the 64x128 tile gives stream-K more, smaller tiles (batch 1: 2.28 -> 2.15 ms per forward).
   // The detector's tile set (conv_det.hip) has no 64x128 instance.
   if (!h->detector && p.M <= 4096 && nsplit == 1) tile = TILE_64x128;
-  // the head FC of a serving batch (M = n <= 64 rows, split-K over taps and K quarters)
-  if (!h->detector && p.M <= 64 && nsplit > 1 && cw.kh == 7) tile = TILE_64x128;
+  // the head FC (split-K) of a serving batch (M = n <= 64 rows) or a lane of <= 128 crops
+  // (tools/fc_sweep.py --batch 128: 76.9 us on 256x128/W8, 48.4 on 128x64/W8)
+  if (!h->detector && nsplit > 1 && cw.kh == 7 && p.M <= 128) tile = p.M <= 64 ? TILE_64x128 : TILE_128x64_W8;
   ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
   hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s, h->prec);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
