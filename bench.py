@@ -352,7 +352,10 @@ def main():
         roofline = {"bound": "mfma", "kernel": kernel_name,
                     "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach * mult / peak, 4),
-                    "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_launch": alg_bytes,
+                    # traffic is NOT observed in this run: PMC counters need their own rocprofv3 passes,
+                    # so it is read from the committed profile of the same workload (traffic_source)
+                    "traffic": traffic, "traffic_from_profile": traffic is not None,
+                    "traffic_source": traffic_src, "alg_bytes_per_launch": alg_bytes,
                     "launches": kp["launches"],
                     "flop_per_launch": (kp["exec_flop"] if dom == "winograd" else kp["flop"]) / kp["launches"],
                     "avg_launch_ms": round(kp["ms"] / kp["launches"], 5),

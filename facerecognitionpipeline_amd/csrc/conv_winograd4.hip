@@ -17,18 +17,22 @@
 // Work item = 16 tiles x 64 couts x all 36 xi; a workgroup (512 threads) is persistent and
 // streams its items' K-steps (16 input channels each) through a 4-deep LDS ring of V:
 //   * 4 MFMA waves, one per SIMD: wave w owns couts 16w .. 16w+15 of the item for ALL 36 xi
-//     (36 16x16 accumulators, 144 registers).  Per K-step and xi: one ds_read_b128 of V (A
-//     operand), one 1-KiB coalesced load of U in fragment order straight from L2 (B operand,
-//     9 xi-slots ahead in a register ring), 4 MFMAs.  Because a lane holds all 36 xi of its
-//     (tile, cout) positions, the output transform A^T M A is lane-local: no LDS exchange and
-//     no barrier in the epilogue.
+//     (36 16x16 accumulators, 144 registers).  Per K-step and xi: one ds_read_b128 of V (the B
+//     operand), one 1-KiB coalesced load of U in fragment order straight from L2 (the A
+//     operand, held in a register ring 12 xi ahead, 9 for the residual epilogues whose
+//     registers it needs), 4 MFMAs; xi go in pairs so two accumulation chains interleave.
+//     Because U is the A operand, a lane's accumulators hold 4 consecutive couts of one tile
+//     for every xi: the output transform A^T M A is lane-local (no LDS exchange, no barrier in
+//     the epilogue) and each output pixel is one 16-byte store.
 //   * 4 transform waves, one per SIMD: every K-step, transform wave t handles tiles 4t..4t+3 of
-//     the item for the step's 16 channels, one 6x6 patch per lane (36 4-byte loads issued a
-//     whole step ahead, addressed from a per-item geometry kept in registers), applies the
-//     pre-activation BN (folded: scale into U, shift/scale added at in-image pixels),
-//     transforms and writes its 36 values into the ring
-//     (ds_write_b32).  Each SIMD thus carries a quarter of the transform every step, beside its
-//     MFMA wave.
+//     the item for the step's 16 channels.  A lane holds HALF a patch of two channels: 3
+//     columns x 6 rows as 18 8-byte buffer loads from per-item precomputed offsets, issued two
+//     K-steps ahead into three rotating register buffers (padding reads 0 through the buffer
+//     range check).  It adds the folded pre-activation BN shift (scale folded into U) at
+//     in-image pixels, applies B^T down its 3 columns, trades 9 values with its partner lane
+//     (v_permlane32_swap: one half keeps patch rows 0-2, the other rows 3-5), applies B^T
+//     along its 3 rows and writes them into the ring (18 ds_write_b64).  Each SIMD thus
+//     carries a quarter of the transform every step, beside its MFMA wave.
 //   * One workgroup barrier per K-step (s_barrier with an LDS-only wait: prefetched global
 //     loads stay in flight across it).  Step g + 2 is written between barriers g and g + 1
 //     (its slot last held step g - 2, read before barrier g - 1) and read between barriers
@@ -650,7 +654,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 }
 
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
-// B-fragment order wino4_kernel reads: [xi][Cout/16][Cin/16][lane = 16 k + cout%16][m] with
+// A-fragment (U) order wino4_kernel reads: [xi][Cout/16][Cin/16][lane = 16 k + cout%16][m] with
 // cin % 16 = 4k + m.
 // Split-K / stream-K finish: y = epilogue(sum of an item's raw partial outputs, in part order:
 // deterministic) at the item's in-image pixels.  Thread = (tile n, pixel, cout quad); grid

@@ -416,6 +416,20 @@ LaneWs lane0_ws(fr_handle* h) {
   return L;
 }
 
+// Frees lane l's (>= 1) activation workspace (after a failed ensure_lane)
+void release_lane(fr_handle* h, int l) {
+  LaneWs& L = h->lane_ws[l];
+  (void)hipDeviceSynchronize();
+  for (auto& a : L.act) {
+    if (a) (void)hipFree(a);
+    a = nullptr;
+  }
+  if (L.sc_buf) (void)hipFree(L.sc_buf);
+  if (L.partial) (void)hipFree(L.partial);
+  L.sc_buf = L.partial = nullptr;
+  h->lane_batch[l] = 0;
+}
+
 // Lane l's (>= 1) workspace for up to `batch` crops, its stream and its join event.
 int ensure_lane(fr_handle* h, int l, int batch) {
   LaneWs& L = h->lane_ws[l];
@@ -529,9 +543,14 @@ int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int norma
     cnt[l] = n / nl + (l < n % nl ? 1 : 0);
     off[l] = o;
     o += cnt[l];
-    if (l > 0) {
-      const int rc = ensure_lane(h, l, std::max(cnt[l], cap));
-      if (rc) return rc;
+    if (l > 0 && ensure_lane(h, l, std::max(cnt[l], cap)) != FR_OK) {
+      // no memory for the second lane's workspace: run this and later forwards as one lane
+      // (what worked before lanes existed) instead of failing the call; fr_set_lanes re-enables
+      (void)hipGetLastError();  // clear the failed allocation's sticky error
+      release_lane(h, l);
+      h->lane_min = 0;
+      const int off0 = 0;
+      return forward_lanes(h, rgb, &off0, &n, 1, out, normalize, &s, &L0);
     }
     st[l] = l ? h->lane_stream[l] : s;
     L[l] = l ? h->lane_ws[l] : L0;
@@ -615,21 +634,35 @@ int embed_device(fr_handle* h, const uint8_t* rgb, int n, float* out, int normal
 
 // cv2.resize(crop, (112, 112), INTER_LINEAR) of n H x W crops (face_embedder.py:94-96), device to
 // device, in OpenCV's fixed point (the letterbox kernel of the detector with a 112 x 112 canvas).
-// The coefficient tables are built once per source size and kept on the device.
+// The coefficient tables are built once per source size and kept on the device, at most
+// RS_TABS_MAX of them (least recently used one replaced: a server resizing crops of arbitrary
+// sizes keeps a bounded cache).
 int resize_device(fr_handle* h, const uint8_t* src, int n, int H, int W, uint8_t* dst, hipStream_t s) {
-  const fr_handle::ResizeTab* t = nullptr;
-  for (const auto& r : h->rs_tabs)
+  fr_handle::ResizeTab* t = nullptr;
+  for (auto& r : h->rs_tabs)
     if (r.H == H && r.W == W) t = &r;
   if (!t) {
     std::vector<int> host(4 * (112 + 112));
     resize_axis_table(112, W, host.data());
     resize_axis_table(112, H, host.data() + 4 * 112);
-    int* d = nullptr;
-    FR_HIP(h, hipMalloc((void**)&d, host.size() * sizeof(int)));
-    FR_HIP(h, hipMemcpy(d, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice));
-    h->rs_tabs.push_back({H, W, resize_simd_end(112 * 3), d});
-    t = &h->rs_tabs.back();
+    if (h->rs_tabs.size() >= fr_handle::RS_TABS_MAX) {
+      t = &*std::min_element(h->rs_tabs.begin(), h->rs_tabs.end(),
+                             [](const fr_handle::ResizeTab& a, const fr_handle::ResizeTab& b) { return a.used < b.used; });
+      // the replaced table may still be read by a resize queued on s: copy in stream order
+      FR_HIP(h, hipMemcpyAsync(t->tab, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice, s));
+      FR_HIP(h, hipStreamSynchronize(s));  // the pageable host table must outlive the copy
+      t->H = H;
+      t->W = W;
+      t->simd_end = resize_simd_end(112 * 3);
+    } else {
+      int* d = nullptr;
+      FR_HIP(h, hipMalloc((void**)&d, host.size() * sizeof(int)));
+      FR_HIP(h, hipMemcpy(d, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice));
+      h->rs_tabs.push_back({H, W, resize_simd_end(112 * 3), d, 0});
+      t = &h->rs_tabs.back();
+    }
   }
+  t->used = ++h->rs_clock;
   ProfScope ps(h, s, 0.0, 0);
   hipError_t e = launch_letterbox(src, n, H, W, t->tab, t->tab + 4 * 112, 112, 112, t->simd_end, 112, 112, dst, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("resize launch: ") + hipGetErrorString(e));
@@ -692,87 +725,251 @@ int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float
   return FR_OK;
 }
 
-// ---- FaceAligner (face_recognition.py:50-75) host side: cv2.estimateAffinePartial2D
-// semantics for 5 landmarks, and warpAffine's inverse.  Same IEEE operation order as
-// oracle/align_ref.py so both produce identical doubles.
+// ---- FaceAligner (face_recognition.py:50-75) host side: cv2.estimateAffinePartial2D with its
+// defaults (RANSAC 3 px / 2000 iterations / 0.99, 10 LM refine iterations), restating OpenCV's
+// ptsetreg.cpp + levmarq.cpp, and warpAffine's inverse.  Same IEEE operation order as
+// oracle/align_ref.py (fit_similarity and helpers), so both produce identical doubles.
 #pragma clang fp contract(off)
-void ls_similarity(const double* src, const double* dst, const int* idx, int n, double M[6]) {
-  double sx = 0, sy = 0, dx = 0, dy = 0;
-  for (int k = 0; k < n; ++k) {
-    const int i = idx[k];
-    sx += src[2 * i];
-    sy += src[2 * i + 1];
-    dx += dst[2 * i];
-    dy += dst[2 * i + 1];
+namespace {
+constexpr double kDblMin = 2.2250738585072014e-308, kDblEps = 2.220446049250313e-16;
+constexpr double kFltEps = 1.1920928955078125e-07;
+
+// cv::RNG (core/rand.cpp): 64-bit multiply-with-carry
+struct CvRng {
+  uint64_t state;
+  explicit CvRng(uint64_t s) : state(s ? s : 0xffffffffull) {}
+  unsigned next() {
+    state = (uint64_t)(unsigned)state * 4164903690u + (unsigned)(state >> 32);
+    return (unsigned)state;
   }
-  sx /= n;
-  sy /= n;
-  dx /= n;
-  dy /= n;
-  double num_a = 0, num_b = 0, den = 0;
-  for (int k = 0; k < n; ++k) {
-    const int i = idx[k];
-    const double px = src[2 * i] - sx, py = src[2 * i + 1] - sy;
-    const double qx = dst[2 * i] - dx, qy = dst[2 * i + 1] - dy;
-    num_a += px * qx + py * qy;
-    num_b += px * qy - py * qx;
-    den += px * px + py * py;
-  }
-  const double a = den != 0 ? num_a / den : 0.0, b = den != 0 ? num_b / den : 0.0;
-  M[0] = a;
-  M[1] = -b;
-  M[2] = dx - (a * sx - b * sy);
-  M[3] = b;
-  M[4] = a;
-  M[5] = dy - (b * sx + a * sy);
+  int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + (unsigned)a); }
+};
+
+// AffinePartial2DEstimatorCallback::runKernel: the similarity through 2 point pairs
+void kernel2(const double f[4], const double t[4], double H[6]) {
+  const double x1 = f[0], y1 = f[1], x2 = f[2], y2 = f[3];
+  const double X1 = t[0], Y1 = t[1], X2 = t[2], Y2 = t[3];
+  const double den = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2);
+  const double d = den != 0 ? 1. / den : INFINITY;
+  const double S0 = d * ((X1 - X2) * (x1 - x2) + (Y1 - Y2) * (y1 - y2));
+  const double S1 = d * ((Y1 - Y2) * (x1 - x2) - (X1 - X2) * (y1 - y2));
+  const double S2 = d * ((Y1 - Y2) * (x1 * y2 - x2 * y1) - (X1 * y2 - X2 * y1) * (y1 - y2) - (X1 * x2 - X2 * x1) * (x1 - x2));
+  const double S3 = d * (-(X1 - X2) * (x1 * y2 - x2 * y1) - (Y1 * x2 - Y2 * x1) * (x1 - x2) - (Y1 * y2 - Y2 * y1) * (y1 - y2));
+  H[0] = H[4] = S0;
+  H[1] = -S1;
+  H[2] = S2;
+  H[3] = S1;
+  H[5] = S3;
 }
 
-int count_inliers(const double M[6], const double* src, const double* dst, int n, double thr, bool* in) {
-  int c = 0;
+// computeError (float32 model and arithmetic) + findInliers
+int find_inliers(const double M[6], const float* src, const float* dst, int n, double thr, bool* mask) {
+  const float F0 = (float)M[0], F1 = (float)M[1], F2 = (float)M[2], F3 = (float)M[3], F4 = (float)M[4], F5 = (float)M[5];
+  const float t = (float)(thr * thr);
+  int nz = 0;
   for (int i = 0; i < n; ++i) {
-    const double px = M[0] * src[2 * i] + M[1] * src[2 * i + 1] + M[2];
-    const double py = M[3] * src[2 * i] + M[4] * src[2 * i + 1] + M[5];
-    const double ex = px - dst[2 * i], ey = py - dst[2 * i + 1];
-    in[i] = std::sqrt(ex * ex + ey * ey) < thr;
-    c += in[i];
+    const float a = F0 * src[2 * i] + F1 * src[2 * i + 1] + F2 - dst[2 * i];
+    const float b = F3 * src[2 * i] + F4 * src[2 * i + 1] + F5 - dst[2 * i + 1];
+    mask[i] = a * a + b * b <= t;
+    nz += mask[i];
   }
-  return c;
+  return nz;
 }
 
-void fit_similarity(const float* src_f, const float* dst_f, int n, double M[6]) {
-  double src[16], dst[16];
-  int all[8];
-  bool in[8];
-  for (int i = 0; i < n; ++i) {
-    src[2 * i] = src_f[2 * i];
-    src[2 * i + 1] = src_f[2 * i + 1];
-    dst[2 * i] = dst_f[2 * i];
-    dst[2 * i + 1] = dst_f[2 * i + 1];
-    all[i] = i;
+// RANSACUpdateNumIters, (1 - ep)^2 as one product
+int update_num_iters(double p, double ep, int max_iters) {
+  p = std::min(std::max(p, 0.), 1.);
+  ep = std::min(std::max(ep, 0.), 1.);
+  double num = std::max(1. - p, kDblMin);
+  const double q = 1. - ep;
+  double denom = 1. - q * q;
+  if (denom < kDblMin) return 0;
+  num = std::log(num);
+  denom = std::log(denom);
+  return denom >= 0 || -num >= max_iters * (-denom) ? max_iters : (int)std::nearbyint(num / denom);
+}
+
+// Gaussian elimination with partial pivoting (n = 4); a zero pivot leaves its unknown 0
+void solve4(const double A[4][4], const double b[4], double x[4]) {
+  double M[4][5];
+  for (int i = 0; i < 4; ++i) {
+    for (int j = 0; j < 4; ++j) M[i][j] = A[i][j];
+    M[i][4] = b[i];
   }
-  ls_similarity(src, dst, all, n, M);
-  if (count_inliers(M, src, dst, n, 3.0, in) == n) return;
-  double best[6];
-  int best_n = -1;
-  for (int i = 0; i < n; ++i)
-    for (int j = i + 1; j < n; ++j) {
-      const int pair[2] = {i, j};
-      double Mi[6];
-      ls_similarity(src, dst, pair, 2, Mi);
-      const int c = count_inliers(Mi, src, dst, n, 3.0, in);
-      if (c > best_n) {
-        best_n = c;
-        memcpy(best, Mi, sizeof(best));
-      }
+  for (int c = 0; c < 4; ++c) {
+    int p = c;
+    for (int r = c + 1; r < 4; ++r)
+      if (std::fabs(M[r][c]) > std::fabs(M[p][c])) p = r;
+    if (p != c)
+      for (int k = 0; k < 5; ++k) std::swap(M[c][k], M[p][k]);
+    if (M[c][c] == 0.0) continue;
+    for (int r = c + 1; r < 4; ++r) {
+      const double f = M[r][c] / M[c][c];
+      for (int k = c; k < 5; ++k) M[r][k] = M[r][k] - f * M[c][k];
     }
-  int sel[8], ns = 0;
-  count_inliers(best, src, dst, n, 3.0, in);
+  }
+  for (int c = 3; c >= 0; --c) {
+    x[c] = 0.0;
+    if (M[c][c] == 0.0) continue;
+    double s = M[c][4];
+    for (int k = c + 1; k < 4; ++k) s = s - M[c][k] * x[k];
+    x[c] = s / M[c][c];
+  }
+}
+
+// AffinePartial2DRefineCallback::compute, h = (a, b, tx, ty): residuals r[2n] and, if J, the
+// normal equations A = J^T J, v = J^T r (sums in index order)
+void refine_compute(const double h[4], const double* src, const double* dst, int n, double* r, double A[4][4],
+                    double v[4]) {
+  for (int i = 0; i < n; ++i) {
+    const double Mx = src[2 * i], My = src[2 * i + 1];
+    const double xi = h[0] * Mx - h[1] * My + h[2];
+    const double yi = h[1] * Mx + h[0] * My + h[3];
+    r[2 * i] = xi - dst[2 * i];
+    r[2 * i + 1] = yi - dst[2 * i + 1];
+  }
+  if (!A) return;
+  double J[16][4];
+  for (int i = 0; i < n; ++i) {
+    const double Mx = src[2 * i], My = src[2 * i + 1];
+    const double j0[4] = {Mx, -My, 1., 0.}, j1[4] = {My, Mx, 0., 1.};
+    for (int c = 0; c < 4; ++c) {
+      J[2 * i][c] = j0[c];
+      J[2 * i + 1][c] = j1[c];
+    }
+  }
+  for (int i = 0; i < 4; ++i) {
+    for (int j = 0; j < 4; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < 2 * n; ++k) s += J[k][i] * J[k][j];
+      A[i][j] = s;
+    }
+    double s = 0.0;
+    for (int k = 0; k < 2 * n; ++k) s += J[k][i] * r[k];
+    v[i] = s;
+  }
+}
+
+double sumsq(const double* r, int m) {
+  double s = 0.0;
+  for (int i = 0; i < m; ++i) s += r[i] * r[i];
+  return s;
+}
+
+double dot4(const double* a, const double* b) {
+  double s = 0.0;
+  for (int i = 0; i < 4; ++i) s += a[i] * b[i];
+  return s;
+}
+
+double maxabs(const double* a, int m) {
+  double s = 0.0;
+  for (int i = 0; i < m; ++i) s = std::max(s, std::fabs(a[i]));
+  return s;
+}
+
+// LMSolverImpl::run (levmarq.cpp, OpenCV 3.x-4.5)
+void lm_refine(double x[4], const double* src, const double* dst, int n, int max_iters) {
+  double r[16], rd[16], A[4][4], v[4], D[4];
+  refine_compute(x, src, dst, n, r, A, v);
+  double S = sumsq(r, 2 * n);
+  for (int i = 0; i < 4; ++i) D[i] = A[i][i];
+  const double Rlo = 0.25, Rhi = 0.75;
+  double lambda = 1, lc = 0.75;
+  for (int iter = 0;;) {
+    double Ap[4][4], d[4], xd[4], temp[4];
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) Ap[i][j] = A[i][j] + (i == j ? lambda * D[i] : 0.0);
+    solve4(Ap, v, d);
+    for (int i = 0; i < 4; ++i) xd[i] = x[i] - d[i];
+    refine_compute(xd, src, dst, n, rd, nullptr, nullptr);
+    const double Sd = sumsq(rd, 2 * n);
+    for (int i = 0; i < 4; ++i) temp[i] = -dot4(A[i], d) + 2.0 * v[i];  // gemm(A, d, -1, v, 2)
+    const double dS = dot4(d, temp);
+    const double R = (S - Sd) / (std::fabs(dS) > kDblEps ? dS : 1.0);
+    if (R > Rhi) {
+      lambda *= 0.5;
+      if (lambda < lc) lambda = 0;
+    } else if (R < Rlo) {
+      const double t = dot4(d, v);
+      double nu = (Sd - S) / (std::fabs(t) > kDblEps ? t : 1.0) + 2.0;
+      nu = std::min(std::max(nu, 2.0), 10.0);
+      if (lambda == 0) {
+        double maxval = kDblEps;
+        for (int i = 0; i < 4; ++i) {
+          double e[4] = {0, 0, 0, 0}, col[4];
+          e[i] = 1.0;
+          solve4(A, e, col);
+          maxval = std::max(maxval, std::fabs(col[i]));
+        }
+        lambda = lc = 1.0 / maxval;
+        nu *= 0.5;
+      }
+      lambda *= nu;
+    }
+    if (Sd < S) {
+      S = Sd;
+      memcpy(x, xd, sizeof(xd));
+      refine_compute(x, src, dst, n, r, A, v);
+    }
+    ++iter;
+    if (!(iter < max_iters && maxabs(d, 4) >= kFltEps && maxabs(r, 2 * n) >= kFltEps)) break;
+  }
+}
+}  // namespace
+
+// estimateAffinePartial2D(src, dst)[0]: returns false (M NaN) where cv2 returns None
+bool fit_similarity(const float* src_f, const float* dst_f, int n, double M[6]) {
+  for (int i = 0; i < 6; ++i) M[i] = NAN;
+  if (n < 2 || n > 8) return false;
+  double src[16], dst[16];
+  for (int i = 0; i < 2 * n; ++i) {
+    src[i] = src_f[i];
+    dst[i] = dst_f[i];
+  }
+  if (n == 2) {
+    kernel2(src, dst, M);
+    return true;
+  }
+  CvRng rng(~0ull);
+  bool mask[8], best_mask[8];
+  double best[6];
+  int niters = 2000, good = 0;
+  for (int it = 0; it < niters; ++it) {
+    const int i0 = rng.uniform(0, n);
+    int i1 = rng.uniform(0, n);
+    while (i1 == i0) i1 = rng.uniform(0, n);
+    const double f[4] = {src[2 * i0], src[2 * i0 + 1], src[2 * i1], src[2 * i1 + 1]};
+    const double t[4] = {dst[2 * i0], dst[2 * i0 + 1], dst[2 * i1], dst[2 * i1 + 1]};
+    double Mi[6];
+    kernel2(f, t, Mi);
+    const int g = find_inliers(Mi, src_f, dst_f, n, 3.0, mask);
+    if (g > std::max(good, 1)) {
+      memcpy(best, Mi, sizeof(best));
+      memcpy(best_mask, mask, sizeof(mask));
+      good = g;
+      niters = update_num_iters(0.99, (double)(n - g) / n, niters);
+    }
+  }
+  if (good <= 0) return false;
+  double si[16], di[16];
+  int m = 0;
   for (int i = 0; i < n; ++i)
-    if (in[i]) sel[ns++] = i;
-  if (ns >= 2)
-    ls_similarity(src, dst, sel, ns, M);
-  else
-    memcpy(M, best, sizeof(best));
+    if (best_mask[i]) {
+      si[2 * m] = src[2 * i];
+      si[2 * m + 1] = src[2 * i + 1];
+      di[2 * m] = dst[2 * i];
+      di[2 * m + 1] = dst[2 * i + 1];
+      ++m;
+    }
+  double h[4] = {best[0], best[3], best[2], best[5]};
+  lm_refine(h, si, di, m, 10);
+  M[0] = M[4] = h[0];
+  M[1] = -h[1];
+  M[2] = h[2];
+  M[3] = h[1];
+  M[5] = h[3];
+  return true;
 }
 
 void invert_affine(const double Mf[6], double Mi[6]) {
@@ -1379,7 +1576,9 @@ int fr_align_faces(fr_handle* h, const uint8_t* frame, int height, int width, co
   std::vector<double> minv((size_t)n * 6);
   for (int f = 0; f < n; ++f) {
     double Mf[6];
-    fit_similarity(landmarks + (size_t)f * 10, tmpl, 5, Mf);
+    if (!fit_similarity(landmarks + (size_t)f * 10, tmpl, 5, Mf))
+      // cv2.estimateAffinePartial2D returns None here and the reference's warpAffine raises
+      return fail(h, FR_ERR_INVALID_ARGUMENT, "similarity fit failed for face " + std::to_string(f));
     if (tforms) memcpy(tforms + (size_t)f * 6, Mf, sizeof(Mf));
     invert_affine(Mf, &minv[(size_t)f * 6]);
   }
@@ -1734,8 +1933,7 @@ int frt_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, c
 
 int frt_fit_similarity(const float* src, const float* dst, int n, double* M) {
   if (n < 2 || n > 8) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "n in [2, 8]");
-  fit_similarity(src, dst, n, M);
-  return FR_OK;
+  return fit_similarity(src, dst, n, M) ? FR_OK : fail(nullptr, FR_ERR_INVALID_ARGUMENT, "similarity fit failed");
 }
 
 int frt_detector_forward(fr_handle* h, const uint8_t* frames, int n, int height, int width, float* heads,

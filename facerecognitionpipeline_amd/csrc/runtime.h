@@ -106,8 +106,11 @@ struct fr_handle {
   struct ResizeTab {
     int H, W, simd_end;
     int* tab;
+    unsigned long long used;  // last use (LRU clock)
   };
+  static constexpr size_t RS_TABS_MAX = 16;  // coefficient tables kept per handle (LRU)
   std::vector<ResizeTab> rs_tabs;
+  unsigned long long rs_clock = 0;
   uint8_t* rs_stage = nullptr;
   void* rs_src = nullptr;
   size_t rs_src_cap = 0;

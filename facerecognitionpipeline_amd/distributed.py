@@ -46,7 +46,8 @@ def broadcast_gallery(gallery: Optional[torch.Tensor], rows: int, device: torch.
 
 
 def gather_topk(idx: torch.Tensor, score: torch.Tensor, n_total: int, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """all_gather every rank's [n_r, k] results back into input order [n_total, k]."""
+    """all_gather every rank's [n_r, k] results back into input order [n_total, k], on ``idx``'s device
+    whatever the backend (gloo gathers through the host, RCCL in place)."""
     world = dist.get_world_size(group)
     k = idx.shape[1]
     longest = shard_range(n_total, world, 0)[1]
@@ -66,7 +67,7 @@ def gather_topk(idx: torch.Tensor, score: torch.Tensor, n_total: int, group=None
         a, b = shard_range(n_total, world, r)
         out_i.append(all_i[r][: b - a])
         out_s.append(all_s[r][: b - a])
-    return torch.cat(out_i), torch.cat(out_s)
+    return torch.cat(out_i).to(idx.device), torch.cat(out_s).to(score.device)
 
 
 def embed_match_sharded(probes: torch.Tensor, local_fn: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]],

@@ -199,14 +199,20 @@ class FaceEmbedder:
     _as_u8 = staticmethod(lambda face_image: as_uint8_crop(face_image))
 
 
-def as_uint8_crop(face_image: np.ndarray) -> np.ndarray:
+def as_uint8_crop(face_image: np.ndarray, input_size=INPUT_SIZE) -> np.ndarray:
     """The device path computes on uint8 pixels (a 256-entry LUT of the reference's float64
-    normalisation, face_embedder.py:99-100).  Non-uint8 crops whose values are integers in
-    [0, 255] convert exactly, so the result is the reference's; any other value (fractional,
-    out of range) would be normalised differently, so it is refused."""
+    normalisation, face_embedder.py:99-100).  A non-uint8 crop is accepted only when it is
+    already ``input_size`` (112x112) and its values are integers in [0, 255]: it then converts
+    exactly and the result is the reference's.  Any other size is refused: the reference
+    resizes a float or 16-bit crop in that dtype (cv2.resize on the original array,
+    face_embedder.py:94-96), with no 8-bit fixed-point rounding, which the uint8 device resize
+    does not restate.  Fractional or out-of-range values are refused too (the LUT covers bytes)."""
     a = np.asarray(face_image)
     if a.dtype == np.uint8:
         return a
+    if tuple(a.shape[:2]) != tuple(input_size):
+        raise ValueError(f"non-uint8 crops ({a.dtype}) must already be {input_size[0]}x{input_size[1]}: the reference "
+                         f"resizes them in {a.dtype} (cv2.resize), which the uint8 device resize does not restate")
     if a.dtype.kind in "biuf" and np.all(np.isfinite(a)) and np.all((a >= 0) & (a <= 255) & (a == np.floor(a))):
         return a.astype(np.uint8)
     raise ValueError(f"crops must be uint8 (or integer-valued in [0, 255]); got {a.dtype} with other values")

@@ -22,6 +22,7 @@ reference's ``export_for_backup`` JSON (``:246-270``).
 """
 from __future__ import annotations
 
+import copy
 import json
 import os
 import shutil
@@ -250,10 +251,11 @@ class GalleryManager:
         return self.students
 
     def get_gallery_embeddings(self) -> Tuple[np.ndarray, List[str]]:
-        if not self.students:
-            return np.array([]), []
-        ids = list(self.students.keys())
-        return np.vstack([self.students[s].template_embedding for s in ids]), ids
+        with self._lock:
+            if not self.students:
+                return np.array([]), []
+            ids = list(self.students.keys())
+            return np.vstack([self.students[s].template_embedding for s in ids]), ids
 
     # -- matching (device) ---------------------------------------------------
     def search(self, query_embedding: np.ndarray, top_k: int = 5) -> List[Tuple[str, str, float]]:
@@ -385,16 +387,18 @@ class GalleryManager:
 
     def save(self, path: Optional[str] = None) -> None:
         path = path or self.gallery_path
-        ids = list(self.students.keys())
-        arrays = {}
-        for i, s in enumerate(ids):
-            arrays[f"e{i}"] = np.asarray(self.students[s].embeddings)
-            arrays[f"t{i}"] = np.asarray(self.students[s].template_embedding)
+        # snapshot under the lock (a concurrent add/delete cannot tear the JSON / npz pair), write outside
+        with self._lock:
+            ids = list(self.students.keys())
+            arrays = {}
+            for i, s in enumerate(ids):
+                arrays[f"e{i}"] = np.array(self.students[s].embeddings)
+                arrays[f"t{i}"] = np.array(self.students[s].template_embedding)
+            meta = {"num_students": len(ids), "last_saved": datetime.now().isoformat(), "order": ids,
+                    "students": {s: {"student_id": r.student_id, "name": r.name, "num_samples": r.num_samples,
+                                     "enrollment_date": r.enrollment_date, "last_updated": r.last_updated,
+                                     "metadata": copy.deepcopy(r.metadata)} for s, r in self.students.items()}}
         np.savez(self._arrays_path(path), **arrays)
-        meta = {"num_students": len(ids), "last_saved": datetime.now().isoformat(), "order": ids,
-                "students": {s: {"student_id": r.student_id, "name": r.name, "num_samples": r.num_samples,
-                                 "enrollment_date": r.enrollment_date, "last_updated": r.last_updated,
-                                 "metadata": r.metadata} for s, r in self.students.items()}}
         with open(os.path.splitext(path)[0] + ".json", "w") as f:
             json.dump(meta, f, indent=2)
 
@@ -430,20 +434,24 @@ class GalleryManager:
         if os.path.exists(self._arrays_path(self.gallery_path)):
             shutil.copy2(self._arrays_path(self.gallery_path), os.path.join(backup_dir, stem + ".npz"))
         out = os.path.join(backup_dir, stem + ".json")
+        with self._lock:  # snapshot: to_dict() copies every record into plain lists
+            doc = {"backup_date": datetime.now().isoformat(), "backup_name": backup_name,
+                   "num_students": len(self.students),
+                   "students": {s: r.to_dict() for s, r in self.students.items()}}
         with open(out, "w") as f:
-            json.dump({"backup_date": datetime.now().isoformat(), "backup_name": backup_name,
-                       "num_students": len(self.students),
-                       "students": {s: r.to_dict() for s, r in self.students.items()}}, f, indent=2)
+            json.dump(doc, f, indent=2)
         return out
 
     def get_statistics(self) -> Dict:
-        n = len(self.students)
+        with self._lock:
+            recs = list(self.students.values())
+        n = len(recs)
         if n == 0:
             return {"num_students": 0, "total_embeddings": 0, "avg_embeddings_per_student": 0}
-        total = sum(r.num_samples for r in self.students.values())
+        total = sum(r.num_samples for r in recs)
         return {"num_students": n, "total_embeddings": total, "avg_embeddings_per_student": total / n,
                 "students": [{"id": r.student_id, "name": r.name, "num_samples": r.num_samples,
-                              "enrollment_date": r.enrollment_date} for r in self.students.values()]}
+                              "enrollment_date": r.enrollment_date} for r in recs]}
 
     # -- template construction (host; offline, KAT-pinned) -------------------
     def _filter_quality_embeddings(self, embeddings: np.ndarray, min_similarity: float = 0.70) -> np.ndarray:

@@ -185,7 +185,9 @@ int fr_set_graph_batch(fr_handle* h, int max_n);
  * Embeddings are those of separate forwards of the parts (batch-invariant to ~1e-6).
  * min_n 0 = one lane.  fr_create's default: FR_LANES_MIN_DEFAULT crops per lane, at most
  * FR_LANES_MAX_DEFAULT lanes (measured on MI355X, IR-101 C3: batch 256 as 2 x 128 +6%, as 3 or 4
- * parts -1..-2%; batch 128 as 2 x 64 +8%; batch 64 as 2 x 32 -6%). */
+ * parts -1..-2%; batch 128 as 2 x 64 +8%; batch 64 as 2 x 32 -6%).  Lane 1's workspace (~1.2 GB
+ * at max_batch 256) is allocated by the first forward that uses it; if that allocation fails the
+ * forward runs as one lane and lanes stay off until the next fr_set_lanes. */
 #define FR_LANES_MIN_DEFAULT 64
 #define FR_LANES_MAX_DEFAULT 2
 int fr_set_lanes(fr_handle* h, int min_n, int max_lanes);

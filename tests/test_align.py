@@ -4,7 +4,9 @@ PARITY UNPINNED against OpenCV (absent here; the reference has no aligned-crop
 fixtures).  The HIP kernels are pinned bit for bit to oracle/align_ref.py, the
 restatement of OpenCV's uint8 fixed-point arithmetic; CPU tests check the
 restatement's own invariants (identity / integer shifts copy pixels exactly,
-half-pixel shifts round half up, the fit is the least-squares similarity).
+half-pixel shifts round half up, the fit recovers an exact similarity, the
+RANSAC consensus drops outliers, cv::RNG's sequence and the adaptive iteration
+count follow OpenCV's published formulas).
 """
 import ctypes
 
@@ -65,17 +67,65 @@ def test_fit_outlier_is_excluded():
     assert np.abs(M - np.array([[0.5, 0, -5], [0, 0.5, -5]])).max() < 1e-9
 
 
+def test_cv_rng_sequence():
+    """cv::RNG((uint64)-1) as RANSAC seeds it: state' = lo32(state) * 4164903690 + hi32(state)."""
+    r = A.CvRNG((1 << 64) - 1)
+    s = (1 << 64) - 1
+    for _ in range(5):
+        s = ((s & 0xFFFFFFFF) * 4164903690 + (s >> 32)) & ((1 << 64) - 1)
+        assert r.next() == s & 0xFFFFFFFF
+    assert A.CvRNG(0).state == 0xFFFFFFFF  # RNG(0) is seeded with 0xffffffff
+    assert [A.CvRNG((1 << 64) - 1).uniform(3, 3)] == [3]
+
+
+def test_ransac_iteration_update():
+    """RANSACUpdateNumIters: log(1-p)/log(1-(1-ep)^2), capped; every inlier found -> 0 more iterations."""
+    assert A._update_num_iters(0.99, 0.0, 2, 2000) == 0
+    want = int(round(np.log(1 - 0.99) / np.log(1 - 0.6 ** 2)))
+    assert A._update_num_iters(0.99, 0.4, 2, 2000) == want == 10
+    assert A._update_num_iters(0.99, 0.4, 2, 5) == 5
+
+
+def _hard_landmarks(rng, n, S=112):
+    """Landmark sets whose least-squares similarity leaves a residual > 3 px (outliers / strong noise)."""
+    t = A.reference_template(S).astype(np.float64)
+    out = []
+    while len(out) < n:
+        s = rng.uniform(1.0, 4.0)
+        th = rng.uniform(-0.5, 0.5)
+        R = s * np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+        p = (t - S / 2) @ R.T + rng.uniform(100, 1800, 2) + rng.normal(0, rng.uniform(1, 6), t.shape)
+        k = rng.integers(0, 3)
+        p[rng.choice(5, k, replace=False)] += rng.normal(0, 25, (k, 2))  # 0-2 gross outliers
+        p = p.astype(np.float32)
+        q = p.astype(np.float64)
+        one, zero = np.ones((5, 1)), np.zeros((5, 1))
+        lhs = np.block([[q[:, :1], -q[:, 1:], one, zero], [q[:, 1:], q[:, :1], zero, one]])
+        a, b, tx, ty = np.linalg.lstsq(lhs, np.concatenate([t[:, 0], t[:, 1]]), rcond=None)[0]
+        res = np.hypot(a * p[:, 0] - b * p[:, 1] + tx - t[:, 0], b * p[:, 0] + a * p[:, 1] + ty - t[:, 1])
+        if res.max() > 3.0:
+            out.append(p)
+    return np.array(out, dtype=np.float32)
+
+
 def test_host_fit_matches_restatement_bitwise():
-    """The C++ fit behind fr_align_faces performs the oracle's IEEE operation sequence (no GPU needed)."""
+    """The C++ fit behind fr_align_faces performs the oracle's IEEE operation sequence (no GPU needed):
+    ordinary landmark sets and sets whose least-squares residuals exceed the 3-px RANSAC threshold."""
     from facerecognitionpipeline_amd import _lib
     lib = _lib.load()
     lib.frt_fit_similarity.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int, ctypes.c_void_p]
     rng = np.random.default_rng(1)
     t = A.reference_template(112)
-    for lm in _faces(rng, 50, 1080, 1920, jitter=3.0):
+    sets = list(_faces(rng, 40, 1080, 1920, jitter=3.0)) + list(_hard_landmarks(rng, 60))
+    partial = 0
+    for lm in sets:
         M = np.zeros(6)
         assert lib.frt_fit_similarity(lm.ctypes.data, t.ctypes.data, 5, M.ctypes.data) == 0
-        assert np.array_equal(M.reshape(2, 3), A.fit_similarity(lm, t))
+        want = A.fit_similarity(lm, t)
+        assert np.array_equal(M.reshape(2, 3), want)
+        e = lm.astype(np.float64) @ want[:, :2].T + want[:, 2] - t
+        partial += int((np.hypot(e[:, 0], e[:, 1]) > 3.0).any())
+    assert partial >= 10  # the hard sets really exercise the consensus (some points left out)
 
 
 def test_laplacian_var_matches_direct_definition():

@@ -220,3 +220,21 @@ def test_match_batcher_routes_concurrent_requests():
             mb.match_single_face(crops[0], 3)
     with pytest.raises(RuntimeError, match="closed"):
         mb.submit(crops[0])
+
+
+def test_non_uint8_crops_only_at_input_size():
+    """Float / 16-bit crops convert exactly only at 112x112; at other sizes the reference resizes them
+    in their own dtype (cv2.resize, face_embedder.py:94-96), so the uint8 device path refuses them."""
+    from facerecognitionpipeline_amd.face_embedder import as_uint8_crop
+    rng = np.random.default_rng(0)
+    ok = rng.integers(0, 256, (112, 112, 3)).astype(np.float64)
+    assert np.array_equal(as_uint8_crop(ok), ok.astype(np.uint8))
+    assert as_uint8_crop(ok.astype(np.uint16)).dtype == np.uint8
+    for bad in (rng.integers(0, 256, (224, 200, 3)).astype(np.float64),
+                rng.integers(0, 256, (224, 224, 3)).astype(np.uint16)):
+        with pytest.raises(ValueError, match="must already be 112x112"):
+            as_uint8_crop(bad)
+    with pytest.raises(ValueError):
+        as_uint8_crop(ok + 0.5)
+    u8 = rng.integers(0, 256, (224, 200, 3), dtype=np.uint8)
+    assert as_uint8_crop(u8) is u8  # uint8 of any size goes to the device resize unchanged

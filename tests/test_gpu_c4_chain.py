@@ -1,0 +1,122 @@
+"""C4 as ONE chain: GPU SCRFD detect -> device align -> IR-101 embed + match, vs the oracle chain.
+
+Reference: ``FaceProcessor.process_numpy`` (face_recognition.py:184-216) feeding
+``FaceMatcher.match_single_face`` (face_matcher.py:52-58).  Product side: ``FaceDetector.detect_batch``
+(SCRFD-10G on the GPU), then ``RecognitionPipeline.recognize`` (``fr_align_faces`` -> blur ->
+quality gate -> one ``fr_embed_match``).  Oracle side, the chain bench.py's ``cpu_baseline_c4`` runs:
+``scrfd.detect`` (restated SCRFD on PyTorch CPU) -> ``align_ref.fit_similarity`` /
+``warp_affine_linear`` -> oracle IR-101 embed -> ``reference_path.search``.
+
+Both detectors, the embedding network and the gallery use seeded synthetic weights; detection
+parity against insightface itself stays unpinned (oracle/scrfd.py).  The gallery is the oracle
+embeddings of the oracle chain's faces (enrolment) plus noisy copies of them as distractors.
+
+Bars: same number of confident detections and the same order wherever the
+oracle's scores are separated; crops bit-identical to the restated warp of the GPU's own landmarks,
+and to the oracle chain's crops wherever the two fits land on the same fixed-point source map;
+identical top-1 ids and cosine scores within 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import align_ref as AR
+from oracle import reference_path as rp
+from oracle import scrfd as R
+
+pytestmark = pytest.mark.gpu
+FACES = 8        # top detections per frame fed to recognition
+CONF = 0.5 + 1e-3  # "confident": clear of the 0.5 threshold by more than head rounding can move it
+
+
+def _frame(seed, H=1080, W=1920):
+    return np.random.default_rng(seed).integers(0, 256, (H, W, 3), dtype=np.uint8)
+
+
+def test_c4_chain_gpu_vs_oracle_chain():
+    from facerecognitionpipeline_amd import weights as W
+    from facerecognitionpipeline_amd.detector_arch import synthetic_detector_state_dict
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    from facerecognitionpipeline_amd.face_recognition import FaceDetector
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    from facerecognitionpipeline_amd.pipeline import RecognitionPipeline
+    from oracle.adaface_net import load_oracle
+
+    torch.set_num_threads(16)
+    dev = torch.device("cuda", 0)
+    frames = np.stack([_frame(401), _frame(402)])
+    det_sd = synthetic_detector_state_dict()
+    fd = FaceDetector(state_dict=det_sd, device=dev, max_frames=2)
+    det_o = R.load_oracle(det_sd)
+    sd = W.synthetic_state_dict("ir_101")
+    emb = FaceEmbedder(architecture="ir_101", state_dict=sd, device=dev, max_batch=64)
+    net_o = load_oracle("ir_101", sd)
+    t = AR.reference_template(112)
+
+    gpu_dets = fd.detect_batch(torch.from_numpy(frames).to(dev))
+    o_dets, o_crops, g_sel = [], [], []
+    n_conf = n_ordered = 0
+    for f in range(2):
+        od, gd = R.detect(det_o, frames[f], 0.5), gpu_dets[f]
+        # -- detection parity: the confident detections, count and order
+        oc = [d for d in od if d["det_score"] >= CONF]
+        gc = [d for d in gd if d["det_score"] >= CONF]
+        assert len(oc) == len(gc) and len(oc) > FACES, (f, len(oc), len(gc))
+        osc = np.array([d["det_score"] for d in oc])
+        for i, (o, g) in enumerate(zip(oc, gc)):
+            gap = min(abs(osc[i] - osc[j]) for j in (i - 1, i + 1) if 0 <= j < len(oc))
+            if gap > 1e-5:  # separated scores: the same face at the same rank
+                assert np.abs(o["bbox"].astype(int) - g["bbox"].astype(int)).max() <= 1, (f, i)
+                assert np.abs(o["landmarks"] - g["landmarks"]).max() <= 0.05, (f, i)
+                assert abs(o["det_score"] - g["det_score"]) <= 1e-4
+                n_ordered += 1
+        n_conf += len(oc)
+        # the recognised faces: the top FACES of each side, the same faces (separated scores)
+        assert all(abs(osc[i] - osc[i + 1]) > 1e-5 for i in range(FACES))
+        o_dets += oc[:FACES]
+        g_sel.append(gc[:FACES])
+        o_crops += [AR.warp_affine_linear(frames[f], AR.fit_similarity(d["landmarks"], t), 112) for d in oc[:FACES]]
+    assert n_ordered >= 0.9 * n_conf
+
+    # -- oracle chain: embed + reference search against the enrolled gallery
+    o_emb = rp.extract_embeddings_batch(net_o, o_crops)
+    gal = W.expand_gallery(o_emb, 200)
+    ids = [f"S{i}" for i in range(gal.shape[0])]
+    names = {s: "N" + s for s in ids}
+    o_res = [rp.search(gal, ids, names, q, top_k=3) for q in o_emb]
+
+    # -- product chain: RecognitionPipeline on each frame with the GPU detections
+    gm = GalleryManager(gallery_path="/tmp/frhip_c4chain/students.npz", device=dev, verbose=False)
+    gm.add_students_batch([(s, names[s], gal[i][None]) for i, s in enumerate(ids)])
+    loose = {"min_det_score": 0.0, "min_face_size": 0, "max_yaw": 1e9, "max_pitch": 1e9, "max_roll": 1e9,
+             "check_blur": False}
+    pipe = RecognitionPipeline(emb, gm, quality_filter_config=loose)
+    g_res, g_crops = [], []
+    for f in range(2):
+        out = pipe.recognize(frames[f], g_sel[f], top_k=3)
+        assert all(o["is_valid"] for o in out)
+        g_res += [o["matches"] for o in out]
+        lm = np.stack([d["landmarks"] for d in g_sel[f]])
+        g_crops += list(pipe.aligner.align_batch(torch.from_numpy(frames[f]).to(dev), lm).cpu().numpy())
+
+    # -- crops: bit-exact vs the restated warp of the GPU's own landmarks; vs the oracle chain's
+    # crops wherever both fits give the same fixed-point source map
+    same_map = 0
+    for i in range(2 * FACES):
+        f = i // FACES
+        g_lm = g_sel[f][i % FACES]["landmarks"]
+        Mg, Mo = AR.fit_similarity(g_lm, t), AR.fit_similarity(o_dets[i]["landmarks"], t)
+        assert np.array_equal(g_crops[i], AR.warp_affine_linear(frames[f], Mg, 112)), i
+        (Xg, Yg), (Xo, Yo) = AR.warp_maps(Mg, 112), AR.warp_maps(Mo, 112)
+        agree = (Xg == Xo) & (Yg == Yo)
+        assert np.array_equal(g_crops[i][agree], o_crops[i][agree]), i
+        same_map += int(agree.all())
+    # -- match: identical top-1 ids, scores within 1e-4 (north_star)
+    worst = 0.0
+    for i in range(2 * FACES):
+        assert g_res[i][0][0] == o_res[i][0][0], (i, g_res[i], o_res[i])
+        worst = max(worst, max(abs(a[2] - b[2]) for a, b in zip(g_res[i], o_res[i])
+                               if a[0] == b[0]))
+    assert worst <= 1e-4, worst
+    print(f"c4 chain: {n_conf} confident detections ({n_ordered} rank-checked), {same_map}/{2 * FACES} crops on "
+          f"the oracle's fixed-point map, max |score - oracle| {worst:.2e}")
