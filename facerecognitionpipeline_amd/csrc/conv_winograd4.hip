@@ -83,7 +83,11 @@ constexpr int uring_depth() {
   return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 9 : 12;
 }
 constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum with it is past the range
-static_assert((NBUF * VSTEP + 4 * FT * 8) * 4 <= 160 * 1024, "LDS budget");
+// output-geometry tables of the items in flight: the transform waves' load stream runs at most
+// NBUF + 2 K-steps (so items) ahead of the MFMA waves' consumption
+constexpr int NGEO = 8;
+static_assert(NGEO > NBUF + 2, "geometry table overwritten while an epilogue may still read it");
+static_assert((NBUF * VSTEP + NGEO * FT * 8 + 8) * 4 <= 160 * 1024, "LDS budget");
 static_assert(NXI % uring_depth<EPI_AFFINE_RES>() == 0 && NXI % uring_depth<EPI_AFFINE>() == 0,
               "U ring phase must repeat every K-step");
 
@@ -121,11 +125,38 @@ __device__ __forceinline__ int vslot(int l) {
   return l ^ ((k & 1) * 2 + (k >> 1) * 12);
 }
 
-// Workgroup barrier that waits for this wave's LDS operations only: global loads issued ahead
-// (U fragments, the next turn's patches) stay in flight across it.
-__device__ __forceinline__ void lds_barrier() {
+// Ring hand-off between the two wave roles, one LDS counter per wave instead of a workgroup
+// barrier per K-step: transform wave t publishes rdy[t] = the number of K-steps it has written,
+// MFMA wave w publishes fre[w] = the number of K-steps it has finished reading.  A consumer
+// waits for the minimum of the four counters it depends on.  (With one s_barrier per K-step the
+// slowest of the 8 waves gated every step: measured at stage 3, ~14% of every wave's time went
+// to waiting at that barrier, and an MFMA wave's epilogue held the transform waves too.)
+// Single writer per counter: a plain ds_write after the wave's earlier LDS operations have
+// completed (LDS serves a wave's operations in order); readers poll with volatile reads.
+typedef __attribute__((address_space(3))) int lds_int;  // LDS pointers: ds_* instructions, not flat_*
+__device__ __forceinline__ int lds_min4(const int* c) {
+  const volatile lds_int* v = (const volatile lds_int*)c;
+  const int m = min(min(v[0], v[1]), min(v[2], v[3]));
+  return __builtin_amdgcn_readfirstlane(m);
+}
+
+// Wait until min(c[0..3]) >= need; returns the value seen.  The spin is bounded (2^16 polls,
+// a few ms): a lost hand-off cannot hang the GPU (the results would be wrong, and the tests
+// compare every output against the CPU references).
+__device__ __forceinline__ int lds_wait_min4(const int* c, int need) {
+  int seen = lds_min4(c);
+  for (int it = 0; seen < need && it < (1 << 16); ++it) {
+    __builtin_amdgcn_s_sleep(1);
+    seen = lds_min4(c);
+  }
+  asm volatile("" ::: "memory");
+  return seen;
+}
+
+// Publish `n` in this wave's counter once its earlier LDS operations have completed.
+__device__ __forceinline__ void lds_publish(int* c, int lane, int n) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  if (lane == 0) *(volatile lds_int*)c = n;
   asm volatile("" ::: "memory");
 }
 
@@ -221,7 +252,7 @@ __device__ __forceinline__ Item item_of(const Wino4Params& p, int gi) {
 template <bool PRE, int EPI, int MODE>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   constexpr bool SPLIT = MODE == 1, SK = MODE == 2;
-  __shared__ __attribute__((aligned(16))) float ring[NBUF * VSTEP + 4 * FT * 8];
+  __shared__ __attribute__((aligned(16))) float ring[NBUF * VSTEP + NGEO * FT * 8 + 8];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout;
@@ -252,7 +283,12 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   auto steps_of = [&](const Item& it) { return SPLIT ? min(KS, KST - it.split * KS) : KST; };
   const int G = SK ? u_hi - u_lo : nloc * KS;  // K-steps in this workgroup's stream (one barrier each)
 
-  int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [4 items][16 tiles][8]
+  int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [NGEO items][16 tiles][8]
+  int* const rdy = geo + NGEO * FT * 8;                           // [4] K-steps written, per transform wave
+  int* const fre = rdy + 4;                                       // [4] K-steps read, per MFMA wave
+  if (tid < 8) rdy[tid] = 0;
+  __syncthreads();  // the kernel's only workgroup barrier
+  if (G <= 0) return;
   if (wid >= 4) {
     // ---- transform waves: every K-step, wave t transforms tiles 4t .. 4t+3 of the item for
     // the step's 16 channels in packed f32, two channels per lane and half a patch per lane:
@@ -264,6 +300,11 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     // period between barriers g and g + 1 (its ring slot last held step g - 2, read before
     // barrier g - 1); its patch loads were issued two periods earlier.
     const int t = wid - 4;
+    // conv1's transform (pre-BN folded in: 18 more packed FMAs per K-step) is the slower side of
+    // the hand-off; at issue priority over its SIMD's MFMA wave it keeps the ring ahead
+    // (measured per launch, B = 256: stage-3 conv1 242 -> 232 us, stage-2 229 -> 215; for the
+    // conv2 epilogues, whose transform has no pre-BN, priority was neutral to +3%)
+    if constexpr (PRE) __builtin_amdgcn_s_setprio(1);
     const int half = lane >> 5, ii = (lane >> 3) & 3, pr = lane & 7;
     const int i = 4 * t + ii, ch = 2 * pr;
     const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
@@ -315,9 +356,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         for (int e = 0; e < 3; ++e) colm[e] = cin[e] ? 1.f : 0.f;
       }
       // output geometry of the item's tiles, for the MFMA waves' epilogue (not for the
-      // stream's overrun: item j - 4's table may still be in use)
+      // stream's overrun past the last item)
       if (half == 0 && pr == 0 && j <= t_last) {
-        int* gt = geo + ((j & 3) * FT + i) * 8;
+        int* gt = geo + ((j % NGEO) * FT + i) * 8;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           int rs, cs;
@@ -413,38 +454,34 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(dst + (6 * k + b) * 256) = v[b];
       }
     };
-    // prologue: steps 0 and 1 written before the first barrier, steps 2 and 3 in flight (the
-    // load stream runs ahead, into the next item at item ends: each buffer carries its own t)
-    load(pa);
-    store(pa, 0);
-    load(pa);
-    store(pa, 1);
+    // Step g is stored into ring slot g % NBUF once every MFMA wave has finished reading step
+    // g - NBUF (fre >= g - NBUF + 1), then published (rdy[t] = g + 1).  Its patch loads were
+    // issued two steps earlier (three patch buffers rotate), so a store never waits for its own
+    // loads' issue.  Loads run past the stream's end unconditionally (they fetch whatever the
+    // clamped geometry names and are never stored): a branch around them would make the
+    // compiler's wait-count tracking wait for the freshly issued loads before the store.
+    int fseen = 0;
+    auto put = [&](Patch& P, int g) {
+      if (g - NBUF + 1 > fseen) fseen = lds_wait_min4(fre, g - NBUF + 1);
+      store(P, g);
+      lds_publish(rdy + t, lane, g + 1);
+    };
     load(pa);
     load(pb);
-    // Step g + 2 is stored in period g from loads issued two periods earlier (three patch
-    // buffers rotate).  The loads are unconditional (past the stream's end they fetch whatever
-    // the clamped geometry names, and are never read): a branch around them would make the
-    // compiler's wait-count tracking wait for the freshly issued loads before the store.
-    // Stores past the end are unconditional too: step g >= G's slot held step g - 4, already
-    // read, and nothing reads it again.
     for (int b = 0;; b += 3) {
-      lds_barrier();  // barrier b
       load(pc);
       __builtin_amdgcn_sched_barrier(0);  // the loads go out first
-      store(pa, b + 2);
+      put(pa, b);
       if (b + 1 >= G) break;
-      lds_barrier();  // barrier b + 1
       load(pa);
       __builtin_amdgcn_sched_barrier(0);
-      store(pb, b + 3);
+      put(pb, b + 1);
       if (b + 2 >= G) break;
-      lds_barrier();  // barrier b + 2
       load(pb);
       __builtin_amdgcn_sched_barrier(0);
-      store(pc, b + 4);
+      put(pc, b + 2);
       if (b + 3 >= G) break;
     }
-    lds_barrier();  // barrier G: the MFMA waves close their last K-step with it
     return;
   }
 
@@ -472,9 +509,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
   for (int r = 0; r < URING; ++r) uring[r] = ld4(ur, lo, r * XS + ub + s_beg * 1024);
   const float* vrd = ring + vslot(lane) * 4;
-  // A fragments (V) of the next xi pair, carried across K-steps: step g + 1's slot was written
-  // before barrier g, so its first pair is read during step g's last MFMAs
-  lds_barrier();  // barrier 0: steps 0 and 1 are in the ring
+  // B fragments (V) of the next xi pair, carried across K-steps: step g + 1's first pair is read
+  // during step g's last MFMAs, once the transform waves have published it
+  int rseen = lds_wait_min4(rdy, 1);  // step 0 is in the ring
   f4 a0n = *reinterpret_cast<const f4*>(vrd), a1n = *reinterpret_cast<const f4*>(vrd + 256);
   int g = 0;
   for (; SK ? g < G : j < nloc; ++j) {
@@ -487,8 +524,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
     for (int x = 0; x < NXI; ++x) acc[x] = f4{0.f, 0.f, 0.f, 0.f};
     auto kstep = [&](int s) {
-      // between barriers g and g + 1: ring slot g % 4 holds step g (barrier g closed the
-      // previous K-step, or is the stream's first)
+      // ring slot g % NBUF holds step g (published before this wave read its first pair)
       const float* vb = vrd + (g % NBUF) * VSTEP;
       const float* vn = vrd + ((g + 1) % NBUF) * VSTEP;
       // U refills: xi + URING of this step, or xi + URING - 36 of the next step (or item)
@@ -501,6 +537,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
       for (int x = 0; x < NXI; x += 2) {
         const f4 a0 = a0n, a1 = a1n;
+        // the last pair reads step g + 1's first fragments: wait until it is published (the
+        // counter seen last time usually already covers it: no poll)
+        if (x + 2 == NXI && g + 1 < G && rseen < g + 2) rseen = lds_wait_min4(rdy, g + 2);
         const float* nb = x + 2 < NXI ? vb + (x + 2) * 256 : vn;
         a0n = *reinterpret_cast<const f4*>(nb);
         a1n = *reinterpret_cast<const f4*>(nb + 256);
@@ -526,7 +565,8 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         __builtin_amdgcn_sched_barrier(0);
       }
       ++g;
-      lds_barrier();  // barrier g + 1
+      // every fragment of step g - 1 has been read (they fed this step's MFMAs): free its slot
+      lds_publish(fre + w, lane, g);
     };
     // the item's first K-step is peeled off the loop: it follows the previous item's epilogue
     // in straight-line code, so the wait for its U fragments counts exactly the epilogue's
@@ -550,7 +590,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     constexpr bool PRELU = !SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU);
     const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, RES ? p.B * H * W * Cout * 4 : 0);
     // byte offsets of tile n's 16 outputs (BIGOFF: outside the images, dropped)
-    const int* gt = geo + ((j & 3) * FT + n) * 8;
+    const int* gt = geo + ((j % NGEO) * FT + n) * 8;
     int oo[4][4];
 #pragma unroll
     for (int y = 0; y < 4; ++y)

@@ -18,72 +18,96 @@ namespace frhip {
 constexpr int IMG = 112;
 constexpr int STEM_C = 64;
 
-// One block per (image, STEM_ROWS output rows).  LDS: STEM_ROWS+2 LUT-normalised input rows
-// with a zero halo ([STEM_ROWS+2][IMG+2][3] floats) and the [27][64] weights.  Thread t owns 4
-// output channels (t&15) of pixels (t>>4) + 16j of every row; its 27x4 weights live in
-// registers for the whole block.  A wave writes 4 pixels x 256 B contiguous.  Per output the
-// 27 FMAs run in (ky, kx, c) order, as before the row blocking.
+// One block (4 waves) per (image, STEM_ROWS output rows).  The 3x3x3 -> 64 conv is a GEMM with
+// K = 27 (padded to 28 with a zero tap) on v_mfma_f32_16x16x4_f32: the weights are the A operand
+// (16 output channels x 4 taps per fragment, 28 registers per lane for all 64 channels, loaded
+// once), the im2col of 16 pixels the B operand (one ds_read_b32 per lane and K-step from the
+// LUT-normalised input rows staged in LDS with a zero halo), so a lane's accumulator holds 4
+// consecutive channels of one pixel and every store is 16 bytes.  An f32 MFMA accumulates its 4
+// products as a chain of fmaf (bitwise), so with K in (ky, kx, c) order each output is the same
+// fmaf sequence as the scalar 27-tap loop it replaces; the padded tap adds 0 * x.  Per 16 pixels x
+// 64 channels: 28 MFMAs (the VALU version's 1,728 FMAs), 7 LDS reads, 4 stores; the kernel is
+// bound by its 822 MB (B = 256) output write.
 constexpr int STEM_ROWS = 4;
-static_assert(IMG % STEM_ROWS == 0, "rows per block must divide the image height");
+constexpr int STEM_W = IMG + 2;  // staged row width with the halo
+static_assert(IMG % STEM_ROWS == 0 && IMG % 16 == 0, "row blocks and 16-pixel groups must tile the image");
+typedef float stem_f4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, const float* __restrict__ lut,
                                                    const float* __restrict__ w27x64,
                                                    const float* __restrict__ bn_scale,
                                                    const float* __restrict__ bn_shift,
                                                    const float* __restrict__ prelu, float* __restrict__ y) {
   __shared__ float s_lut[256];
-  __shared__ __attribute__((aligned(16))) float s_w[27 * STEM_C];
-  __shared__ float s_in[STEM_ROWS + 2][IMG + 2][3];
+  __shared__ float s_in[(STEM_ROWS + 2) * STEM_W * 3 + 1];  // + one zero cell for the padded tap
   constexpr int RB = IMG / STEM_ROWS;  // row blocks per image
+  constexpr int NIN = (STEM_ROWS + 2) * STEM_W * 3;
   const int b = blockIdx.x / RB;
   const int oy0 = (blockIdx.x - b * RB) * STEM_ROWS;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   s_lut[tid] = lut[tid];
-  for (int i = tid; i < 27 * STEM_C; i += 256) s_w[i] = w27x64[i];
+  // weights as A fragments: lane (cout m = lane & 15, tap group kk = lane >> 4), K-step s holds
+  // tap 4 s + kk of channel 16 cb + m (tap 27 = 0)
+  const int m = lane & 15, kk = lane >> 4;
+  float wa[4][7];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int st = 0; st < 7; ++st) {
+      const int k = 4 * st + kk;
+      wa[cb][st] = k < 27 ? w27x64[k * STEM_C + 16 * cb + m] : 0.f;
+    }
   __syncthreads();
-  for (int i = tid; i < (STEM_ROWS + 2) * (IMG + 2) * 3; i += 256) {
-    const int r = i / ((IMG + 2) * 3);
-    const int rem = i - r * (IMG + 2) * 3;
+  const uint8_t* src = img + (size_t)b * IMG * IMG * 3;
+  for (int i = tid; i < NIN + 1; i += 256) {
+    const int r = i / (STEM_W * 3);
+    const int rem = i - r * STEM_W * 3;
     const int xx = rem / 3;
-    const int c = rem - xx * 3;
     const int iy = oy0 + r - 1, ix = xx - 1;
     float v = 0.f;
-    if ((unsigned)iy < IMG && (unsigned)ix < IMG) v = s_lut[img[(((long long)b * IMG + iy) * IMG + ix) * 3 + c]];
-    s_in[r][xx][c] = v;
+    if (i < NIN && (unsigned)iy < IMG && (unsigned)ix < IMG) v = s_lut[src[(iy * IMG + ix) * 3 + rem - xx * 3]];
+    s_in[i] = v;
   }
   __syncthreads();
-  const int cg = tid & 15;
-  float4 w[27];
+  // the lane's im2col offsets: tap k = (ky * 3 + kx) * 3 + c at staged (row ky, column kx, c)
+  int koff[7];
 #pragma unroll
-  for (int t = 0; t < 27; ++t) w[t] = *reinterpret_cast<const float4*>(s_w + t * STEM_C + 4 * cg);
-  const float4 sc = *reinterpret_cast<const float4*>(bn_scale + 4 * cg);
-  const float4 sh = *reinterpret_cast<const float4*>(bn_shift + 4 * cg);
-  const float4 al = *reinterpret_cast<const float4*>(prelu + 4 * cg);
-  for (int r = 0; r < STEM_ROWS; ++r) {
-    for (int px = tid >> 4; px < IMG; px += 16) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int st = 0; st < 7; ++st) {
+    const int k = 4 * st + kk;
+    const int ky = k / 9, kx = (k / 3) % 3, c = k % 3;
+    koff[st] = k < 27 ? (ky * STEM_W + kx) * 3 + c : -1;
+  }
+  const int rg = lane >> 4;  // this lane's output channels: 16 cb + 4 rg .. + 3
+  stem_f4 sc[4], sh[4], al[4];
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+  for (int cb = 0; cb < 4; ++cb) {
+    sc[cb] = *reinterpret_cast<const stem_f4*>(bn_scale + 16 * cb + 4 * rg);
+    sh[cb] = *reinterpret_cast<const stem_f4*>(bn_shift + 16 * cb + 4 * rg);
+    al[cb] = *reinterpret_cast<const stem_f4*>(prelu + 16 * cb + 4 * rg);
+  }
+  // 16-pixel groups of the block (STEM_ROWS rows x 7), round-robin over the 4 waves
+  for (int grp = wv; grp < STEM_ROWS * (IMG / 16); grp += 4) {
+    const int r = grp / (IMG / 16), px = (grp - r * (IMG / 16)) * 16 + m;
+    const int base = (r * STEM_W + px) * 3;
+    float bv[7];
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
+    for (int st = 0; st < 7; ++st) bv[st] = s_in[koff[st] < 0 ? NIN : base + koff[st]];
+    stem_f4 acc[4];
 #pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const float v = s_in[r + ky][px + kx][c];
-            const float4 wt = w[(ky * 3 + kx) * 3 + c];
-            acc.x = fmaf(v, wt.x, acc.x);
-            acc.y = fmaf(v, wt.y, acc.y);
-            acc.z = fmaf(v, wt.z, acc.z);
-            acc.w = fmaf(v, wt.w, acc.w);
-          }
-      float4 o;
-      o.x = acc.x * sc.x + sh.x;
-      o.y = acc.y * sc.y + sh.y;
-      o.z = acc.z * sc.z + sh.z;
-      o.w = acc.w * sc.w + sh.w;
-      o.x = o.x > 0.f ? o.x : o.x * al.x;
-      o.y = o.y > 0.f ? o.y : o.y * al.y;
-      o.z = o.z > 0.f ? o.z : o.z * al.z;
-      o.w = o.w > 0.f ? o.w : o.w * al.w;
-      *reinterpret_cast<float4*>(y + (((long long)b * IMG + oy0 + r) * IMG + px) * STEM_C + 4 * cg) = o;
+    for (int cb = 0; cb < 4; ++cb) {
+      acc[cb] = stem_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 7; ++st) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[cb][st], bv[st], acc[cb], 0, 0, 0);
+    }
+    float* out = y + (((size_t)b * IMG + oy0 + r) * IMG + px) * STEM_C + 4 * rg;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      stem_f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = acc[cb][e] * sc[cb][e] + sh[cb][e];
+        o[e] = t > 0.f ? t : t * al[cb][e];
+      }
+      *reinterpret_cast<stem_f4*>(out + 16 * cb) = o;
     }
   }
 }

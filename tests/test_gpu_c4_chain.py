@@ -25,7 +25,8 @@ from oracle import reference_path as rp
 from oracle import scrfd as R
 
 pytestmark = pytest.mark.gpu
-FACES = 8        # top detections per frame fed to recognition
+FACES = 6        # top detections per frame fed to recognition (the synthetic detector's
+                 # scores cluster near 0.606: below rank 6 neighbours sit within ~1e-5)
 CONF = 0.5 + 1e-3  # "confident": clear of the 0.5 threshold by more than head rounding can move it
 
 
@@ -44,9 +45,10 @@ def test_c4_chain_gpu_vs_oracle_chain():
 
     torch.set_num_threads(16)
     dev = torch.device("cuda", 0)
-    frames = np.stack([_frame(401), _frame(402)])
+    NF = 3
+    frames = np.stack([_frame(401 + f) for f in range(NF)])
     det_sd = synthetic_detector_state_dict()
-    fd = FaceDetector(state_dict=det_sd, device=dev, max_frames=2)
+    fd = FaceDetector(state_dict=det_sd, device=dev, max_frames=NF)
     det_o = R.load_oracle(det_sd)
     sd = W.synthetic_state_dict("ir_101")
     emb = FaceEmbedder(architecture="ir_101", state_dict=sd, device=dev, max_batch=64)
@@ -56,7 +58,7 @@ def test_c4_chain_gpu_vs_oracle_chain():
     gpu_dets = fd.detect_batch(torch.from_numpy(frames).to(dev))
     o_dets, o_crops, g_sel = [], [], []
     n_conf = n_ordered = 0
-    for f in range(2):
+    for f in range(NF):
         od, gd = R.detect(det_o, frames[f], 0.5), gpu_dets[f]
         # -- detection parity: the confident detections, count and order
         oc = [d for d in od if d["det_score"] >= CONF]
@@ -92,7 +94,7 @@ def test_c4_chain_gpu_vs_oracle_chain():
              "check_blur": False}
     pipe = RecognitionPipeline(emb, gm, quality_filter_config=loose)
     g_res, g_crops = [], []
-    for f in range(2):
+    for f in range(NF):
         out = pipe.recognize(frames[f], g_sel[f], top_k=3)
         assert all(o["is_valid"] for o in out)
         g_res += [o["matches"] for o in out]
@@ -102,7 +104,7 @@ def test_c4_chain_gpu_vs_oracle_chain():
     # -- crops: bit-exact vs the restated warp of the GPU's own landmarks; vs the oracle chain's
     # crops wherever both fits give the same fixed-point source map
     same_map = 0
-    for i in range(2 * FACES):
+    for i in range(NF * FACES):
         f = i // FACES
         g_lm = g_sel[f][i % FACES]["landmarks"]
         Mg, Mo = AR.fit_similarity(g_lm, t), AR.fit_similarity(o_dets[i]["landmarks"], t)
@@ -113,10 +115,10 @@ def test_c4_chain_gpu_vs_oracle_chain():
         same_map += int(agree.all())
     # -- match: identical top-1 ids, scores within 1e-4 (north_star)
     worst = 0.0
-    for i in range(2 * FACES):
+    for i in range(NF * FACES):
         assert g_res[i][0][0] == o_res[i][0][0], (i, g_res[i], o_res[i])
         worst = max(worst, max(abs(a[2] - b[2]) for a, b in zip(g_res[i], o_res[i])
                                if a[0] == b[0]))
     assert worst <= 1e-4, worst
-    print(f"c4 chain: {n_conf} confident detections ({n_ordered} rank-checked), {same_map}/{2 * FACES} crops on "
+    print(f"c4 chain: {n_conf} confident detections ({n_ordered} rank-checked), {same_map}/{NF * FACES} crops on "
           f"the oracle's fixed-point map, max |score - oracle| {worst:.2e}")

@@ -297,9 +297,10 @@ def test_resize_branch_embeddings_vs_reference(golden_dir):
     out = np.empty((6, 512), np.float32)
     _lib.check(_lib.load().fr_embed_host(emb.model.h, big.ctypes.data, 6, 224, 224, out.ctypes.data, 1), emb.model.h)
     assert np.abs(out - f["emb"][:6]).max() <= EMB_TOL
-    # 224x224 float crops with integer values give the same result (face_embedder.py:100 computes on them)
-    # (batch of 1 vs batch of 8: equal to the forward's batch invariance, 1e-6)
-    assert np.abs(emb.extract_embeddings_batch([crops[0].astype(np.float64)]) - got[:1]).max() <= 1e-6
+    # a 224x224 float crop is refused: the reference resizes it in float64 (cv2.resize on the
+    # original dtype, face_embedder.py:94-96), which the uint8 device resize does not restate
+    with pytest.raises(ValueError, match="must already be 112x112"):
+        emb.extract_embeddings_batch([crops[0].astype(np.float64)])
 
 
 def test_fused_shortcut_matches_two_launches(arch_embedder):

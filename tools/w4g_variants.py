@@ -101,7 +101,7 @@ def samegeo(s):
     return s
 
 
-KBAR = "      lds_barrier();  // barrier g + 1"
+KBAR = "      lds_publish(fre + w, lane, g);"
 
 
 def nobar(s):
@@ -141,6 +141,30 @@ def scalartr(s):
     return s.replace(BT6V, BT6S).replace(PREFMA, PRES)
 
 
+AT6V = """  const f2 c2 = {2.f, 2.f}, c4 = {4.f, 4.f}, c8 = {8.f, 8.f};
+  const f2 p12 = m[1] + m[2], m12 = m[1] - m[2];
+  const f2 p34 = m[3] + m[4], m34 = m[3] - m[4];
+  o[0] = m[0] + p12 + p34;
+  o[1] = __builtin_elementwise_fma(c2, m34, m12);
+  o[2] = __builtin_elementwise_fma(c4, p34, p12);
+  o[3] = __builtin_elementwise_fma(c8, m34, m12 + m[5]);"""
+AT6S = """#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float p12 = m[1][e] + m[2][e], m12 = m[1][e] - m[2][e];
+    const float p34 = m[3][e] + m[4][e], m34 = m[3][e] - m[4][e];
+    o[0][e] = m[0][e] + p12 + p34;
+    o[1][e] = __builtin_fmaf(2.f, m34, m12);
+    o[2][e] = __builtin_fmaf(4.f, p34, p12);
+    o[3][e] = __builtin_fmaf(8.f, m34, m12 + m[5][e]);
+  }"""
+
+
+def scalarepi(s):
+    # the epilogue's output transform in scalar f32 (same arithmetic per element)
+    assert AT6V in s
+    return s.replace(AT6V, AT6S)
+
+
 def res12(s):
     # 12-deep U ring for the residual epilogues too, with the residual loaded one output row ahead
     for a, b in (("  return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 9 : 12;", "  return 12;"),
@@ -152,7 +176,99 @@ def res12(s):
     return s
 
 
+STAMP_HDR = """
+// ---- stamps variant: per-wave cycle accounting (s_memtime), written once per wave by lane 0 ----
+__device__ unsigned long long w4dbg[1024 * 8 * 4];
+#define W4_WAIT(c_, n_)                                             \\
+  ({                                                                \\
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime();    \\
+    const int r_ = lds_wait_min4(c_, n_);                           \\
+    bar_cyc += __builtin_amdgcn_s_memtime() - t0_;                  \\
+    r_;                                                             \\
+  })
+#define W4_PUT()                                                                        \\
+  if (lane == 0) {                                                                      \\
+    unsigned long long* d_ = w4dbg + ((size_t)blockIdx.x * 8 + wid) * 4;                \\
+    d_[0] = __builtin_amdgcn_s_memtime() - t_start;                                     \\
+    d_[1] = bar_cyc;                                                                    \\
+    d_[2] = epi_cyc;                                                                    \\
+    d_[3] = (unsigned long long)G;                                                      \\
+  }
+"""
+STAMP_HOST = """
+#include <cstdio>
+extern "C" void w4g_after_run() {
+  static unsigned long long h[1024 * 8 * 4];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(frhip::w4dbg), sizeof(h)) != hipSuccess) return;
+  double tot[2] = {0, 0}, bar[2] = {0, 0}, epi[2] = {0, 0}, st[2] = {0, 0};
+  unsigned long long tmax[2] = {0, 0};
+  int n[2] = {0, 0};
+  for (int b = 0; b < 1024; ++b)
+    for (int w = 0; w < 8; ++w) {
+      const unsigned long long* d = h + ((size_t)b * 8 + w) * 4;
+      if (!d[0]) continue;
+      const int k = w < 4 ? 0 : 1;
+      tot[k] += d[0]; bar[k] += d[1]; epi[k] += d[2]; st[k] += d[3]; ++n[k];
+      if (d[0] > tmax[k]) tmax[k] = d[0];
+    }
+  for (int k = 0; k < 2; ++k)
+    if (n[k])
+      printf("  %s waves: %d, avg total %.0f cyc (max %llu), hand-off wait %.0f (%.1f%%), epilogue %.0f (%.1f%%), "
+             "K-steps %.1f -> %.0f cyc/K-step, %.0f outside waits+epilogue per K-step\\n",
+             k ? "transform" : "MFMA", n[k], tot[k] / n[k], tmax[k], bar[k] / n[k], 100 * bar[k] / tot[k],
+             epi[k] / n[k], 100 * epi[k] / tot[k], st[k] / n[k], tot[k] / st[k], (tot[k] - bar[k] - epi[k]) / st[k]);
+}
+"""
+
+
+def stamps(s):
+    # s_memtime accounting per wave: total, time waiting on the ring counters (the per-K-step
+    # barrier before the counter hand-off), MFMA-wave epilogue
+    s = s.replace("= lds_wait_min4(", "= W4_WAIT(")
+    a = "__device__ __forceinline__ int canvas_coord("
+    assert a in s
+    s = s.replace(a, STAMP_HDR + a, 1)
+    a = "  const int tid = threadIdx.x, lane = tid & 63;\n"
+    assert a in s
+    s = s.replace(a, a + "  unsigned long long bar_cyc = 0, epi_cyc = 0;\n"
+                         "  const unsigned long long t_start = __builtin_amdgcn_s_memtime();\n", 1)
+    a = "      if (b + 3 >= G) break;\n    }\n    return;"
+    assert a in s
+    s = s.replace(a, "      if (b + 3 >= G) break;\n    }\n    W4_PUT();\n    return;")
+    assert EPI_START in s
+    s = s.replace(EPI_START, "    const unsigned long long t_e0 = __builtin_amdgcn_s_memtime();\n" + EPI_START, 1)
+    assert EPI_END in s
+    s = s.replace(EPI_END, "\n    epi_cyc += __builtin_amdgcn_s_memtime() - t_e0;\n  }\n  W4_PUT();\n}\n\n// G g G^T", 1)
+    return s + STAMP_HOST
+
+
+MFMA_START = "  // ---- MFMA waves: wave w owns couts 16w .. 16w+15 of every item"
+TR_START = "    const int t = wid - 4;\n"
+
+
+def prio_mfma(s):
+    # MFMA waves at s_setprio 1: they win issue arbitration on their SIMD
+    assert MFMA_START in s
+    return s.replace(MFMA_START, "  __builtin_amdgcn_s_setprio(1);\n" + MFMA_START, 1)
+
+
+def prio_tr(s):
+    # transform waves (the younger half, waves 4-7) at s_setprio 1
+    assert TR_START in s
+    return s.replace(TR_START, TR_START + "    __builtin_amdgcn_s_setprio(1);\n", 1)
+
+
 VARIANTS = {
+    "prio_mfma": prio_mfma,
+    "prio_tr": prio_tr,
+    "stamps_prio_mfma": lambda s: stamps(prio_mfma(s)),
+    "stamps_prio_tr": lambda s: stamps(prio_tr(s)),
+    "stamps": stamps,
+    "scalarepi": scalarepi,
+    "scalarall": lambda s: scalarepi(scalartr(s)),
+    "stamps_scalarall": lambda s: stamps(scalarepi(scalartr(s))),
+    "scalartr_prio_tr": lambda s: prio_tr(scalartr(s)),
+    "stamps_scalartr": lambda s: stamps(scalartr(s)),
     "res12": res12,
     "uring12": lambda s: s.replace("constexpr int URING = 9; ", "constexpr int URING = 12;"),
     "noenter": noenter,
