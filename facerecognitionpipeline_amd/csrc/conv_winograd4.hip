@@ -33,11 +33,12 @@
 //     (v_permlane32_swap: one half keeps patch rows 0-2, the other rows 3-5), applies B^T
 //     along its 3 rows and writes them into the ring (18 ds_write_b64).  Each SIMD thus
 //     carries a quarter of the transform every step, beside its MFMA wave.
-//   * One workgroup barrier per K-step (s_barrier with an LDS-only wait: prefetched global
-//     loads stay in flight across it).  Step g + 2 is written between barriers g and g + 1
-//     (its slot last held step g - 2, read before barrier g - 1) and read between barriers
-//     g + 2 and g + 3.  The transform waves also leave each item's output geometry in LDS
-//     for the epilogue.
+//   * No workgroup barrier per K-step: each wave publishes its progress in an LDS counter
+//     (transform wave t: K-steps written; MFMA wave w: K-steps read).  An MFMA wave reads step
+//     g once all four transform waves have written it; a transform wave writes step g into
+//     slot g % NBUF once all four MFMA waves have read step g - NBUF.  The transform waves may
+//     thus run up to NBUF - 1 steps ahead and keep working through an MFMA wave's epilogue.
+//     They also leave each item's output geometry in LDS for the epilogue.
 // Compared with one 32-output-channel block per workgroup and the transform redone for each
 // (round 1), each patch is transformed Cout/64 times instead of Cout/32, and the epilogue
 // needs neither LDS staging nor barriers.
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   // K-steps item `it` really has (split-K: the last split may be short; its stream is padded
   // with steps whose patches load as zeros, so every item is KS stream steps long)
   auto steps_of = [&](const Item& it) { return SPLIT ? min(KS, KST - it.split * KS) : KST; };
-  const int G = SK ? u_hi - u_lo : nloc * KS;  // K-steps in this workgroup's stream (one barrier each)
+  const int G = SK ? u_hi - u_lo : nloc * KS;  // K-steps in this workgroup's stream (one hand-off each)
 
   int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [NGEO items][16 tiles][8]
   int* const rdy = geo + NGEO * FT * 8;                           // [4] K-steps written, per transform wave
@@ -296,9 +297,8 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     // 2pr, 2pr+1 (18 8-byte loads; a wave's load covers 8 runs of 64 contiguous bytes), adds
     // the folded pre-BN shift, applies B^T down its 3 columns, trades 9 values with its partner
     // lane (v_permlane32_swap: half 0 keeps patch rows 0-2, half 1 rows 3-5), applies B^T
-    // along its 3 rows and writes them (18 ds_write_b64).  Step g + 2 is written during the
-    // period between barriers g and g + 1 (its ring slot last held step g - 2, read before
-    // barrier g - 1); its patch loads were issued two periods earlier.
+    // along its 3 rows and writes them (18 ds_write_b64) into ring slot g % NBUF once the MFMA
+    // waves have read that slot's previous step; its patch loads were issued two steps earlier.
     const int t = wid - 4;
     // conv1's transform (pre-BN folded in: 18 more packed FMAs per K-step) is the slower side of
     // the hand-off; at issue priority over its SIMD's MFMA wave it keeps the ring ahead
@@ -734,17 +734,18 @@ __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
   if (pix >= (long long)p.B * H * W) return;
   const float4* slab = reinterpret_cast<const float4*>(p.part);
   float v[4] = {0.f, 0.f, 0.f, 0.f};
-  // eight slot loads in flight at a time, summed in part order (deterministic): a loop of one
-  // load and one add per part waited out every load's latency in turn (batch 1: 7.3 us per
-  // fixup launch, 94 launches per forward)
-  for (int s0 = 0; s0 < S; s0 += 8) {
-    float4 a[8];
+  // sixteen slot loads in flight at a time (every part of a split-K item: S <= 16 K-steps of
+  // 16 channels per part at the serving sizes), summed in part order (deterministic): a loop of
+  // one load and one add per part waited out every load's latency in turn (batch 1: 7.3 us per
+  // fixup launch, 94 launches per forward; eight at a time: ~5 us)
+  for (int s0 = 0; s0 < S; s0 += 16) {
+    float4 a[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < 16; ++u)
       a[u] = s0 + u < S ? slab[((((long long)slot0 + s0 + u) * FT + n) * 16 + px) * (FN / 4) + cq]
                         : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < 16; ++u)
       if (s0 + u < S) {
         v[0] += a[u].x;
         v[1] += a[u].y;
@@ -866,6 +867,7 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   // the K-steps and the slot workspace; ks_per steps each
   auto split_of = [&](int n, int& ks_per) {
     int S = (int)std::min<long long>(std::min(KST, cus / n), p.part_floats / (SLOT * n));
+    if (p.max_split > 0) S = std::min(S, p.max_split);
     ks_per = KST;
     if (S > 1) {
       ks_per = (KST + S - 1) / S;
@@ -906,9 +908,9 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
     const int nit = MODE_ == 2 ? nT : pw.nitem * pw.ksplit;                                                 \
     hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, MODE_>), dim3(MODE_ == 2 ? cus : std::min(nit, cus)),      \
                        dim3(512), 0, s, pw);                                                                \
-    if (MODE_ == 1)                                                                                         \
-      hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_, false>), dim3(FT * 16 * FN / 4 / 256, pw.nitem),    \
-                         dim3(256), 0, s, pw, KST, cus);                                                    \
+    if (MODE_ == 1) /* 64-thread blocks: a serving grid's few items still spread over the CUs */          \
+      hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_, false>), dim3(FT * 16 * FN / 4 / 64, pw.nitem),     \
+                         dim3(64), 0, s, pw, KST, cus);                                                     \
     if (MODE_ == 2)                                                                                         \
       hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_, true>), dim3(FT * 16 * FN / 4 / 256, cus - 1),      \
                          dim3(256), 0, s, pw, KST, cus);                                                    \

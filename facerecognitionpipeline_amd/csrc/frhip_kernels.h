@@ -131,6 +131,7 @@ struct Wino4Params {
   // grid has more items than CUs (experiments); 0: whole items only
   int sk_mode;
   int no_split;  // 1: never split-K (tests compare the two schedules)
+  int max_split;  // > 0: at most this many K parts per item in a split-K launch (serving sweeps)
 };
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16
 size_t wino4_weight_floats(int Cout, int Cin);

@@ -267,6 +267,8 @@ struct ProfScope {
 // default: measured neutral on the IR-101 layers where its policy applies (stage 2, B=256:
 // 241-246 vs 239-243 us whole items), DESIGN.md §4.
 static int g_wino4_streamk = 0;
+// cap on the F(4x4) split-K parts of small grids (frt_set_wino4_max_split: serving sweeps); 0 = none
+static int g_wino4_max_split = 0;
 
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
@@ -344,6 +346,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.part = w4part;
     wp.part_floats = w4part ? fr_handle::W4PART_FLOATS : 0;
     wp.sk_mode = g_wino4_streamk;
+    wp.max_split = g_wino4_max_split;
     Wino4Params cv = wp;
     wino4_canvas(cv);
     // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
@@ -393,9 +396,9 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // the 64x128 tile gives stream-K more, smaller tiles (batch 1: 2.28 -> 2.15 ms per forward).
   // The detector's tile set (conv_det.hip) has no 64x128 instance.
   if (!h->detector && p.M <= 4096 && nsplit == 1) tile = TILE_64x128;
-  // the head FC (split-K) of a serving batch (M = n <= 64 rows) or a lane of <= 128 crops
-  // (tools/fc_sweep.py --batch 128: 76.9 us on 256x128/W8, 48.4 on 128x64/W8)
-  if (!h->detector && nsplit > 1 && cw.kh == 7 && p.M <= 128) tile = p.M <= 64 ? TILE_64x128 : TILE_128x64_W8;
+  // the head FC (split-K) of a serving batch (M = n <= 64 rows) or of <= 256 crops (tools/fc_sweep.py,
+  // 32 splits: --batch 128 43.0 us on 128x64/W8 vs 106 on 256x128/W8; --batch 256 69.3 vs 111.8)
+  if (!h->detector && nsplit > 1 && cw.kh == 7 && p.M <= 256) tile = p.M <= 64 ? TILE_64x128 : TILE_128x64_W8;
   ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
   hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s, h->prec);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
@@ -446,7 +449,7 @@ int ensure_lane(fr_handle* h, int l, int batch) {
     for (auto& a : L.act) FR_HIP(h, hipMalloc((void**)&a, mb * 112 * 112 * 64 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&L.sc_buf, mb * 56 * 56 * 64 * sizeof(float)));
     // head partials: also a serving batch's 4x split (forward_lanes), whatever the lane's size
-    FR_HIP(h, hipMalloc((void**)&L.partial, (size_t)h->head_split * std::max<size_t>(mb, h->max_batch) * 512 *
+    FR_HIP(h, hipMalloc((void**)&L.partial, (size_t)fr_handle::HEAD_PARTS * std::max<size_t>(mb, h->max_batch) * 512 *
                                                 sizeof(float)));
     h->lane_batch[l] = batch;
   }
@@ -506,11 +509,12 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
   for (int l = 0; l < nl; ++l) {
     const int n = cnt[l];
     const long long split_stride = (long long)n * 512;
-    // serving batches (4 n <= max_batch): the FC's 784 K-steps in 196 splits of 4 instead of 49
-    // taps of 16, so its 51 MB of weights stream through 4x the workgroups (batch 1: 78 us).
-    // Decided by n alone (every lane's partials hold head_split x max_batch rows), so a lane's
-    // part computes exactly as a one-lane forward of the same crops.
-    const int hs = 4 * n <= h->max_batch ? 4 * h->head_split : h->head_split;
+    // serving batches (4 n <= max_batch): the FC's 784 K-steps in 196 splits of 4, so its 51 MB
+    // of weights stream through many workgroups (batch 1: 78 us with 49); larger batches in 32
+    // splits of 25 (tools/fc_sweep.py: B = 256 79.2 -> 69.3 us, a 128-crop lane 47.3 -> 43.0,
+    // vs 49 splits).  Decided by n alone (every lane's partials hold HEAD_PARTS x max_batch
+    // rows), so a lane's part computes exactly as a one-lane forward of the same crops.
+    const int hs = 4 * n <= h->max_batch ? fr_handle::HEAD_SPLIT_SMALL : fr_handle::HEAD_SPLIT;
     int rc = run_conv(h, h->head, L[l].act[cur], L[l].partial, n, 7, 7, EPI_RAW, nullptr, 0, 0, hs,
                       split_stride, st[l], &L[l]);
     if (rc) return rc;
@@ -1313,7 +1317,7 @@ int fr_finalize(fr_handle* h) {
     for (auto& a : h->act) FR_HIP(h, hipMalloc((void**)&a, mb * 112 * 112 * 64 * sizeof(float)));
     // shortcut output: 28x28x128 per image (AdaFace; stage 1 has no conv shortcut), 56x56x64 (ArcFace)
     FR_HIP(h, hipMalloc((void**)&h->sc_buf, mb * 56 * 56 * 64 * sizeof(float)));
-    FR_HIP(h, hipMalloc((void**)&h->partial, (size_t)h->head_split * mb * 512 * sizeof(float)));
+    FR_HIP(h, hipMalloc((void**)&h->partial, (size_t)fr_handle::HEAD_PARTS * mb * 512 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->in_stage, mb * 112 * 112 * 3));
     FR_HIP(h, hipMalloc((void**)&h->rs_stage, mb * 112 * 112 * 3));
     FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
@@ -1856,6 +1860,10 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 static int g_frt_wino4_split = 1;
 int frt_set_wino4_streamk(int on) {
   g_wino4_streamk = on < 0 ? 0 : (on > 2 ? 2 : on);
+  return FR_OK;
+}
+int frt_set_wino4_max_split(int s) {
+  g_wino4_max_split = s < 0 ? 0 : s;
   return FR_OK;
 }
 int frt_set_fuse_shortcut(fr_handle* h, int on) {

@@ -96,7 +96,9 @@ struct fr_handle {
   float *act[3] = {nullptr, nullptr, nullptr};
   float* sc_buf = nullptr;
   float* partial = nullptr;
-  int head_split = 49;
+  // head FC split-K parts: serving batches (4 n <= max_batch) / larger; partial buffers hold
+  // HEAD_PARTS x max_batch rows (>= 196 n for the serving split, >= 32 n for the other)
+  static constexpr int HEAD_SPLIT_SMALL = 196, HEAD_SPLIT = 32, HEAD_PARTS = 49;
   uint8_t* in_stage = nullptr;
   float* emb_stage = nullptr;
 

@@ -43,6 +43,9 @@ int frt_set_wino4_split(int on);
  * (last round >= 10% empty, U fits an XCD's L2, >= 8 K-steps per item), 2 = whenever the grid
  * has more items than CUs, 0 = whole items round-robin over the persistent grid. */
 int frt_set_wino4_streamk(int on);
+/* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
+ * before the call keep their schedule). */
+int frt_set_wino4_max_split(int s);
 /* Handle h runs the stride-2 conv2 of a block with a conv shortcut and that shortcut as one
  * GEMM (on = 1, default: BN scales folded into the weights, extra K-steps over the block input)
  * or as two launches (0).  Drops captured graphs. */

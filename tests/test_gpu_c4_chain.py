@@ -72,13 +72,20 @@ def test_c4_chain_gpu_vs_oracle_chain():
                 assert np.abs(o["landmarks"] - g["landmarks"]).max() <= 0.05, (f, i)
                 assert abs(o["det_score"] - g["det_score"]) <= 1e-4
                 n_ordered += 1
+        # every confident detection, tied scores included, has its counterpart (as a set)
+        gb = np.array([g["bbox"] for g in gc], np.int64)
+        gl = np.stack([g["landmarks"] for g in gc])
+        for o in oc:
+            near = (np.abs(gb - o["bbox"].astype(np.int64)).max(1) <= 1) & \
+                   (np.abs(gl - o["landmarks"]).reshape(len(gc), -1).max(1) <= 0.05)
+            assert near.any(), (f, o["bbox"])
         n_conf += len(oc)
         # the recognised faces: the top FACES of each side, the same faces (separated scores)
         assert all(abs(osc[i] - osc[i + 1]) > 1e-5 for i in range(FACES))
         o_dets += oc[:FACES]
         g_sel.append(gc[:FACES])
         o_crops += [AR.warp_affine_linear(frames[f], AR.fit_similarity(d["landmarks"], t), 112) for d in oc[:FACES]]
-    assert n_ordered >= 0.9 * n_conf
+    assert n_ordered >= 0.5 * n_conf  # the synthetic detector's scores cluster within 1e-5 below rank ~6
 
     # -- oracle chain: embed + reference search against the enrolled gallery
     o_emb = rp.extract_embeddings_batch(net_o, o_crops)

@@ -16,14 +16,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--splits", default="49,98,196")
+    ap.add_argument("--tiles", default="")
     a = ap.parse_args()
     B, dev = a.batch, torch.device("cuda", 0)
     x = torch.randn(B, 7, 7, 512, device=dev)
     w = torch.randn(512, 7, 7, 512, device=dev) / 25088 ** 0.5
     flop = 2.0 * B * 512 * 25088
-    for ns in (49, 98, 196):
+    tiles = [int(t) for t in a.tiles.split(",")] if a.tiles else list(range(11))
+    for ns in (int(v) for v in a.splits.split(",")):
         row = []
-        for t in range(11):
+        for t in tiles:
             try:
                 _frt.conv2d(x, w, B, 7, 7, 512, 512, 7, 7, 1, 0, epi=4, nsplit=ns, tile=t)
             except Exception:  # noqa: BLE001

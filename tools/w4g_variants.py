@@ -258,7 +258,41 @@ def prio_tr(s):
     return s.replace(TR_START, TR_START + "    __builtin_amdgcn_s_setprio(1);\n", 1)
 
 
+LD4_DEF = "__device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, int off, int soff = 0) {"
+
+
+def upolicy(aux):
+    # U fragment loads with a cache-policy aux field (sc0 = 1, nt = 2, sc1 = 16): L1 bypass
+    def f(s):
+        assert LD4_DEF in s
+        extra = ("template <int AUX>\n__device__ __forceinline__ f4 ld4p(__amdgpu_buffer_rsrc_t r, int off, int soff = 0) {\n"
+                 "  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, AUX);\n"
+                 "  return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};\n}\n\n")
+        s = s.replace(LD4_DEF, extra + LD4_DEF, 1)
+        n = s.count("ld4(ur, ")
+        assert n >= 3, n
+        return s.replace("ld4(ur, ", f"ld4p<{aux}>(ur, ")
+    return f
+
+
+def early_res(s):
+    # residual rows 0-1 issued before the output transform, rows 2-3 before couts 2-3 (scalar
+    # output transform: fewer live registers)
+    s = scalarepi(s)
+    for a, b in (("      if (!SK && q == 1) load_res(0);", "      if (!SK && q == 0) load_res(0);\n      if (!SK && q == 1) load_res(2);"),
+                 ("    if constexpr (!SK) load_res(2);", "")):
+        assert a in s, a
+        s = s.replace(a, b)
+    return s
+
+
 VARIANTS = {
+    "nbuf3": lambda s: s.replace("constexpr int NBUF = 4; ", "constexpr int NBUF = 3; "),
+    "early_res": early_res,
+    "u_sc1": upolicy(16),
+    "u_nt": upolicy(2),
+    "u_sc01": upolicy(17),
+    "u_sc0": upolicy(1),
     "prio_mfma": prio_mfma,
     "prio_tr": prio_tr,
     "stamps_prio_mfma": lambda s: stamps(prio_mfma(s)),
