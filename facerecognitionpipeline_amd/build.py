@@ -28,7 +28,9 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
 # F(4x4): keep the transform's f32 math scalar -- packed f32 VALU beside MFMAs costs more issue
 # cycles than the two scalar ops it replaces (MI355X_MICROARCH.md, 'price of one filler')
-EXTRA = {"conv_winograd4.hip": ["-fno-slp-vectorize"]}
+EXTRA = {"conv_winograd4.hip": ["-fno-slp-vectorize"],
+         # the stem's MFMA accumulators in VGPRs: no v_accvgpr_read per output before its epilogue
+         "embed_misc.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 LDFLAGS = ["-shared", f"--offload-arch={ARCH}", f"-Wl,-rpath,{ROCM}/lib", "-Wl,--no-undefined"]
 
 

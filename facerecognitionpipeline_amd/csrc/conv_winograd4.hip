@@ -850,7 +850,11 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   }
   p.mblocks = (p.ntiles + FT - 1) / FT;
   p.nblocks = (p.Cout + FN - 1) / FN;
-  p.nbg = std::max(1, std::min(p.mblocks, 32 / p.nblocks));  // tile blocks per XCD group (32 items)
+  // tile blocks per XCD item group: 32 items for up to 4 cout blocks; at Cout = 512 (8 cout
+  // blocks) 8 tile blocks x 8 cout blocks, so an XCD round streams half of the layer's U (37.7 MB)
+  // instead of all of it, for patches read twice (stage 4: 238 -> 232 us, PMC-modelled traffic
+  // 677 -> 453 MB per launch)
+  p.nbg = std::max(1, std::min(p.mblocks, std::max(32 / p.nblocks, 8)));
   const int KST = p.Cin / KC;
   const int nT = p.mblocks * p.nblocks;
   constexpr long long SLOT = (long long)FT * 16 * FN;  // floats of one compact partial slot

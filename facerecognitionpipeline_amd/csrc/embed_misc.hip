@@ -28,7 +28,7 @@ constexpr int STEM_C = 64;
 // fmaf sequence as the scalar 27-tap loop it replaces; the padded tap adds 0 * x.  Per 16 pixels x
 // 64 channels: 28 MFMAs (the VALU version's 1,728 FMAs), 7 LDS reads, 4 stores; the kernel is
 // bound by its 822 MB (B = 256) output write.
-constexpr int STEM_ROWS = 4;
+constexpr int STEM_ROWS = 16;
 constexpr int STEM_W = IMG + 2;  // staged row width with the halo
 static_assert(IMG % STEM_ROWS == 0 && IMG % 16 == 0, "row blocks and 16-pixel groups must tile the image");
 typedef float stem_f4 __attribute__((ext_vector_type(4)));
@@ -39,6 +39,8 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
                                                    const float* __restrict__ prelu, float* __restrict__ y) {
   __shared__ float s_lut[256];
   __shared__ float s_in[(STEM_ROWS + 2) * STEM_W * 3 + 1];  // + one zero cell for the padded tap
+  // per-wave output transpose: [16 pixels][64 channels + 4 pad] (MFMA layout in, row-major out)
+  __shared__ __attribute__((aligned(16))) float s_out[4][16 * 68];
   constexpr int RB = IMG / STEM_ROWS;  // row blocks per image
   constexpr int NIN = (STEM_ROWS + 2) * STEM_W * 3;
   const int b = blockIdx.x / RB;
@@ -56,16 +58,37 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
       const int k = 4 * st + kk;
       wa[cb][st] = k < 27 ? w27x64[k * STEM_C + 16 * cb + m] : 0.f;
     }
-  __syncthreads();
-  const uint8_t* src = img + (size_t)b * IMG * IMG * 3;
-  for (int i = tid; i < NIN + 1; i += 256) {
-    const int r = i / (STEM_W * 3);
-    const int rem = i - r * STEM_W * 3;
-    const int xx = rem / 3;
-    const int iy = oy0 + r - 1, ix = xx - 1;
-    float v = 0.f;
-    if (i < NIN && (unsigned)iy < IMG && (unsigned)ix < IMG) v = s_lut[src[(iy * IMG + ix) * 3 + rem - xx * 3]];
-    s_in[i] = v;
+  // the block's STEM_ROWS + 2 input rows are whole image rows (336 contiguous bytes each): all
+  // their dwords are loaded at once (one memory latency, not one per byte), then unpacked
+  // through the LUT into the zero-haloed LDS rows
+  constexpr int RDW = IMG * 3 / 4;                         // dwords per image row
+  constexpr int NDW = (STEM_ROWS + 2) * RDW;
+  constexpr int PER = (NDW + 255) / 256;
+  const unsigned* src = reinterpret_cast<const unsigned*>(img + (size_t)b * IMG * IMG * 3);
+  unsigned raw[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = tid + 256 * k;
+    const int r = i / RDW, iy = oy0 + r - 1;
+    raw[k] = i < NDW && (unsigned)iy < IMG ? src[iy * RDW + (i - r * RDW)] : 0u;
+  }
+  for (int i = tid; i < (STEM_ROWS + 2) * 2 * 3 + 1; i += 256) {  // halo columns and the zero cell
+    const int r = i / 6, e = i - r * 6;
+    s_in[i < (STEM_ROWS + 2) * 6 ? (r * STEM_W + (e < 3 ? 0 : STEM_W - 1)) * 3 + e % 3 : NIN] = 0.f;
+  }
+  __syncthreads();  // s_lut (the row loads above are already in flight)
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = tid + 256 * k;
+    if (i < NDW) {
+      const int r = i / RDW, q = 4 * (i - r * RDW);  // first byte of the dword within the row
+      const bool in = (unsigned)(oy0 + r - 1) < IMG;   // rows above / below the image: zero padding
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int xb = q + e, ix = xb / 3;
+        s_in[(r * STEM_W + ix + 1) * 3 + (xb - ix * 3)] = in ? s_lut[(raw[k] >> (8 * e)) & 255u] : 0.f;
+      }
+    }
   }
   __syncthreads();
   // the lane's im2col offsets: tap k = (ky * 3 + kx) * 3 + c at staged (row ky, column kx, c)
@@ -77,12 +100,17 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
     koff[st] = k < 27 ? (ky * STEM_W + kx) * 3 + c : -1;
   }
   const int rg = lane >> 4;  // this lane's output channels: 16 cb + 4 rg .. + 3
-  stem_f4 sc[4], sh[4], al[4];
+  // PReLU as med3(t, a t, c) with c = +inf for a slope a <= 1 (= max(t, a t)) and -inf for
+  // a > 1 (= min(t, a t)): t > 0 ? t : a t exactly (med3 returns one of its operands), in two
+  // instructions instead of a multiply, a compare and a select
+  stem_f4 sc[4], sh[4], al[4], cl[4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
     sc[cb] = *reinterpret_cast<const stem_f4*>(bn_scale + 16 * cb + 4 * rg);
     sh[cb] = *reinterpret_cast<const stem_f4*>(bn_shift + 16 * cb + 4 * rg);
     al[cb] = *reinterpret_cast<const stem_f4*>(prelu + 16 * cb + 4 * rg);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cl[cb][e] = al[cb][e] <= 1.f ? INFINITY : -INFINITY;
   }
   // 16-pixel groups of the block (STEM_ROWS rows x 7), round-robin over the 4 waves
   for (int grp = wv; grp < STEM_ROWS * (IMG / 16); grp += 4) {
@@ -98,16 +126,25 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
 #pragma unroll
       for (int st = 0; st < 7; ++st) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[cb][st], bv[st], acc[cb], 0, 0, 0);
     }
-    float* out = y + (((size_t)b * IMG + oy0 + r) * IMG + px) * STEM_C + 4 * rg;
+    // through the wave's LDS tile, so each store writes 4 whole 256-byte pixel rows (1 KiB
+    // contiguous) instead of 16 scattered 64-byte pieces
+    float* so = s_out[wv];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       stem_f4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float t = acc[cb][e] * sc[cb][e] + sh[cb][e];
-        o[e] = t > 0.f ? t : t * al[cb][e];
+        o[e] = __builtin_amdgcn_fmed3f(t, t * al[cb][e], cl[cb][e]);
       }
-      *reinterpret_cast<stem_f4*>(out + 16 * cb) = o;
+      *reinterpret_cast<stem_f4*>(so + m * 68 + 16 * cb + 4 * rg) = o;
+    }
+    float* out = y + (((size_t)b * IMG + oy0 + r) * IMG + px - m) * STEM_C;  // the group's first pixel
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pp = 4 * j + (lane >> 4);  // pixel of the group, 16-byte channel piece lane & 15
+      *reinterpret_cast<stem_f4*>(out + pp * STEM_C + 4 * (lane & 15)) =
+          *reinterpret_cast<const stem_f4*>(so + pp * 68 + 4 * (lane & 15));
     }
   }
 }

@@ -45,8 +45,8 @@ def layers(arch, B, fused=True):
             out.append((f"s{st}.conv2.{d}->{d}@{ho}{'/s2' if s == 2 else ''}", 2.0 * B * ho * ho * d * 9 * d,
                         f4 * B * hw * hw * d + f4 * d * 9 * d + 2 * y_b))
         hw = ho
-    out.append(("head.fc7x7", 2.0 * B * 512 * 25088, f4 * B * 25088 + f4 * 512 * 25088 + f4 * 49 * B * 512))
-    out.append(("head_reduce", 0.0, f4 * 49 * B * 512 + f4 * B * 512))
+    out.append(("head.fc7x7", 2.0 * B * 512 * 25088, f4 * B * 25088 + f4 * 512 * 25088 + f4 * 32 * B * 512))
+    out.append(("head_reduce", 0.0, f4 * 32 * B * 512 + f4 * B * 512))
     return out
 
 

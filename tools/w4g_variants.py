@@ -286,7 +286,21 @@ def early_res(s):
     return s
 
 
+NBG = "  p.nbg = std::max(1, std::min(p.mblocks, std::max(32 / p.nblocks, 8)));"
+
+
+def nbg(minimum):
+    # at least `minimum` tile blocks per XCD item group (Cout = 512: 4 -> 8, U streamed per XCD
+    # round halves, patches read twice)
+    def f(s):
+        assert NBG in s
+        return s.replace(NBG, f"  p.nbg = std::max(1, std::min(p.mblocks, std::max(32 / p.nblocks, {minimum})));")
+    return f
+
+
 VARIANTS = {
+    "nbg8": nbg(8),
+    "nbg16": nbg(16),
     "nbuf3": lambda s: s.replace("constexpr int NBUF = 4; ", "constexpr int NBUF = 3; "),
     "early_res": early_res,
     "u_sc1": upolicy(16),
