@@ -8,13 +8,14 @@ TAG=${TAG:-r1}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 BARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline"}
+PARGS=${PMC_ARGS:-"--steps 1 --warmup 1 --no-cpu-baseline --lanes-min 0"}
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 bench.py $BARGS > $OUT/trace_bench.log 2>&1 || { echo "trace pass failed rc=$?"; tail -20 $OUT/trace_bench.log; exit 3; }
 echo trace ok; tail -1 $OUT/trace_bench.log
 if [ "${PMC:-1}" = "1" ]; then
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$C -o run -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/pmc_$C.log 2>&1 || { echo "pmc $C failed rc=$?"; tail -20 $OUT/pmc_$C.log; exit 3; }
+    python3 bench.py $PARGS > $OUT/pmc_$C.log 2>&1 || { echo "pmc $C failed rc=$?"; tail -20 $OUT/pmc_$C.log; exit 3; }
   echo pmc $C ok
 done
 fi

@@ -60,12 +60,12 @@ def wino4_tiles(h, B):
 
 def align(rows, L, B):
     """[(layer name, row)] for every B-image forward found in a sorted kernel-trace."""
-    stem_grids = (B * 28 * 256, B * 112 * 256)  # 4 rows per workgroup (1 before the row blocking)
+    # the stem's grid is B x (112 / rows per workgroup) x 256 threads (1, 4 or 16 rows by round)
     found = []
     i = 0
     while i < len(rows):
         r = rows[i]
-        if "stem_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) in stem_grids and i + len(L) <= len(rows):
+        if "stem_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) % (B * 256) == 0 and i + len(L) <= len(rows):
             seq = rows[i:i + len(L)]
             if "head_reduce" in seq[-1]["Kernel_Name"]:
                 found.append([(n[0], d) for n, d in zip(L, seq)])

@@ -31,14 +31,13 @@ def nouload(s):
     return s.replace(ULOAD, "")
 
 
-TRANS_TURNS = ["      store(pa, b + 2);", "      store(pb, b + 3);", "      store(pc, b + 4);"]
+TRANS_PUT = "      store(P, g);\n"
 
 
 def notrans(s):
-    for t in TRANS_TURNS:
-        assert t in s
-        s = s.replace(t, "")
-    return s
+    """the transform waves keep loading and publishing, but transform and write nothing"""
+    assert TRANS_PUT in s
+    return s.replace(TRANS_PUT, "")
 
 
 def noepi(s):
@@ -298,6 +297,28 @@ def nbg(minimum):
     return f
 
 
+def halftrans(s):
+    """transform + LDS writes on even K-steps only (wrong results): the gain an item with twice
+    the couts per transformed patch could reach"""
+    assert TRANS_PUT in s
+    return s.replace(TRANS_PUT, "      if ((g & 1) == 0) store(P, g);\n")
+
+
+def halfpatch(s):
+    """halftrans + patch loads of odd K-steps skipped"""
+    a = "          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);"
+    assert a in s
+    s = s.replace(a, "          const u32x2 v = (ls & 1) ? u32x2{0u, 0u} : __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);")
+    return halftrans(s)
+
+
+def halfu(s):
+    """U refills of odd xi skipped (wrong results): the gain of twice the tiles per U fragment"""
+    a = "          uring[y % URING] = y + URING < NXI ?"
+    assert a in s
+    return s.replace(a, "          if (e == 0) uring[y % URING] = y + URING < NXI ?")
+
+
 VARIANTS = {
     "nbg8": nbg(8),
     "nbg16": nbg(16),
@@ -328,6 +349,9 @@ VARIANTS = {
     "st_sc01": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 17);")),
     "reswarm": reswarm,
     "base": lambda s: s,
+    "halftrans": halftrans,
+    "halfpatch": halfpatch,
+    "halfu": halfu,
     "noepi": noepi,
     "notrans": notrans,
     "noload": lambda s: s.replace("""          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);""",
