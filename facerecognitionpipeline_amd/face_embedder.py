@@ -12,9 +12,9 @@ Crops of any other size go through the device restatement of the reference's
 fixed-point bilinear, parity vs cv2 itself unpinned: cv2 is absent here).
 
 Differences (documented in DESIGN.md): ``model_type='arcface'`` runs the same kernels with the insightface
-IResNet weights of an ``arcface_torch`` state dict (the ONNX files the reference
-loads need onnxruntime, which is absent), and ``device`` must be a HIP device —
-there is no CPU fallback.
+IResNet weights, read from the ``.onnx`` file the reference opens with onnxruntime
+(``onnx_import``: the graph's weights, no onnxruntime) or from an ``arcface_torch``
+state dict, and ``device`` must be a HIP device — there is no CPU fallback.
 """
 from __future__ import annotations
 
@@ -75,7 +75,7 @@ class FaceEmbedder:
                     raise FileNotFoundError(f"{'AdaFace checkpoint' if model_type == 'adaface' else 'ONNX model'} "
                                             f"not found at: {model_path}")
                 state_dict = (load_checkpoint_state_dict(model_path) if model_type == "adaface"
-                              else load_arcface_state_dict(model_path))
+                              else load_arcface_state_dict(model_path, architecture))
         block_specs(architecture)
         self.model = _lib.Handle(architecture, model_type, self.device, max_batch)
         self.model.load_state_dict(state_dict)

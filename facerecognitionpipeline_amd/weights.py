@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import zlib
 from collections import OrderedDict
-from typing import Dict
+from typing import Dict, Optional
 
 import numpy as np
 
@@ -72,17 +72,17 @@ def load_checkpoint_state_dict(model_path: str) -> Dict[str, np.ndarray]:
     return {k[6:]: v.detach().cpu().numpy() for k, v in statedict.items() if k.startswith("model.")}
 
 
-def load_arcface_state_dict(model_path: str) -> Dict[str, np.ndarray]:
-    """IResNet weights for the ArcFace branch from an ``arcface_torch`` ``backbone.pth``
-    (plain state dict, optionally under ``'state_dict'`` and/or ``module.``-prefixed).
-
-    The reference loads ONNX exports of the same network (``face_embedder.py:64-81``); an
-    ONNX graph has BN folded into anonymous initialisers, so its weights cannot be mapped
-    back to this schema without onnx tooling that is absent here."""
-    import torch
+def load_arcface_state_dict(model_path: str, architecture: Optional[str] = None) -> Dict[str, np.ndarray]:
+    """IResNet weights for the ArcFace branch: the ``.onnx`` export the reference opens with
+    onnxruntime (``face_embedder.py:64-81``), read by ``onnx_import`` (no onnx packages), or an
+    ``arcface_torch`` ``backbone.pth`` (plain state dict, optionally under ``'state_dict'`` and/or
+    ``module.``-prefixed)."""
     if model_path.endswith(".onnx"):
-        raise NotImplementedError("ArcFace .onnx models need onnxruntime; pass the arcface_torch backbone.pth "
-                                  "state dict of the same network instead")
+        from .onnx_import import arcface_state_dict_from_onnx
+        if architecture is None:
+            raise ValueError("an ArcFace .onnx model needs its architecture ('ir_50' or 'ir_101')")
+        return arcface_state_dict_from_onnx(model_path, architecture)
+    import torch
     ckpt = torch.load(model_path, map_location="cpu", weights_only=True)
     sd = ckpt.get("state_dict", ckpt) if isinstance(ckpt, dict) else ckpt
     out = {}

@@ -70,12 +70,31 @@ def test_arcface_search_parity(arc, tmp_path):
         assert np.abs(np.array([x[2] for x in r]) - np.array([x[2] for x in want])).max() <= 1e-4
 
 
-def test_arcface_onnx_path_is_refused(tmp_path):
+def test_arcface_onnx_model_path(tmp_path):
+    """model_path='*.onnx' (the reference's ArcFace input, face_embedder.py:64-81): the graph's
+    weights through onnx_import.  Unfused export: the same parameters as the state-dict path, so
+    bit-identical embeddings; fused export (BN folded into the convs): the oracle's embeddings
+    within 1e-5.  Graphs written by tests/_onnx_write.py (no real .onnx files offline: unpinned)."""
     from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
-    p = tmp_path / "m.onnx"
-    p.write_bytes(b"\x08\x07")
-    with pytest.raises(NotImplementedError):
-        FaceEmbedder(architecture="ir_50", model_type="arcface", model_path=str(p))
+    from oracle import iresnet
+    from tests._onnx_write import iresnet_onnx
+    sd = W.synthetic_state_dict("ir_50", model_type="arcface")
+    crops = list(W.synthetic_crops(6))
+    ref = FaceEmbedder(architecture="ir_50", model_type="arcface", state_dict=sd, max_batch=8)
+    base = ref.extract_embeddings_batch(crops)
+    for fused in (False, True):
+        p = tmp_path / f"m{int(fused)}.onnx"
+        p.write_bytes(iresnet_onnx(sd, "ir_50", fused=fused))
+        e = FaceEmbedder(architecture="ir_50", model_type="arcface", model_path=str(p), max_batch=8)
+        got = e.extract_embeddings_batch(crops)
+        if not fused:
+            assert np.array_equal(got, base)
+        want = iresnet.extract_embeddings_batch(iresnet.load_oracle("ir_50", sd), crops)
+        assert np.abs(got - want).max() <= EMB_TOL
+    bad = tmp_path / "bad.onnx"
+    bad.write_bytes(b"\x08\x07")
+    with pytest.raises(ValueError):
+        FaceEmbedder(architecture="ir_50", model_type="arcface", model_path=str(bad))
 
 
 def test_arcface_checkpoint_roundtrip(tmp_path):

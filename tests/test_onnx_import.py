@@ -1,0 +1,69 @@
+"""ArcFace ``.onnx`` import (face_embedder.py:64-88: the reference opens the ONNX export of
+insightface IResNet with onnxruntime).  No onnx package or model file exists here, so the
+graphs are written from seeded IResNet weights by tests/_onnx_write.py in both export forms
+(BN nodes kept / BN folded into the convs), and the importer must give back the weights
+(bit for bit, unfused) or the same network (fused: the oracle IResNet's embeddings within
+1e-5).  Parity against insightface's published .onnx files: UNPINNED."""
+import numpy as np
+import pytest
+import torch
+
+from facerecognitionpipeline_amd import weights as W
+from facerecognitionpipeline_amd.onnx_import import arcface_state_dict_from_onnx, read_graph
+from tests._onnx_write import iresnet_onnx
+
+
+@pytest.fixture(scope="module")
+def sd50():
+    return W.synthetic_state_dict("ir_50", model_type="arcface")
+
+
+@pytest.mark.parametrize("raw", [True, False])
+def test_unfused_graph_gives_back_the_weights(sd50, tmp_path, raw):
+    p = tmp_path / "m.onnx"
+    p.write_bytes(iresnet_onnx(sd50, "ir_50", fused=False, raw=raw))
+    got = arcface_state_dict_from_onnx(str(p), "ir_50")
+    want = {k: v for k, v in sd50.items() if not k.endswith("num_batches_tracked")}
+    assert set(got) == set(want)
+    for k, v in want.items():
+        assert got[k].dtype == np.float32 and np.array_equal(got[k].reshape(v.shape), v), k
+
+
+def test_fused_graph_is_the_same_network(sd50, tmp_path):
+    from oracle import iresnet
+    p = tmp_path / "m.onnx"
+    p.write_bytes(iresnet_onnx(sd50, "ir_50", fused=True))
+    got = arcface_state_dict_from_onnx(str(p), "ir_50")
+    # folded convs come back as conv weight + an identity BN carrying the bias (scale exactly 1)
+    assert np.all(np.float32(got["layer1.0.bn2.running_var"]) + np.float32(1e-5) == np.float32(1.0))
+    assert not np.array_equal(got["layer1.0.conv1.weight"], sd50["layer1.0.conv1.weight"])
+    torch.set_num_threads(min(8, torch.get_num_threads()))
+    crops = list(W.synthetic_crops(2))
+    want = iresnet.extract_embeddings_batch(iresnet.load_oracle("ir_50", sd50), crops)
+    have = iresnet.extract_embeddings_batch(iresnet.load_oracle("ir_50", got), crops)
+    assert np.abs(have - want).max() <= 1e-5
+
+
+def test_graph_reader_fields(sd50, tmp_path):
+    p = tmp_path / "m.onnx"
+    p.write_bytes(iresnet_onnx(sd50, "ir_50", fused=True))
+    nodes, inits, g_in, g_out = read_graph(str(p))
+    ops = [n.op for n in nodes]
+    assert g_in == ["data"] and len(g_out) == 1
+    assert ops.count("Add") == 24 and ops.count("PRelu") == 25 and ops.count("Gemm") == 1
+    conv = nodes[0]
+    assert conv.op == "Conv" and conv.attrs["strides"] == [1, 1] and conv.attrs["pads"] == [1, 1, 1, 1]
+    assert inits[conv.inputs[1]].shape == (64, 3, 3, 3)
+
+
+def test_wrong_architecture_or_graph_is_refused(sd50, tmp_path):
+    p = tmp_path / "m.onnx"
+    p.write_bytes(iresnet_onnx(sd50, "ir_50", fused=True))
+    with pytest.raises(NotImplementedError):
+        arcface_state_dict_from_onnx(str(p), "ir_101")  # 13 stage-2 units expected, the graph has 4
+    q = tmp_path / "empty.onnx"
+    q.write_bytes(b"\x08\x07")  # a ModelProto with an ir_version and no graph
+    with pytest.raises(ValueError):
+        arcface_state_dict_from_onnx(str(q), "ir_50")
+    with pytest.raises(ValueError):
+        W.load_arcface_state_dict(str(p))  # an .onnx file needs its architecture

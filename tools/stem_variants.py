@@ -15,6 +15,17 @@ VARIANTS = {
     "rows8": SRC.replace("constexpr int STEM_ROWS = 16;", "constexpr int STEM_ROWS = 8;"),
     "rows28": SRC.replace("constexpr int STEM_ROWS = 16;", "constexpr int STEM_ROWS = 28;"),
 }
+STORE = """      *reinterpret_cast<stem_f4*>(out + pp * STEM_C + 4 * (lane & 15)) =
+          *reinterpret_cast<const stem_f4*>(so + pp * 68 + 4 * (lane & 15));"""
+NT = """      __builtin_nontemporal_store(*reinterpret_cast<const stem_f4*>(so + pp * 68 + 4 * (lane & 15)),
+                                  reinterpret_cast<stem_f4*>(out + pp * STEM_C + 4 * (lane & 15)));"""
+assert STORE in SRC
+VARIANTS["nt"] = SRC.replace(STORE, NT)
+VARIANTS["rows8nt"] = VARIANTS["rows8"].replace(STORE, NT)
+VARIANTS["rows28nt"] = VARIANTS["rows28"].replace(STORE, NT)
+ONLY = os.environ.get("ONLY")
+if ONLY:
+    VARIANTS = {k: v for k, v in VARIANTS.items() if k in ONLY.split(",")}
 objs = [o for o in glob.glob(os.path.join(REPO, "build", "frhip", "*.o")) if "embed_misc" not in os.path.basename(o)]
 # newest object per source
 latest = {}

@@ -319,6 +319,99 @@ def halfu(s):
     return s.replace(a, "          if (e == 0) uring[y % URING] = y + URING < NXI ?")
 
 
+LOOP3 = """    Patch pa, pb, pc;"""
+LOOPBODY3 = """    load(pa);
+    load(pb);
+    for (int b = 0;; b += 3) {
+      load(pc);
+      __builtin_amdgcn_sched_barrier(0);  // the loads go out first
+      put(pa, b);
+      if (b + 1 >= G) break;
+      load(pa);
+      __builtin_amdgcn_sched_barrier(0);
+      put(pb, b + 1);
+      if (b + 2 >= G) break;
+      load(pb);
+      __builtin_amdgcn_sched_barrier(0);
+      put(pc, b + 2);
+      if (b + 3 >= G) break;
+    }"""
+LOOPBODY4 = """    load(pa);
+    load(pb);
+    load(pc);
+    for (int b = 0;; b += 4) {
+      load(pd);
+      __builtin_amdgcn_sched_barrier(0);  // the loads go out first
+      put(pa, b);
+      if (b + 1 >= G) break;
+      load(pa);
+      __builtin_amdgcn_sched_barrier(0);
+      put(pb, b + 1);
+      if (b + 2 >= G) break;
+      load(pb);
+      __builtin_amdgcn_sched_barrier(0);
+      put(pc, b + 2);
+      if (b + 3 >= G) break;
+      load(pc);
+      __builtin_amdgcn_sched_barrier(0);
+      put(pd, b + 3);
+      if (b + 4 >= G) break;
+    }"""
+
+
+def pf3(s):
+    """patch loads three K-steps ahead (four rotating buffers) instead of two"""
+    assert LOOP3 in s and LOOPBODY3 in s
+    return s.replace(LOOP3, "    Patch pa, pb, pc, pd;").replace(LOOPBODY3, LOOPBODY4)
+
+
+PLOAD = """#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);
+          P.d[a][b] = f2{__uint_as_float(v.x), __uint_as_float(v.y)};
+        }"""
+PLOAD12 = """#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, poff[a][0], soff, 0);
+        P.d[a][0] = f2{__uint_as_float(v.x), __uint_as_float(v.y)};
+        P.d[a][1] = f2{__uint_as_float(v.z), __uint_as_float(v.w)};
+        const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][2], soff, 0);
+        P.d[a][2] = f2{__uint_as_float(w.x), __uint_as_float(w.y)};
+      }"""
+
+
+def load12(s):
+    """12 patch loads per lane and step (6 of them 16-byte) instead of 18 8-byte ones, same bytes
+    give or take (wrong data): does the load instruction count or the bytes cost?"""
+    assert PLOAD in s
+    return s.replace(PLOAD, PLOAD12)
+
+
+PLOAD_PAIR = """#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          u32x2 v = {0u, 0u};
+          if (odd == 0) {
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, poff[a][b], soff, 0);
+            v = u32x2{q.x ^ q.z, q.y ^ q.w};
+          }
+          P.d[a][b] = f2{__uint_as_float(v.x), __uint_as_float(v.y)};
+        }"""
+
+
+def pair128(s):
+    """patch loads of two K-steps at once: 16-byte loads on even steps, none on odd (wrong data):
+    the bound for loading a pixel's whole 128-B line of 32 channels once per two steps"""
+    assert PLOAD in s
+    s = s.replace(PLOAD, PLOAD_PAIR)
+    a = "      const int soff = step * KC * 4;"
+    assert a in s
+    return s.replace(a, a + "\n      const int odd = __builtin_amdgcn_readfirstlane(ls & 1);")
+
+
 VARIANTS = {
     "nbg8": nbg(8),
     "nbg16": nbg(16),
@@ -349,6 +442,11 @@ VARIANTS = {
     "st_sc01": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 17);")),
     "reswarm": reswarm,
     "base": lambda s: s,
+    "nonpersist": lambda s: s.replace("dim3(MODE_ == 2 ? cus : std::min(nit, cus))", "dim3(MODE_ == 2 ? cus : (MODE_ == 0 ? nit : std::min(nit, cus)))"),
+    "pair128": pair128,
+    "load12": load12,
+    "u18split": lambda s: s.replace("  constexpr int URING = uring_depth<EPI>();", "  constexpr int URING = MODE == 1 ? 18 : uring_depth<EPI>();"),
+    "pf3": pf3,
     "halftrans": halftrans,
     "halfpatch": halfpatch,
     "halfu": halfu,
