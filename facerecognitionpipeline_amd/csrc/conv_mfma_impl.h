@@ -499,13 +499,19 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_mfma_kernel(ConvParams p
     }
     // slab of this block for this tile: slot 1 if the block had an earlier segment
     const int slot = (lo < (long long)tl * S) ? 1 : 0;
+    // write-through (sc1) slab stores: the release below then has no dirty slab lines to write
+    // back from L2 before the ticket (the last arriver may sit on another XCD)
     float* mine = ws + ((long long)bid * 2 + slot) * (ACC * NTHREADS);
+    const __amdgpu_buffer_rsrc_t mr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)mine, (short)0, ACC * NTHREADS * 4, 0x00020000);
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
       for (int b = 0; b < TN; ++b)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) mine[((a * TN + b) * 16 + e) * NTHREADS + tid] = acc[a][b][e];
+        for (int e = 0; e < 16; ++e)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e]), mr,
+                                                (((a * TN + b) * 16 + e) * NTHREADS + tid) * 4, 0, 16);
     // blocks holding a segment of tile tl: first..last (block ranges are contiguous)
     const long long t_lo = (long long)tl * S, t_hi = t_lo + S;
     int first = (int)((t_lo * P) / U);

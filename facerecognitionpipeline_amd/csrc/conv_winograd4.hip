@@ -83,6 +83,7 @@ template <int EPI>
 constexpr int uring_depth() {
   return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 9 : 12;
 }
+constexpr int CPOL_SC1 = 16;         // buffer-store cache policy bit sc1 (write-through to memory)
 constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum with it is past the range
 // output-geometry tables of the items in flight: the transform waves' load stream runs at most
 // NBUF + 2 K-steps (so items) ahead of the MFMA waves' consumption
@@ -644,6 +645,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       // range start); summed in part order and finished by wino4_part_fixup_kernel
       const int slot = SPLIT ? it.li * p.ksplit + it.split : (s0 == 0 ? bl + 1 : bl) * 2 + (s0 == 0 ? 0 : 1);
       const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
+      // write-through (sc1): the fixup on other XCDs reads the slots right after this launch, and
+      // a launch that leaves its slots dirty in L2 pays for their write-back at the kernel
+      // boundary (serving batch 1: embed + match 1.925 -> 1.851 ms, same box)
 #pragma unroll
       for (int y = 0; y < 4; ++y)
 #pragma unroll
@@ -651,7 +655,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
           const f4 v = out4(y, x);
           const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
           const int off = ((((slot * FT + n) * 16 + y * 4 + x) * FN) + w * 16 + 4 * rg) * 4;
-          __builtin_amdgcn_raw_buffer_store_b128(bits, sr, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(bits, sr, off, 0, CPOL_SC1);
         }
       continue;
     }
@@ -764,7 +768,10 @@ __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
     }
     v[r] = t;
   }
-  *reinterpret_cast<float4*>(p.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
+  // write-through like the slots: the next layer's split-K launch reads this output from every XCD
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(p.y, p.B * H * W * p.Cout * 4);
+  const u32x4 bits = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(bits, yr, (int)(yo * 4), 0, CPOL_SC1);
 }
 
 __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __restrict__ pre_scale,

@@ -43,7 +43,11 @@ def main():
     ap.add_argument("--algos", default="", help="only sweep these conv algorithms (comma list) x --ns")
     ap.add_argument("--ns", default="1,4,16,64")
     ap.add_argument("--graph", type=int, default=0, help="--algos: fr_set_graph_batch value")
+    ap.add_argument("--so", default=None, help="a libfrhip.so build to load instead of the package's (A/B)")
     args = ap.parse_args()
+    if args.so:
+        from facerecognitionpipeline_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(args.so)
     emb = FaceEmbedder(architecture="ir_101", model_path="synthetic", max_batch=256, graph_batch=0)
     G = args.gallery
     base = W.synthetic_crops(G, seed=W.CROP_SEED_GALLERY)
