@@ -590,17 +590,25 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     constexpr bool RES = !SPLIT && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
     constexpr bool PRELU = !SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU);
     const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, RES ? p.B * H * W * Cout * 4 : 0);
-    // byte offsets of tile n's 16 outputs (BIGOFF: outside the images, dropped)
+    // byte offsets of tile n's 16 outputs = a row part + a column part (8 multiplies, not 16).
+    // Padding rows / columns and an idle quarter get BIGOFF, so every sum with them lies past the
+    // buffer's range (unsigned) and the store / residual load is dropped by the range check,
+    // which also drops the pixels of absent images in a partial last canvas row (>= B*H*W).
     const int* gt = geo + ((j % NGEO) * FT + n) * 8;
     int oo[4][4];
+    {
+      int ro[4], co[4];
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int orow = gt[y], ocol = gt[4 + x], pix = orow + ocol;
-        const bool ok = orow >= 0 && ocol >= 0 && pix < p.B * H * W;
-        oo[y][x] = ok && live ? (pix * Cout + cout0) * 4 : BIGOFF;
+      for (int e = 0; e < 4; ++e) {
+        const int orow = gt[e], ocol = gt[4 + e];
+        ro[e] = orow >= 0 && live ? (orow * Cout + cout0) * 4 : BIGOFF;
+        co[e] = ocol >= 0 ? ocol * Cout * 4 : BIGOFF;
       }
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) oo[y][x] = (int)((unsigned)ro[y] + (unsigned)co[x]);
+    }
     // residual rows 0-1 in flight during the output transform of couts 2-3, rows 2-3 while rows
     // 0-1 are stored (issued earlier they would spill beside the 144 accumulators)
     f4 rv[4][4];
@@ -659,12 +667,26 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         }
       continue;
     }
-    f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f}, al = {0.f, 0.f, 0.f, 0.f};
+    f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f}, al = {0.f, 0.f, 0.f, 0.f}, cl = al;
     if constexpr (!SPLIT) {
       sc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
       sh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
     }
-    if constexpr (PRELU) al = *reinterpret_cast<const f4*>(p.prelu + cout0);
+    // PReLU t > 0 ? t : a t as med3(t, a t, c): c = +inf for a slope a <= 1 (= max(t, a t)),
+    // -inf for a > 1 (= min(t, a t)); med3 returns one of its operands, so the value is the
+    // reference's exactly (up to the sign of a zero), in a packed multiply and a med3 per value
+    // instead of a multiply, a compare and a select
+    if constexpr (PRELU) {
+      al = *reinterpret_cast<const f4*>(p.prelu + cout0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cl[r] = al[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
+    }
+    auto prelu4 = [&](f4 v) {
+      const f4 av = v * al;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = __builtin_amdgcn_fmed3f(v[r], av[r], cl[r]);
+      return v;
+    };
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
       if constexpr (SK && RES) {
@@ -680,14 +702,10 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         f4 v = out4(y, x);
         if constexpr (!SPLIT) {
           v = __builtin_elementwise_fma(v, sc, sh);
-          if constexpr (EPI == EPI_AFFINE_PRELU)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * al[r];
+          if constexpr (EPI == EPI_AFFINE_PRELU) v = prelu4(v);
           if constexpr (RES) {
             v += rv[y][x];
-            if constexpr (EPI == EPI_AFFINE_RES_PRELU)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * al[r];
+            if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = prelu4(v);
           }
         }
         const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};

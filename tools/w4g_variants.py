@@ -412,6 +412,37 @@ def pair128(s):
     return s.replace(a, a + "\n      const int odd = __builtin_amdgcn_readfirstlane(ls & 1);")
 
 
+REFILL = """#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int y = x + e;
+          uring[y % URING] = y + URING < NXI ? ld4(ur, lo, (y + URING) * XS + cur)
+                                             : ld4(ur, lo, (y + URING - NXI) * XS + nxt);
+        }"""
+
+
+def nofirstrefill(s):
+    """no U refills in an item's first K-step (wrong results): the cost of those refills waiting
+    behind the previous epilogue's stores in vmcnt order (plus 1/KS of the U traffic)"""
+    for a in (REFILL, "    auto kstep = [&](int s) {", "    kstep(s0);\n", "for (int s = s0 + 1; s < s1; ++s) kstep(s);"):
+        assert a in s, a
+    s = s.replace(REFILL, "        if constexpr (!decltype(FIRST)::value)\n" + REFILL)
+    s = s.replace("    auto kstep = [&](int s) {", "    auto kstep = [&](int s, auto FIRST) {")
+    s = s.replace("    kstep(s0);\n", "    kstep(s0, std::true_type{});\n")
+    s = s.replace("for (int s = s0 + 1; s < s1; ++s) kstep(s);", "for (int s = s0 + 1; s < s1; ++s) kstep(s, std::false_type{});")
+    return "#include <type_traits>\n" + s
+
+
+def noscale(s):
+    """epilogue BN scale / shift / PReLU slopes as constants instead of per-item global loads
+    (wrong results): the cost of those loads' latency, exposed in the MFMA waves' epilogue"""
+    for a, b in (("      sc = *reinterpret_cast<const f4*>(p.post_scale + cout0);", "      sc = f4{1.01f, 0.99f, 1.02f, 0.98f};"),
+                 ("      sh = *reinterpret_cast<const f4*>(p.post_shift + cout0);", "      sh = f4{0.01f, -0.01f, 0.02f, -0.02f};"),
+                 ("      al = *reinterpret_cast<const f4*>(p.prelu + cout0);", "      al = f4{0.25f, 0.2f, 0.3f, 0.1f};")):
+        assert a in s, a
+        s = s.replace(a, b)
+    return s
+
+
 VARIANTS = {
     "nbg8": nbg(8),
     "nbg16": nbg(16),
@@ -442,6 +473,8 @@ VARIANTS = {
     "st_sc01": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 17);")),
     "reswarm": reswarm,
     "base": lambda s: s,
+    "noscale": noscale,
+    "nofirstrefill": nofirstrefill,
     "nonpersist": lambda s: s.replace("dim3(MODE_ == 2 ? cus : std::min(nit, cus))", "dim3(MODE_ == 2 ? cus : (MODE_ == 0 ? nit : std::min(nit, cus)))"),
     "pair128": pair128,
     "load12": load12,
