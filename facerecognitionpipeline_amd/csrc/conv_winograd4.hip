@@ -896,6 +896,11 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   // the K-steps and the slot workspace; ks_per steps each
   auto split_of = [&](int n, int& ks_per) {
     int S = (int)std::min<long long>(std::min(KST, cus / n), p.part_floats / (SLOT * n));
+    // a grid of one-K-step splits over more than half the chip loses to half the grid with two
+    // steps each (half the slots for the fixup to sum): IR-101 batch 4, 2.37 -> 2.18 ms per
+    // embed + match; batch 1 (64 workgroups at stage 3) and batch 8 (two-step splits over the
+    // whole chip; halving them again cost +2.6%) keep theirs
+    if (S * n > cus / 2 && (KST + S - 1) / S < 2) S = std::max(1, std::min(S, (cus / 2) / n));
     if (p.max_split > 0) S = std::min(S, p.max_split);
     ks_per = KST;
     if (S > 1) {

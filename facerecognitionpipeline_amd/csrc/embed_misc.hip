@@ -28,15 +28,17 @@ constexpr int STEM_C = 64;
 // fmaf sequence as the scalar 27-tap loop it replaces; the padded tap adds 0 * x.  Per 16 pixels x
 // 64 channels: 28 MFMAs (the VALU version's 1,728 FMAs), 7 LDS reads, 4 stores; the kernel is
 // bound by its 822 MB (B = 256) output write.
-constexpr int STEM_ROWS = 16;
+// STEM_ROWS output rows per block: 16 for batches (fewer halo rows re-read), 4 for serving
+// batches of <= 8 crops, whose 7 blocks per image would leave the chip idle (batch 1: 26 -> 9 us)
 constexpr int STEM_W = IMG + 2;  // staged row width with the halo
-static_assert(IMG % STEM_ROWS == 0 && IMG % 16 == 0, "row blocks and 16-pixel groups must tile the image");
 typedef float stem_f4 __attribute__((ext_vector_type(4)));
+template <int STEM_ROWS>
 __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ img, const float* __restrict__ lut,
                                                    const float* __restrict__ w27x64,
                                                    const float* __restrict__ bn_scale,
                                                    const float* __restrict__ bn_shift,
                                                    const float* __restrict__ prelu, float* __restrict__ y) {
+  static_assert(IMG % STEM_ROWS == 0 && IMG % 16 == 0, "row blocks and 16-pixel groups must tile the image");
   __shared__ float s_lut[256];
   __shared__ float s_in[(STEM_ROWS + 2) * STEM_W * 3 + 1];  // + one zero cell for the padded tap
   // per-wave output transpose: [16 pixels][64 channels + 4 pad] (MFMA layout in, row-major out)
@@ -154,8 +156,12 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
 hipError_t launch_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, const float* bn_scale,
                        const float* bn_shift, const float* prelu, float* y, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(stem_kernel, dim3(B * (IMG / STEM_ROWS)), dim3(256), 0, s, img, lut, w27x64, bn_scale, bn_shift,
-                     prelu, y);
+  if (B <= 8)
+    hipLaunchKernelGGL(stem_kernel<4>, dim3(B * (IMG / 4)), dim3(256), 0, s, img, lut, w27x64, bn_scale, bn_shift,
+                       prelu, y);
+  else
+    hipLaunchKernelGGL(stem_kernel<16>, dim3(B * (IMG / 16)), dim3(256), 0, s, img, lut, w27x64, bn_scale,
+                       bn_shift, prelu, y);
   return hipGetLastError();
 }
 
@@ -170,56 +176,94 @@ __device__ __forceinline__ float block_sum_256(float v, float* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// One block (256 threads, 2 columns each) per embedding row, D = 512.
-__global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restrict__ partial, int nsplit,
-                                                          long long split_stride, const float* __restrict__ fc_bias,
-                                                          const float* __restrict__ bn_scale,
-                                                          const float* __restrict__ bn_shift, float* __restrict__ emb,
-                                                          int normalize, int model_l2) {
-  __shared__ float red[4];
+// Block-wide sum over 1024 threads whose waves 4..15 hold zeros: the same value as
+// block_sum_256 over waves 0..3 (the extra terms add exact zeros).
+__device__ __forceinline__ float block_sum_1024(float v, float* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int wid = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[wid] = v;
+  __syncthreads();
+  float r = (red[0] + red[1]) + (red[2] + red[3]);
+#pragma unroll
+  for (int w = 4; w < 16; ++w) r += red[w];
+  return r;
+}
+
+// One block per embedding row, D = 512: 4 groups of 256 threads (2 columns per thread) sum
+// split ranges g*nsplit/4 .. (g+1)*nsplit/4 with eight loads in flight each, and the group sums
+// are added in group order (deterministic).  One group per row walked all splits in turn: the
+// 196-split serving FC's reduce took 15 us at batch 1, a chain of 25 load latencies.
+__global__ __launch_bounds__(1024) void head_reduce_kernel(const float* __restrict__ partial, int nsplit,
+                                                           long long split_stride, const float* __restrict__ fc_bias,
+                                                           const float* __restrict__ bn_scale,
+                                                           const float* __restrict__ bn_shift, float* __restrict__ emb,
+                                                           int normalize, int model_l2) {
+  __shared__ float part[3][512];
+  __shared__ float red[16];
   const int row = blockIdx.x;
-  const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
+  const int g = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int c0 = t, c1 = t + 256;
   float v0 = 0.f, v1 = 0.f;
   const float* p = partial + (long long)row * 512;
-  // eight splits' loads in flight at a time, summed in split order (deterministic)
-  for (int s0 = 0; s0 < nsplit; s0 += 8) {
+  const int s_lo = g * nsplit / 4, s_hi = (g + 1) * nsplit / 4;
+  for (int s0 = s_lo; s0 < s_hi; s0 += 8) {
     float a0[8], a1[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const bool ok = s0 + u < nsplit;
+      const bool ok = s0 + u < s_hi;
       a0[u] = ok ? p[(long long)(s0 + u) * split_stride + c0] : 0.f;
       a1[u] = ok ? p[(long long)(s0 + u) * split_stride + c1] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (s0 + u < nsplit) {
+      if (s0 + u < s_hi) {
         v0 += a0[u];
         v1 += a1[u];
       }
   }
-  v0 += fc_bias[c0];
-  v1 += fc_bias[c1];
-  v0 = v0 * bn_scale[c0] + bn_shift[c0];
-  v1 = v1 * bn_scale[c1] + bn_shift[c1];
+  if (g > 0) {
+    part[g - 1][c0] = v0;
+    part[g - 1][c1] = v1;
+  }
+  __syncthreads();
+  // group 0 finishes the row; the other groups stay for the block-wide norms with zeros (x + 0
+  // is exact, so the sums are those of group 0's four waves)
+  if (g == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      v0 += part[k][c0];
+      v1 += part[k][c1];
+    }
+    v0 += fc_bias[c0];
+    v1 += fc_bias[c1];
+    v0 = v0 * bn_scale[c0] + bn_shift[c0];
+    v1 = v1 * bn_scale[c1] + bn_shift[c1];
+  } else {
+    v0 = v1 = 0.f;
+  }
   if (model_l2) {  // AdaFace forward tail x / ||x|| (ArcFace's model has none)
-    const float norm = sqrtf(block_sum_256(v0 * v0 + v1 * v1, red));
+    const float norm = sqrtf(block_sum_1024(v0 * v0 + v1 * v1, red));
     v0 = v0 / norm;
     v1 = v1 / norm;
   }
   if (normalize) {
-    const float n2 = sqrtf(block_sum_256(v0 * v0 + v1 * v1, red)) + 1e-8f;
+    const float n2 = sqrtf(block_sum_1024(v0 * v0 + v1 * v1, red)) + 1e-8f;
     v0 = v0 / n2;
     v1 = v1 / n2;
   }
-  emb[(long long)row * 512 + c0] = v0;
-  emb[(long long)row * 512 + c1] = v1;
+  if (g == 0) {
+    emb[(long long)row * 512 + c0] = v0;
+    emb[(long long)row * 512 + c1] = v1;
+  }
 }
 
 hipError_t launch_head_reduce(const float* partial, int nsplit, long long split_stride, const float* fc_bias,
                               const float* bn_scale, const float* bn_shift, float* emb, int n, int normalize,
                               int model_l2, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(head_reduce_kernel, dim3(n), dim3(256), 0, s, partial, nsplit, split_stride, fc_bias, bn_scale,
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(n), dim3(1024), 0, s, partial, nsplit, split_stride, fc_bias, bn_scale,
                      bn_shift, emb, normalize, model_l2);
   return hipGetLastError();
 }
