@@ -338,13 +338,9 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sco
 // best KMAX (score, index) pairs of a strided slice in registers (unrolled insertion, no
 // runtime-indexed arrays), then k block-wide arg-max rounds pop the global best in order.
 template <int KMAX>
-__global__ __launch_bounds__(256) void topk_small_kernel(const float* __restrict__ scores, int G, int k,
-                                                         int32_t* __restrict__ idx, float* __restrict__ val) {
-  __shared__ float s_s[4];
-  __shared__ int s_i[4];
-  const int row = blockIdx.x;
+__device__ __forceinline__ void topk_row_small(const float* __restrict__ r, int G, int k, int32_t* __restrict__ idx,
+                                               float* __restrict__ val, float* s_s, int* s_i) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const float* r = scores + (long long)row * G;
   float ls[KMAX];
   int li[KMAX];
 #pragma unroll
@@ -407,8 +403,8 @@ __global__ __launch_bounds__(256) void topk_small_kernel(const float* __restrict
       }
     __syncthreads();
     if (tid == 0) {
-      idx[(long long)row * k + t] = bi < 0 ? -1 : bi;
-      val[(long long)row * k + t] = bs;
+      idx[t] = bi < 0 ? -1 : bi;
+      val[t] = bs;
     }
     if (li[0] == bi && bi >= 0) {  // indices are unique: exactly one owner pops
 #pragma unroll
@@ -420,6 +416,69 @@ __global__ __launch_bounds__(256) void topk_small_kernel(const float* __restrict
       li[KMAX - 1] = NO_ROW;
     }
   }
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void topk_small_kernel(const float* __restrict__ scores, int G, int k,
+                                                         int32_t* __restrict__ idx, float* __restrict__ val) {
+  __shared__ float s_s[4];
+  __shared__ int s_i[4];
+  const int row = blockIdx.x;
+  topk_row_small<KMAX>(scores + (long long)row * G, G, k, idx + (long long)row * k, val + (long long)row * k, s_s, s_i);
+}
+
+// Serving-sized match scores: block (64 gallery rows, query q) of 256 threads.  The query is
+// normalised exactly as l2norm_rows_kernel does it (same per-thread terms, same block reduction),
+// kept in LDS, and each group of 4 lanes dots one gallery row, a quarter of the 512 dimensions per
+// lane (32 float4 loads, 8 in flight), the quarters summed in a fixed order.  For n <= 16 it
+// replaces l2norm + the implicit-GEMM score launch (a stream-K grid over a 1-row M): batch-1
+// embed + match 1.823 -> 1.810 ms.  (Taking the top-k in the query's last-arriving block as well
+// -- release, arrival ticket, acquire -- measured the same 1.810 ms as the separate top-k launch.)
+__global__ __launch_bounds__(256) void scores_small_kernel(const float* __restrict__ q,
+                                                           const float* __restrict__ gallery, int G,
+                                                           float* __restrict__ scores) {
+  __shared__ float red[4];
+  __shared__ __attribute__((aligned(16))) float qn[512];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int qi = blockIdx.y;
+  const float* r = q + (long long)qi * 512;
+  const float r0 = r[tid], r1 = r[tid + 256];
+  const float nrm = sqrtf(block_sum_256(r0 * r0 + r1 * r1, red)) + 1e-8f;
+  qn[tid] = r0 / nrm;
+  qn[tid + 256] = r1 / nrm;
+  __syncthreads();
+  const int row = blockIdx.x * 64 + w * 16 + (lane & 15), part = lane >> 4;
+  float acc = 0.f;
+  if (row < G) {
+    const float4* g4 = reinterpret_cast<const float4*>(gallery + (long long)row * 512 + part * 128);
+    const float4* q4 = reinterpret_cast<const float4*>(qn + part * 128);
+    for (int c0 = 0; c0 < 32; c0 += 8) {
+      float4 a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = g4[c0 + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 b = q4[c0 + u];
+        acc = fmaf(a[u].x, b.x, acc);
+        acc = fmaf(a[u].y, b.y, acc);
+        acc = fmaf(a[u].z, b.z, acc);
+        acc = fmaf(a[u].w, b.w, acc);
+      }
+    }
+  }
+  // quarters in order: (p0 + p1) + (p2 + p3)
+  const float o1 = __shfl_xor(acc, 16, 64);
+  const float s01 = (lane & 16) ? o1 + acc : acc + o1;
+  const float o2 = __shfl_xor(s01, 32, 64);
+  const float sum = (lane & 32) ? o2 + s01 : s01 + o2;
+  if (part == 0 && row < G) scores[(long long)qi * G + row] = sum;
+}
+
+hipError_t launch_scores_small(const float* q, const float* gallery, int G, float* scores, int n, hipStream_t s) {
+  if (n <= 0 || G <= 0) return hipSuccess;
+  if (n > 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scores_small_kernel, dim3((G + 63) / 64, n), dim3(256), 0, s, q, gallery, G, scores);
+  return hipGetLastError();
 }
 
 hipError_t launch_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, hipStream_t s) {

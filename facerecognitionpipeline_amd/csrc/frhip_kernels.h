@@ -152,6 +152,9 @@ hipError_t launch_head_reduce(const float* partial, int nsplit, long long split_
 
 // q / (||q|| + 1e-8) row-wise over D=512 rows.
 hipError_t launch_l2norm_rows(const float* q, float* out, int n, int d, hipStream_t s);
+// serving-sized match scores (n <= 16 queries, D = 512): q / (||q|| + 1e-8) as l2norm_rows computes
+// it, fused with the scores against the G x 512 gallery rows: scores [n][G]
+hipError_t launch_scores_small(const float* q, const float* gallery, int G, float* scores, int n, hipStream_t s);
 
 // Per row of a [n][G] score matrix: top-k by (score desc, index asc).
 hipError_t launch_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, hipStream_t s);

@@ -698,7 +698,18 @@ int match_device(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float
   if (h->G <= 0) return fail(h, FR_ERR_STATE, "gallery is empty (fr_gallery_set first)");
   if (k < 1 || k > h->G) return fail(h, FR_ERR_INVALID_ARGUMENT, "k must be in [1, G]");
   if (n <= 0) return FR_OK;
-  int rc = ensure_buf(h, (void**)&h->qn, &h->qn_cap, (size_t)n * 512 * sizeof(float));
+  int rc;
+  if (n <= 16 && (long long)n * h->G * 4 < (1ll << 31)) {
+    // serving-sized: normalisation fused into one scores launch (embed_misc.hip), then top-k
+    rc = ensure_buf(h, (void**)&h->scores, &h->scores_cap, (size_t)n * h->G * sizeof(float));
+    if (rc) return rc;
+    ProfScope ps(h, s, 0.0, 0);
+    hipError_t e = launch_scores_small(Q, h->gallery, h->G, h->scores, n, s);
+    if (e == hipSuccess) e = launch_topk(h->scores, n, h->G, k, idx, score, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("match launch: ") + hipGetErrorString(e));
+    return FR_OK;
+  }
+  rc = ensure_buf(h, (void**)&h->qn, &h->qn_cap, (size_t)n * 512 * sizeof(float));
   if (rc) return rc;
   if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");

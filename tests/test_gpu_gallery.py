@@ -243,3 +243,41 @@ def test_match_scores_over_2gib_are_chunked(handle):
     assert torch.equal(idx[:, 0].long(), rows)
     assert (score[:, 0] - 1).abs().max().item() < 1e-5 and score[:, 1].max().item() < 0.5
     handle.gallery_set(torch.empty((0, 512), device="cuda"))
+
+
+@pytest.mark.parametrize("G", [1, 7, 64, 1000, 4099])
+def test_small_batch_match_vs_reference(handle, G):
+    """Serving-sized match (n <= 16: normalisation fused into the scores launch, then top-k) and
+    the batched path (n = 17: l2norm + score GEMM + top-k) vs ``search``'s arithmetic in float64
+    (gallery_manager.py:195-197).  Ties are planted (duplicate rows): they must rank by
+    descending row, the documented policy.  Run twice: reused workspaces."""
+    g = np.random.default_rng(G)
+    E = g.standard_normal((G, 512)).astype(np.float32)
+    E /= np.linalg.norm(E, axis=1, keepdims=True)
+    if G >= 7:
+        E[G // 2] = E[1]  # a tie with row 1
+    handle.gallery_set(torch.from_numpy(E).cuda())
+    Q = g.standard_normal((17, 512)).astype(np.float32)
+    Q[2] = E[min(1, G - 1)] * 3.0        # exact-tie query (G >= 7): rows 1 and G // 2 score the same
+    for n in (1, 5, 16, 17):
+        k = min(8 if n <= 16 else 5, G)
+        q = torch.from_numpy(Q[:n]).cuda()
+        for _ in range(2):
+            idx = torch.empty((n, k), dtype=torch.int32, device="cuda")
+            sc = torch.empty((n, k), dtype=torch.float32, device="cuda")
+            handle.match(q, k, idx, sc)
+            torch.cuda.synchronize()
+            qn = Q[:n].astype(np.float64) / (np.linalg.norm(Q[:n].astype(np.float64), axis=1, keepdims=True) + 1e-8)
+            S = qn @ E.astype(np.float64).T
+            assert np.abs(sc.cpu().numpy() - np.take_along_axis(S, idx.cpu().numpy().astype(np.int64), 1)).max() < 2e-6
+            order = np.argsort(-S, axis=1, kind="stable")[:, :k]
+            got = idx.cpu().numpy()
+            for r in range(n):
+                srt = np.sort(S[r])[::-1]
+                top = srt[:k + 1]
+                margin = np.min(np.abs(np.diff(top))) if top.size > 1 else 1.0
+                if margin > 1e-5:
+                    assert np.array_equal(got[r], order[r]), (n, r)
+            if n >= 3 and G >= 7:
+                assert set(got[2][:2].tolist()) == {1, G // 2} and got[2][0] == max(1, G // 2)
+    handle.gallery_set(torch.empty((0, 512), device="cuda"))
