@@ -32,6 +32,52 @@ hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, in
   return launch_conv_f32_w4(p, tile, pre, epi, nsplit, s);
 }
 
+// Split-K finish of a serving-sized direct conv: y[m][n] = epilogue(sum over the S raw slabs
+// part[s][m][n], in split order: deterministic), the epilogue exactly as conv_mfma_kernel's
+// (v * scale + shift, then the residual: same row / the MaxPool2d(1, 2) shortcut pixel).  One
+// thread per output; every slab load of a thread is in flight at once (S <= 32).
+template <int EPI>
+__global__ __launch_bounds__(256) void conv_split_fixup_kernel(ConvParams p, const float* __restrict__ part, int S,
+                                                               long long stride) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)p.M * p.Cout) return;
+  float a[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) a[k] = k < S ? part[k * stride + i] : 0.f;
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; ++k)
+    if (k < S) v += a[k];
+  const int n = (int)(i % p.Cout);
+  const int m = (int)(i / p.Cout);
+  v = v * p.post_scale[n] + p.post_shift[n];
+  if constexpr (EPI == EPI_AFFINE_RES) v += p.res[i];
+  if constexpr (EPI == EPI_AFFINE_RES_SUB) {
+    const int HoWo = p.Ho * p.Wo;
+    const int b = m / HoWo, rem = m - b * HoWo, oy = rem / p.Wo, ox = rem - oy * p.Wo;
+    v += p.res[(((long long)b * p.res_H + 2 * oy) * p.res_W + 2 * ox) * p.Cout + n];
+  }
+  p.y[i] = v;
+}
+
+hipError_t launch_conv_split_fixup(const ConvParams& p, Epi epi, const float* part, int S, long long stride,
+                                   hipStream_t s) {
+  if (S < 1 || S > 32) return hipErrorInvalidValue;
+  const long long n = (long long)p.M * p.Cout;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  switch (epi) {
+    case EPI_AFFINE: hipLaunchKernelGGL(conv_split_fixup_kernel<EPI_AFFINE>, grid, dim3(256), 0, s, p, part, S, stride); break;
+    case EPI_AFFINE_RES:
+      hipLaunchKernelGGL(conv_split_fixup_kernel<EPI_AFFINE_RES>, grid, dim3(256), 0, s, p, part, S, stride);
+      break;
+    case EPI_AFFINE_RES_SUB:
+      hipLaunchKernelGGL(conv_split_fixup_kernel<EPI_AFFINE_RES_SUB>, grid, dim3(256), 0, s, p, part, S, stride);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 int conv_tile_bm(ConvTile t) {
   switch (t) {
     case TILE_256x64: case TILE_256x128: case TILE_256x128_W8: case TILE_256x64_W8: return 256;

@@ -72,6 +72,10 @@ enum ConvTile : int {
 // split-bf16 "bf16x3" (x = hi + lo, x.y ~= hi.hi + hi.lo + lo.hi, f32 accumulation).
 enum Precision : int { PREC_F32 = 0, PREC_BF16X3 = 1 };
 
+// y = epilogue(sum of S raw split-K slabs part[s][M][Cout], in split order) for EPI_AFFINE,
+// EPI_AFFINE_RES and EPI_AFFINE_RES_SUB (conv_mfma.hip; serving-sized direct convs)
+hipError_t launch_conv_split_fixup(const ConvParams& p, Epi epi, const float* part, int S, long long stride,
+                                   hipStream_t s);
 hipError_t launch_conv(const ConvParams& p, ConvTile tile, bool pre, Epi epi, int nsplit, hipStream_t s,
                        Precision prec = PREC_F32);
 int conv_tile_bm(ConvTile t);

@@ -399,6 +399,29 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // the head FC (split-K) of a serving batch (M = n <= 64 rows) or of <= 256 crops (tools/fc_sweep.py,
   // 32 splits: --batch 128 43.0 us on 128x64/W8 vs 106 on 256x128/W8; --batch 256 69.3 vs 111.8)
   if (!h->detector && nsplit > 1 && cw.kh == 7 && p.M <= 256) tile = p.M <= 64 ? TILE_64x128 : TILE_128x64_W8;
+  // serving batches: a stride-2 conv2 (+ fused shortcut) as a split-K launch of >= 4 K-steps per
+  // split in one round of workgroups, then a parallel fixup, instead of stream-K, whose last
+  // arriver per tile summed ~20 slabs of 32 KB alone (batch 1: 26-31 us per launch)
+  if (!h->detector && nsplit == 1 && p.M <= 4096 && cw.kh == 3 && h->prec == PREC_F32 && !cw.pre_scale &&
+      (epi == EPI_AFFINE || epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_SUB) && sk_ws && h->cus > 0) {
+    const long long ntile = (long long)((p.M + 63) / 64) * ((p.Cout + 127) / 128);
+    const long long cap = (L ? L->sk_ws_floats : h->sk_ws_floats) / ((long long)p.M * p.Cout);
+    int S = (int)std::min<long long>(std::min<long long>(32, p.steps_total / 4), std::min<long long>(h->cus / ntile, cap));
+    if (S > 1) {
+      ConvParams q = p;
+      q.sk_cus = 0;
+      q.steps_per_split = (p.steps_total + S - 1) / S;
+      S = (p.steps_total + q.steps_per_split - 1) / q.steps_per_split;
+      q.split_stride = (long long)p.M * p.Cout;
+      q.y = sk_ws;
+      q.res = nullptr;
+      ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
+      hipError_t e = launch_conv(q, TILE_64x128, false, EPI_RAW, S, s, h->prec);
+      if (e == hipSuccess) e = launch_conv_split_fixup(p, epi, sk_ws, S, q.split_stride, s);
+      if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv split-K launch: ") + hipGetErrorString(e));
+      return FR_OK;
+    }
+  }
   ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
   hipError_t e = launch_conv(p, tile, cw.pre_scale != nullptr, epi, nsplit, s, h->prec);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("conv launch: ") + hipGetErrorString(e));
