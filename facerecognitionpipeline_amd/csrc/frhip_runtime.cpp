@@ -532,8 +532,9 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
   for (int l = 0; l < nl; ++l) {
     const int n = cnt[l];
     const long long split_stride = (long long)n * 512;
-    // serving batches (4 n <= max_batch): the FC's 784 K-steps in 196 splits of 4, so its 51 MB
-    // of weights stream through many workgroups (batch 1: 78 us with 49); larger batches in 32
+    // serving batches (4 n <= max_batch): the FC's 784 K-steps in 98 splits of 8, so its 51 MB
+    // of weights stream through many workgroups (batch 1: 78 us with 49 splits on 256x128, 27.7
+    // with 196 on 64x128, 24.8 with 98: tools/fc_sweep.py --batch 1); larger batches in 32
     // splits of 25 (tools/fc_sweep.py: B = 256 79.2 -> 69.3 us, a 128-crop lane 47.3 -> 43.0,
     // vs 49 splits).  Decided by n alone (every lane's partials hold HEAD_PARTS x max_batch
     // rows), so a lane's part computes exactly as a one-lane forward of the same crops.

@@ -97,8 +97,8 @@ struct fr_handle {
   float* sc_buf = nullptr;
   float* partial = nullptr;
   // head FC split-K parts: serving batches (4 n <= max_batch) / larger; partial buffers hold
-  // HEAD_PARTS x max_batch rows (>= 196 n for the serving split, >= 32 n for the other)
-  static constexpr int HEAD_SPLIT_SMALL = 196, HEAD_SPLIT = 32, HEAD_PARTS = 49;
+  // HEAD_PARTS x max_batch rows (>= 98 n for the serving split at 4 n <= max_batch, >= 32 n for the other)
+  static constexpr int HEAD_SPLIT_SMALL = 98, HEAD_SPLIT = 32, HEAD_PARTS = 49;
   uint8_t* in_stage = nullptr;
   float* emb_stage = nullptr;
 
