@@ -142,13 +142,13 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ i
       *reinterpret_cast<stem_f4*>(so + m * 68 + 16 * cb + 4 * rg) = o;
     }
     float* out = y + (((size_t)b * IMG + oy0 + r) * IMG + px - m) * STEM_C;  // the group's first pixel
-    // streaming (nt) stores: the 822 MB output is read back by the next layer from HBM anyway,
-    // and nt keeps it from evicting the input rows and the LUT (same box: 194 -> 191 us)
+    // plain stores: nontemporal ones measured 194 -> 191 us on the stem alone but 149 -> 184 us
+    // inside the forward
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int pp = 4 * j + (lane >> 4);  // pixel of the group, 16-byte channel piece lane & 15
-      __builtin_nontemporal_store(*reinterpret_cast<const stem_f4*>(so + pp * 68 + 4 * (lane & 15)),
-                                  reinterpret_cast<stem_f4*>(out + pp * STEM_C + 4 * (lane & 15)));
+      *reinterpret_cast<stem_f4*>(out + pp * STEM_C + 4 * (lane & 15)) =
+          *reinterpret_cast<const stem_f4*>(so + pp * 68 + 4 * (lane & 15));
     }
   }
 }
