@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void det_stem_kernel(const uint8_t* __restrict
                                                        const float* __restrict__ w27xC,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, float* __restrict__ y) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_w = smem;              // [27][C]
   float* s_in = smem + 27 * C;    // [3][W + 2][3]
   const int Ho = H / 2, Wo = W / 2;
@@ -93,48 +93,68 @@ __global__ __launch_bounds__(256) void det_stem_kernel(const uint8_t* __restrict
 #pragma unroll
         for (int ci = 0; ci < 3; ++ci) {
           const float v = s_in[(ky * (W + 2) + 2 * ox + kx) * 3 + ci];
-          const float* wr = s_w + ((ky * 3 + kx) * 3 + ci) * C + cg;
+          // the tap's 8 weights as two 16-byte LDS reads (8 single-float reads made the kernel
+          // LDS-issue bound: 320 us per 32-frame batch)
+          const float4* wr = reinterpret_cast<const float4*>(s_w + ((ky * 3 + kx) * 3 + ci) * C + cg);
+          const float4 w0 = wr[0], w1 = wr[1];
+          const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-          for (int k = 0; k < 8; ++k) acc[k] = __builtin_fmaf(v, wr[k], acc[k]);
+          for (int k = 0; k < 8; ++k) acc[k] = __builtin_fmaf(v, wk[k], acc[k]);
         }
-    float* dst = y + (((long long)f * Ho + oy) * Wo + ox) * C + cg;
+    float o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) dst[k] = fmaxf(__builtin_fmaf(acc[k], sc[k], sh[k]), 0.f);
+    for (int k = 0; k < 8; ++k) o[k] = fmaxf(__builtin_fmaf(acc[k], sc[k], sh[k]), 0.f);
+    float4* dst = reinterpret_cast<float4*>(y + (((long long)f * Ho + oy) * Wo + ox) * C + cg);
+    dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_float4(o[4], o[5], o[6], o[7]);
   }
 }
 
-__global__ __launch_bounds__(256) void maxpool3_kernel(const float* __restrict__ x, int B, int H, int W, int C,
-                                                       float* __restrict__ y) {
+// MaxPool2d(3, 2, 1) in NHWC, one thread per (output pixel, 4 channels): float4 loads of the 9
+// taps, 32-bit index arithmetic.  (One thread per element with 64-bit div / mod took 519 us for
+// a 32-frame 320x320x32 map, a fifth of the HBM rate.)  fmaxf per element as before: bit-exact.
+__global__ __launch_bounds__(256) void maxpool3_kernel(const float4* __restrict__ x, int B, int H, int W, int C4,
+                                                       float4* __restrict__ y) {
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)B * Ho * Wo * C) return;
-  const int c = (int)(i % C);
-  long long r = i / C;
-  const int ox = (int)(r % Wo);
-  r /= Wo;
-  const int oy = (int)(r % Ho);
-  const int b = (int)(r / Ho);
-  float m = -INFINITY;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * Ho * Wo * C4) return;
+  const int c = i % C4;
+  const int pix = i / C4;
+  const int ox = pix % Wo, t = pix / Wo;
+  const int oy = t % Ho, b = t / Ho;
+  float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
   for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
     for (int dx = -1; dx <= 1; ++dx) {
       const int iy = 2 * oy + dy, ix = 2 * ox + dx;
-      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-        m = fmaxf(m, x[(((long long)b * H + iy) * W + ix) * C + c]);
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
+        const float4 v = x[((b * H + iy) * W + ix) * C4 + c];
+        m.x = fmaxf(m.x, v.x);
+        m.y = fmaxf(m.y, v.y);
+        m.z = fmaxf(m.z, v.z);
+        m.w = fmaxf(m.w, v.w);
+      }
     }
   y[i] = m;
 }
 
-__global__ __launch_bounds__(256) void upsample_add_kernel(float* __restrict__ big, const float* __restrict__ small,
-                                                           int B, int h, int w, int C) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)B * 4 * h * w * C) return;
-  const int c = (int)(i % C);
-  long long r = i / C;
-  const int x = (int)(r % (2 * w));
-  r /= 2 * w;
-  const int yy = (int)(r % (2 * h));
-  const int b = (int)(r / (2 * h));
-  big[i] = big[i] + small[(((long long)b * h + yy / 2) * w + x / 2) * C + c];
+// FPN top-down: big += nearest-2x(small), NHWC, one thread per (pixel, 4 channels), 32-bit indices
+__global__ __launch_bounds__(256) void upsample_add_kernel(float4* __restrict__ big, const float4* __restrict__ small,
+                                                           int B, int h, int w, int C4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * 4 * h * w * C4) return;
+  const int c = i % C4;
+  const int pix = i / C4;
+  const int x = pix % (2 * w), t = pix / (2 * w);
+  const int yy = t % (2 * h), b = t / (2 * h);
+  const float4 s = small[((b * h + yy / 2) * w + x / 2) * C4 + c];
+  float4 v = big[i];
+  v.x = v.x + s.x;
+  v.y = v.y + s.y;
+  v.z = v.z + s.z;
+  v.w = v.w + s.w;
+  big[i] = v;
 }
 
 // Head outputs per level: [B][H*W][32] f32 = [cls a0, cls a1, bbox a0 (4), bbox a1 (4),
@@ -274,15 +294,21 @@ hipError_t launch_det_stem(const uint8_t* img, int n, int H, int W, int C, const
 hipError_t launch_maxpool3(const float* x, int B, int H, int W, int C, float* y, hipStream_t s) {
   const long long total = (long long)B * ((H - 1) / 2 + 1) * ((W - 1) / 2 + 1) * C;
   if (total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(maxpool3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, B, H, W, C, y);
+  if (C % 4 || (long long)B * H * W * C >= (1ll << 31) ||
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool3_kernel, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(x), B, H, W, C / 4, reinterpret_cast<float4*>(y));
   return hipGetLastError();
 }
 
 hipError_t launch_upsample_add(float* big, const float* small, int B, int h, int w, int C, hipStream_t s) {
   const long long total = (long long)B * 4 * h * w * C;
   if (total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, big, small, B, h,
-                     w, C);
+  if (C % 4 || total >= (1ll << 31) || ((reinterpret_cast<uintptr_t>(big) | reinterpret_cast<uintptr_t>(small)) & 15))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<float4*>(big), reinterpret_cast<const float4*>(small), B, h, w, C / 4);
   return hipGetLastError();
 }
 
