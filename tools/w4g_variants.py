@@ -443,6 +443,23 @@ def noscale(s):
     return s
 
 
+def aprio(s):
+    """transform waves at issue priority only while the ring holds <= 1 transformed step ahead of
+    the slowest MFMA wave (else priority 0), for every epilogue"""
+    a = "    if constexpr (PRE) __builtin_amdgcn_s_setprio(1);\n"
+    b = "      store(P, g);\n"
+    assert a in s and b in s
+    s = s.replace(a, "")
+    return s.replace(b, "      {\n        const int ahead = g - lds_min4(fre);\n"
+                        "        if (ahead <= 1) __builtin_amdgcn_s_setprio(1); else __builtin_amdgcn_s_setprio(0);\n"
+                        "      }\n" + b)
+
+
+def aprio2(s):
+    """aprio with the threshold at 2 steps ahead"""
+    return aprio(s).replace("if (ahead <= 1)", "if (ahead <= 2)")
+
+
 VARIANTS = {
     "nbg8": nbg(8),
     "nbg16": nbg(16),
@@ -473,6 +490,8 @@ VARIANTS = {
     "st_sc01": lambda s: s.replace(STORE, STORE.replace(", 0, 0);", ", 0, 17);")),
     "reswarm": reswarm,
     "base": lambda s: s,
+    "aprio": aprio,
+    "aprio2": aprio2,
     "noscale": noscale,
     "nofirstrefill": nofirstrefill,
     "nonpersist": lambda s: s.replace("dim3(MODE_ == 2 ? cus : std::min(nit, cus))", "dim3(MODE_ == 2 ? cus : (MODE_ == 0 ? nit : std::min(nit, cus)))"),
