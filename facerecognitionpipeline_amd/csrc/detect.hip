@@ -8,7 +8,7 @@
 //                      coefficients from the host; SSE2 vertical rounding for the
 //                      vectorised part of each row, scalar rounding for its tail)
 //   det_stem_kernel    blobFromImage ((x - 127.5) / 128, RGB) fused into conv3x3 s2
-//                      3->C + BN + ReLU (K = 27 is too small for MFMA)
+//                      3->C + BN + ReLU; det_stem_mfma_kernel the same on MFMA (K = 27 -> 28)
 //   maxpool3_kernel    MaxPool2d(3, 2, 1), NHWC
 //   upsample_add       FPN top-down: big += nearest-2x(small), NHWC
 //   decode_kernel      sigmoid(score) >= thresh -> distance2bbox / distance2kps at the
@@ -282,10 +282,105 @@ hipError_t launch_letterbox(const uint8_t* frames, int n, int H, int W, const in
   return hipGetLastError();
 }
 
+// The same stem on v_mfma_f32_16x16x4_f32 (as the embedding stem_kernel): K = 27 taps padded to
+// 28, the weights the A operand (16 channels x 4 taps per fragment, CB x 7 registers per lane),
+// 16 output pixels the B operand read from the normalised input rows staged in LDS; an f32 MFMA
+// chains its 4 products as fmaf, so with K in (ky, kx, ci) order every output is bitwise the
+// scalar kernel's.  One block per (frame, 2 output rows): 5 input rows loaded as whole-row dwords
+// and unpacked through a 256-entry table of (x - 127.5) / 128.
+typedef float dst_f4 __attribute__((ext_vector_type(4)));
+template <int CB>
+__global__ __launch_bounds__(256) void det_stem_mfma_kernel(const uint8_t* __restrict__ img, int H, int W,
+                                                            const float* __restrict__ w27xC,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, float* __restrict__ y) {
+  constexpr int C = 16 * CB, R = 2, NROW = 2 * R + 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_lut = smem;
+  float* s_in = smem + 256;  // [NROW][W + 2][3] + one zero cell
+  const int SW = W + 2, NIN = NROW * SW * 3;
+  const int Ho = H / 2, Wo = W / 2, RB = Ho / R;
+  const int f = blockIdx.x / RB, oy0 = (blockIdx.x - f * RB) * R;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  s_lut[tid] = ((float)tid - 127.5f) * 0.0078125f;
+  const int m = lane & 15, kk = lane >> 4;
+  float wa[CB][7];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int st = 0; st < 7; ++st) {
+      const int k = 4 * st + kk;
+      wa[cb][st] = k < 27 ? w27xC[k * C + 16 * cb + m] : 0.f;
+    }
+  const int RDW = W * 3 / 4;  // dwords per input row
+  const unsigned* src = reinterpret_cast<const unsigned*>(img + (size_t)f * H * W * 3);
+  for (int i = tid; i < NROW * 2 * 3 + 1; i += 256) {  // halo columns and the zero cell
+    const int r = i / 6, e = i - r * 6;
+    s_in[i < NROW * 6 ? (r * SW + (e < 3 ? 0 : SW - 1)) * 3 + e % 3 : NIN] = 0.f;
+  }
+  __syncthreads();  // s_lut
+  for (int i = tid; i < NROW * RDW; i += 256) {
+    const int r = i / RDW, q = 4 * (i - r * RDW);
+    const int iy = 2 * oy0 - 1 + r;
+    const bool in = (unsigned)iy < (unsigned)H;
+    const unsigned raw = in ? src[iy * RDW + (i - r * RDW)] : 0u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int xb = q + e, ix = xb / 3;
+      s_in[(r * SW + ix + 1) * 3 + (xb - ix * 3)] = in ? s_lut[(raw >> (8 * e)) & 255u] : 0.f;
+    }
+  }
+  __syncthreads();
+  int koff[7];
+#pragma unroll
+  for (int st = 0; st < 7; ++st) {
+    const int k = 4 * st + kk;
+    const int ky = k / 9, kx = (k / 3) % 3, c = k % 3;
+    koff[st] = k < 27 ? (ky * SW + kx) * 3 + c : -1;
+  }
+  const int rg = lane >> 4;
+  dst_f4 sc[CB], sh[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    sc[cb] = *reinterpret_cast<const dst_f4*>(scale + 16 * cb + 4 * rg);
+    sh[cb] = *reinterpret_cast<const dst_f4*>(shift + 16 * cb + 4 * rg);
+  }
+  const int GPR = Wo / 16;  // 16-pixel groups per output row
+  for (int grp = wv; grp < R * GPR; grp += 4) {
+    const int r = grp / GPR, ox = (grp - r * GPR) * 16 + m;
+    const int base = (2 * r * SW + 2 * ox) * 3;
+    float bv[7];
+#pragma unroll
+    for (int st = 0; st < 7; ++st) bv[st] = s_in[koff[st] < 0 ? NIN : base + koff[st]];
+    float* out = y + (((size_t)f * Ho + oy0 + r) * Wo + ox) * C;
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      dst_f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 7; ++st) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[cb][st], bv[st], acc, 0, 0, 0);
+      // lane (pixel m, row group rg) holds channels 16 cb + 4 rg .. + 3 of its pixel
+      dst_f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = fmaxf(__builtin_fmaf(acc[e], sc[cb][e], sh[cb][e]), 0.f);
+      *reinterpret_cast<dst_f4*>(out + 16 * cb + 4 * rg) = o;
+    }
+  }
+}
+
 hipError_t launch_det_stem(const uint8_t* img, int n, int H, int W, int C, const float* w27xC, const float* scale,
                            const float* shift, float* y, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (C % 8 != 0 || C > 32 || H % 2 || W % 2) return hipErrorInvalidValue;
+  if ((C == 16 || C == 32) && W % 32 == 0 && (H / 2) % 2 == 0) {
+    const size_t lds = (256 + 5 * (W + 2) * 3 + 1) * sizeof(float);
+    if (C == 32)
+      hipLaunchKernelGGL(det_stem_mfma_kernel<2>, dim3(n * (H / 4)), dim3(256), lds, s, img, H, W, w27xC, scale, shift,
+                         y);
+    else
+      hipLaunchKernelGGL(det_stem_mfma_kernel<1>, dim3(n * (H / 4)), dim3(256), lds, s, img, H, W, w27xC, scale, shift,
+                         y);
+    return hipGetLastError();
+  }
   const size_t lds = (27 * C + 3 * (W + 2) * 3) * sizeof(float);
   hipLaunchKernelGGL(det_stem_kernel, dim3(n * (H / 2)), dim3(256), lds, s, img, H, W, C, w27xC, scale, shift, y);
   return hipGetLastError();
