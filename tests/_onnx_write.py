@@ -119,8 +119,11 @@ class _G:
         return y
 
 
-def iresnet_onnx(sd, architecture: str, fused: bool = True, raw: bool = True) -> bytes:
-    """ModelProto bytes of the IResNet of state dict ``sd`` (arcface_torch keys)."""
+def iresnet_onnx(sd, architecture: str, fused: bool = True, raw: bool = True, fc: str = "gemm",
+                 features_folded: bool = False) -> bytes:
+    """ModelProto bytes of the IResNet of state dict ``sd`` (arcface_torch keys).  ``fc``: "gemm"
+    (Gemm, transB=1) or "matmul" (MatMul on the transposed weight + Add, another exporter form);
+    ``features_folded``: the BatchNorm1d after the FC folded into its weight and bias."""
     g = _G(sd, fused, raw)
     x = g.conv_bn("data", "conv1.weight", "bn1", 1)
     x = g.prelu(x, "prelu.weight")
@@ -141,10 +144,23 @@ def iresnet_onnx(sd, architecture: str, fused: bool = True, raw: bool = True) ->
     g.nodes.append(node("Flatten", [x], [f], "flatten", _attr_int("axis", 1)))
     d = g.t()
     g.nodes.append(node("Dropout", [f], [d], "dropout"))
+    fw = np.asarray(sd["fc.weight"], np.float64)
+    fb = np.asarray(sd["fc.bias"], np.float64)
+    if features_folded:
+        gm, bt, mu, var = (np.asarray(sd[f"features.{n}"], np.float64)
+                           for n in ("weight", "bias", "running_mean", "running_var"))
+        sc = gm / np.sqrt(var + EPS)
+        fw, fb = fw * sc[:, None], (fb - mu) * sc + bt
+    fw, fb = fw.astype(np.float32), fb.astype(np.float32)
     y = g.t()
-    g.nodes.append(node("Gemm", [d, g.init(sd["fc.weight"]), g.init(sd["fc.bias"])], [y], "fc",
-                        _attr_float("alpha", 1.0) + _attr_float("beta", 1.0) + _attr_int("transB", 1)))
-    out = g.bn(y, "features")
+    if fc == "gemm":
+        g.nodes.append(node("Gemm", [d, g.init(fw), g.init(fb)], [y], "fc",
+                            _attr_float("alpha", 1.0) + _attr_float("beta", 1.0) + _attr_int("transB", 1)))
+    else:
+        mm = g.t()
+        g.nodes.append(node("MatMul", [d, g.init(np.ascontiguousarray(fw.T))], [mm], "fc.matmul"))
+        g.nodes.append(node("Add", [mm, g.init(fb)], [y], "fc.add"))
+    out = y if features_folded else g.bn(y, "features")
     graph = (b"".join(g.nodes) + _str(2, "iresnet") + b"".join(_len(5, t) for t in g.inits) +
              _len(11, _value_info("data")) + _len(12, _value_info(out)))
     return _int(1, 8) + _len(8, _str(1, "") + _int(2, 13)) + _len(7, graph)

@@ -67,3 +67,19 @@ def test_wrong_architecture_or_graph_is_refused(sd50, tmp_path):
         arcface_state_dict_from_onnx(str(q), "ir_50")
     with pytest.raises(ValueError):
         W.load_arcface_state_dict(str(p))  # an .onnx file needs its architecture
+
+
+@pytest.mark.parametrize("fc,folded", [("matmul", False), ("gemm", True)])
+def test_other_head_forms(sd50, tmp_path, fc, folded):
+    """FC as MatMul + Add, and the features BatchNorm1d folded into the FC: the same network."""
+    from oracle import iresnet
+    p = tmp_path / "m.onnx"
+    p.write_bytes(iresnet_onnx(sd50, "ir_50", fused=True, fc=fc, features_folded=folded))
+    got = arcface_state_dict_from_onnx(str(p), "ir_50")
+    if not folded:
+        assert np.array_equal(got["fc.weight"], sd50["fc.weight"]) and np.array_equal(got["fc.bias"], sd50["fc.bias"])
+    torch.set_num_threads(min(8, torch.get_num_threads()))
+    crops = list(W.synthetic_crops(2))
+    want = iresnet.extract_embeddings_batch(iresnet.load_oracle("ir_50", sd50), crops)
+    have = iresnet.extract_embeddings_batch(iresnet.load_oracle("ir_50", got), crops)
+    assert np.abs(have - want).max() <= 1e-5
