@@ -170,3 +170,25 @@ def test_lanes_equal_separate_part_forwards(embedder):
             h.set_lanes(16, 5)
     finally:
         h.set_lanes(0)
+
+
+@pytest.mark.parametrize("arch", ["ir_50", "ir_101"])
+def test_serving_batch_sizes_vs_reference_golden(arch, golden_dir):
+    """Every serving-sized forward path against the REFERENCE's own embeddings
+    (tests/golden/embed_*.npz: 8 gallery + 8 probe crops run through the reference FaceEmbedder):
+    n = 1..40 crops cover the 4-row stem (n <= 8), the split-count rule of small F(4x4) grids,
+    the split-K direct convs with their parallel fixup (M <= 4096), the 98-way serving FC
+    (4 n <= max_batch) and the 32-way one, and the grouped head reduce.  Bar: 1e-5 per element."""
+    import os
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    g = np.load(os.path.join(golden_dir, f"embed_{arch}.npz"))
+    base = W.synthetic_crops(8, int(g["gallery_seed"]))
+    crops = np.concatenate([base, W.probe_crops(base, 8)])
+    want = np.concatenate([g["gallery_emb"], g["probe_emb"]])
+    emb = FaceEmbedder(architecture=arch, model_path="synthetic", max_batch=64, graph_batch=0)
+    dev = torch.from_numpy(crops).cuda()
+    for n in (1, 2, 3, 5, 8, 9, 16, 17, 40):
+        idx = np.arange(n) % 16
+        got = emb.embed_tensor(dev[torch.from_numpy(idx).cuda()]).cpu().numpy()
+        err = np.abs(got - want[idx]).max()
+        assert err <= 1e-5, (arch, n, err)
