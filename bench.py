@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--model-type", choices=["adaface", "arcface"], default="adaface",
                     help="embedding family (arcface = insightface IResNet weights, face_embedder.py:64-88)")
     ap.add_argument("--faces-per-frame", type=int, default=8, help="c4: faces per 1080p frame")
+    ap.add_argument("--c4-pipeline", choices=["on", "off"], default="on",
+                    help="c4: detect the next batch's frames on a second stream while this batch embeds + "
+                         "matches (on), or run every stage back to back (off)")
     ap.add_argument("--arch", default=None)
     ap.add_argument("--batch", type=int, default=256, help="crops per GPU per step")
     ap.add_argument("--gallery", type=int, default=None, help="gallery rows (0 = embed only)")
@@ -253,13 +256,25 @@ def main():
         from facerecognitionpipeline_amd.detector_arch import synthetic_detector_state_dict
         detector_sd = synthetic_detector_state_dict()
         detector = FaceDetector(device=dev, max_frames=min(32, frames.shape[0]), max_faces=64, state_dict=detector_sd)
+        # pipelined serving: batch i+1's detection runs on its own (non-blocking) stream while batch
+        # i's embed + match run on the main one.  Every step still detects exactly one batch of
+        # frames inside the timed region (the first batch's in warmup; the last step detects one
+        # batch that no timed step consumes, so the timed region holds K detections either way).
+        det_stream = torch.cuda.Stream(device=dev)
+        pending = []
+
+    def detect_batch():
+        if args.c4_pipeline == "on":
+            with torch.cuda.stream(det_stream):
+                return detector.model.detect(frames, detector.det_thresh, detector.max_faces)
+        return detector.model.detect(frames, detector.det_thresh, detector.max_faces)
 
     def step():
         if args.config == "c4":
             # SCRFD on every frame (batched); each frame's top faces_per_frame detections are aligned
             # (a frame with fewer is topped up with the synthetic placements so every step embeds
             # exactly `batch` faces); blur + gate on all crops; one embed+match
-            dets, counts = detector.model.detect(frames, detector.det_thresh, detector.max_faces)
+            dets, counts = pending.pop() if pending else detect_batch()
             o = 0
             for f in range(frames.shape[0]):
                 nf = min(args.faces_per_frame, args.batch - o)
@@ -270,10 +285,15 @@ def main():
                 det_stats["padded"] += nf - nd
                 emb.model.align_faces(frames[f], lm, 112, crops[o:o + nf])
                 o += nf
-            blur = emb.model.blur_scores(crops)
+            blur = emb.model.blur_scores(crops)  # syncs: the previous embed + match have finished
             if not (blur >= 0).all():
                 raise RuntimeError("bad blur scores")
             emb.model.embed_match(crops, k, idx, score, e_out)
+            if args.c4_pipeline == "on":
+                # fr_detect returns host detections (it syncs its own stream only); the embed + match
+                # just queued on the main stream run beside it.  The next step's align writes the
+                # crops on the main stream, so it is ordered after this embed.
+                pending.append(detect_batch())
         elif G > 0:
             emb.model.embed_match(rgb, k, idx, score, e_out)
         else:
@@ -412,6 +432,7 @@ def main():
                        "lanes": (1 if args.lanes_min == 0 else
                                  max(1, min(2, args.batch // (64 if args.lanes_min is None else args.lanes_min)))),
                        **({"frames_per_step": int(frames.shape[0]),
+                           "detect_overlaps_embed": args.c4_pipeline == "on",
                            "detector_gflop_per_frame": round(2 * detector_macs() / 1e9, 3),
                            "aligned_from_detections": det_stats["detected"],
                            "aligned_from_padding": det_stats["padded"]} if args.config == "c4" else {})},
