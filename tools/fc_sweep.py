@@ -18,7 +18,11 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--splits", default="49,98,196")
     ap.add_argument("--tiles", default="")
+    ap.add_argument("--so", default=None, help="a libfrhip.so build to load instead of the package's (A/B)")
     a = ap.parse_args()
+    if a.so:
+        from facerecognitionpipeline_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.so)
     B, dev = a.batch, torch.device("cuda", 0)
     x = torch.randn(B, 7, 7, 512, device=dev)
     w = torch.randn(512, 7, 7, 512, device=dev) / 25088 ** 0.5
