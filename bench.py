@@ -190,7 +190,9 @@ def c4_inputs(n_faces, per_frame, dev, seed=7):
     from facerecognitionpipeline_amd.face_recognition import reference_template
     rng = np.random.default_rng(seed)
     n_frames = (n_faces + per_frame - 1) // per_frame
-    frames = torch.randint(0, 256, (n_frames, 1080, 1920, 3), dtype=torch.uint8, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    frames = torch.randint(0, 256, (n_frames, 1080, 1920, 3), dtype=torch.uint8, device=dev, generator=gen)
     t = reference_template(112).astype(np.float64)
     lms = []
     for f in range(n_frames):
