@@ -238,3 +238,18 @@ def test_non_uint8_crops_only_at_input_size():
         as_uint8_crop(ok + 0.5)
     u8 = rng.integers(0, 256, (224, 200, 3), dtype=np.uint8)
     assert as_uint8_crop(u8) is u8  # uint8 of any size goes to the device resize unchanged
+
+
+def test_bench_c4_frames_are_seeded():
+    """bench.py's C4 frames and landmark placements are a function of the seed (the JSON line
+    says "seeded"): two calls agree, another seed differs."""
+    import torch
+
+    import bench
+    dev = torch.device("cpu")
+    f1, l1 = bench.c4_inputs(9, 8, dev)
+    f2, l2 = bench.c4_inputs(9, 8, dev)
+    f3, _ = bench.c4_inputs(9, 8, dev, seed=8)
+    assert f1.shape == (2, 1080, 1920, 3) and f1.dtype == torch.uint8
+    assert torch.equal(f1, f2) and all(np.array_equal(a, b) for a, b in zip(l1, l2))
+    assert not torch.equal(f1, f3)
