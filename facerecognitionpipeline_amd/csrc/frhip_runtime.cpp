@@ -397,8 +397,11 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // The detector's tile set (conv_det.hip) has no 64x128 instance.
   if (!h->detector && p.M <= 4096 && nsplit == 1) tile = TILE_64x128;
   // the head FC (split-K) of a serving batch (M = n <= 64 rows) or of <= 256 crops (tools/fc_sweep.py,
-  // 32 splits: --batch 128 43.0 us on 128x64/W8 vs 106 on 256x128/W8; --batch 256 69.3 vs 111.8)
-  if (!h->detector && nsplit > 1 && cw.kh == 7 && p.M <= 256) tile = p.M <= 64 ? TILE_64x128 : TILE_128x64_W8;
+  // 32 splits: --batch 128 43.0 us on 128x64/W8 vs 106 on 256x128/W8; --batch 256 69.3 vs 111.8).
+  // 129..256 rows on 64x128 (round 3, inside a one-lane IR-101 forward: 75.6 -> 63.9 us,
+  // tools/gpu_fc_ab.sh)
+  if (!h->detector && nsplit > 1 && cw.kh == 7 && p.M <= 256)
+    tile = (p.M <= 64 || p.M > 128) ? TILE_64x128 : TILE_128x64_W8;
   // serving batches: a stride-2 conv2 (+ fused shortcut) as a split-K launch of >= 4 K-steps per
   // split in one round of workgroups, then a parallel fixup, instead of stream-K, whose last
   // arriver per tile summed ~20 slabs of 32 KB alone (batch 1: 26-31 us per launch)
