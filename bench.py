@@ -4,9 +4,12 @@
 Workload at N=1 (BASELINE.json configs[2]): IR-101 AdaFace embed + cosine top-5
 match of a batch of 256 synthetic 112x112 crops per GPU against a 1k-row
 gallery.  One "step" = one ``fr_embed_match`` over the rank's batch, inputs
-already resident in HBM.  For N>1 (torchrun, one rank per GPU) rank 0 embeds
-the gallery and broadcasts it over RCCL (the path's only exchange step); each
-rank then processes its own probes independently (weak scaling).
+already resident in HBM.  For N>1 there is one rank per GPU: ``--gpus N`` starts
+the N rank processes itself (fresh children, before this process touches the
+GPU), or runs as one of them under ``torchrun`` (WORLD_SIZE set, which must
+equal N).  Rank 0 embeds the gallery and broadcasts it over RCCL (the path's
+only exchange step); each rank then processes its own probes independently
+(weak scaling: N x batch faces per step).
 
 Also reported:
   roofline      the dominant conv kernel (wino4_kernel for the stride-1 3x3 convs
@@ -43,7 +46,13 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU: started here as child processes unless torchrun already did")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
+    ap.add_argument("--same-gpu", action="store_true",
+                    help="testing: every rank on cuda:0 (needs --dist-backend gloo; RCCL refuses two ranks "
+                         "on one GPU)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c3",
@@ -207,19 +216,82 @@ def c4_inputs(n_faces, per_frame, dev, seed=7):
     return frames, lms
 
 
+def launch_ranks(args) -> int:
+    """``--gpus N`` without torchrun: start N fresh rank processes (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* in their environment, the same argv) and return the first non-zero exit code, else 0.
+
+    Runs before anything here touches the GPU: ``torch.cuda.device_count()`` counts devices without
+    initialising HIP on this image, and the children are started as new processes (never exec'd
+    from this one).  Rank 0's stdout is this process's stdout, so the one JSON line comes through.
+    """
+    import signal
+    import socket
+    import subprocess
+    n = args.gpus
+    visible = torch.cuda.device_count()
+    if args.same_gpu:
+        if args.dist_backend != "gloo":
+            sys.exit("bench.py: --same-gpu needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
+        if visible < 1:
+            sys.exit("bench.py: --same-gpu needs one visible GPU, found none")
+    elif n > visible:
+        sys.exit(f"bench.py: --gpus {n} but only {visible} GPU(s) are visible; refusing to run fewer ranks")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    # a dead rank leaves the others blocked in a collective: end them
+                    for q in pending:
+                        os.killpg(q.pid, signal.SIGTERM)
+            time.sleep(0.05)
+    except BaseException:
+        for q in procs:
+            if q.poll() is None:
+                os.killpg(q.pid, signal.SIGKILL)
+        raise
+    return rc
+
+
 def main():
     args = parse()
     arch0, gal0 = PRESETS[args.config]
     args.arch = args.arch or arch0
     args.gallery = gal0 if args.gallery is None else args.gallery
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.same_gpu and args.dist_backend != "gloo":
+        sys.exit("bench.py: --same-gpu needs --dist-backend gloo")
+    if args.same_gpu:
+        local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
     sd = W.synthetic_state_dict(args.arch, model_type=args.model_type)
@@ -314,7 +386,8 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item()
@@ -332,6 +405,11 @@ def main():
     # sanity: probes are noisy copies of gallery rows i % G
     top1_ok = (float((idx[:, 0].cpu().numpy() == np.arange(args.batch) % G0).mean())
                if G > 0 and args.config != "c4" else None)
+    if world > 1 and top1_ok is not None:
+        # the worst rank's self-match rate (every rank's probes are noisy copies of rows i % G0)
+        t1 = torch.tensor([top1_ok], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t1, op=dist.ReduceOp.MIN)
+        top1_ok = t1.item()
 
     if rank == 0:
         faces = world * args.batch * args.steps
@@ -428,7 +506,9 @@ def main():
                                     + f", batch {args.batch}/GPU, 112x112 uint8 RGB"),
                        "arch": args.arch, "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "gallery": G, "top_k": k, "parallelism": f"dp{world}",
-                       "gallery_exchange": "rccl broadcast" if world > 1 else "none",
+                       "gallery_exchange": (("rccl broadcast" if args.dist_backend == "nccl" else "gloo broadcast")
+                                            if world > 1 else "none"),
+                       **({"ranks_share_gpu": True} if args.same_gpu and world > 1 else {}),
                        # concurrent half-batch forwards per GPU (fr_set_lanes; library default 64 crops
                        # per lane, at most 2 lanes); the roofline pass always runs one lane
                        "lanes": (1 if args.lanes_min == 0 else

@@ -26,8 +26,9 @@ SOURCES = ["conv_winograd4.hip", "conv_winograd.hip","conv_f32_w4.hip", "conv_f3
            "embed_misc.hip", "align.hip", "gallery.hip", "detect.hip", "frhip_runtime.cpp", "detector.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
-# F(4x4): keep the transform's f32 math scalar -- packed f32 VALU beside MFMAs costs more issue
-# cycles than the two scalar ops it replaces (MI355X_MICROARCH.md, 'price of one filler')
+# F(4x4): the input / output transforms are packed f32 where the source says so (explicit f2
+# vectors: measured 2-5% faster than their scalar form); the SLP vectorizer is kept
+# from packing the rest (offset arithmetic, the MFMA waves' U-ring bookkeeping) behind our back
 EXTRA = {"conv_winograd4.hip": ["-fno-slp-vectorize"],
          # the stem's MFMA accumulators in VGPRs: no v_accvgpr_read per output before its epilogue
          "embed_misc.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}

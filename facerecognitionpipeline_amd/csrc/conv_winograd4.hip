@@ -142,17 +142,29 @@ __device__ __forceinline__ int lds_min4(const int* c) {
   return __builtin_amdgcn_readfirstlane(m);
 }
 
-// Wait until min(c[0..3]) >= need; returns the value seen.  The spin is bounded (2^16 polls,
-// a few ms): a lost hand-off cannot hang the GPU (the results would be wrong, and the tests
-// compare every output against the CPU references).
-__device__ __forceinline__ int lds_wait_min4(const int* c, int need) {
+// Wait until min(c[0..3]) >= need; returns the value seen.  The spin is bounded (poll_max
+// polls, 2^16 = a few ms by default): a lost hand-off cannot hang the GPU.  An expired wait
+// returns the value seen with W4_EXPIRED set: the caller's counter copy then exceeds every later
+// `need`, so the wave waits no more, carries on (every global access of the kernel is
+// range-checked: wrong data, never a fault) and reports the bit when it leaves the kernel
+// (w4_report_handoff).  Folding the flag into the counter copy keeps the hot loop free of a
+// store and of a register of its own (a separate flag cost the conv2 kernel 2 spilled VGPRs).
+constexpr int W4_EXPIRED = 1 << 30;
+__device__ __forceinline__ int lds_wait_min4(const int* c, int need, int poll_max) {
   int seen = lds_min4(c);
-  for (int it = 0; seen < need && it < (1 << 16); ++it) {
+  for (int it = 0; seen < need && it < poll_max; ++it) {
     __builtin_amdgcn_s_sleep(1);
     seen = lds_min4(c);
   }
   asm volatile("" ::: "memory");
-  return seen;
+  return seen < need ? (seen | W4_EXPIRED) : seen;
+}
+// FR_DEVERR_W4_HANDOFF into the launch's error word (host-pinned, read by the runtime at its sync
+// points, which then fail the call with FR_ERR_HIP): a vector store of a constant from every lane
+// (idempotent, no atomic needed), system scope so the host sees it once the launch has completed
+__device__ __forceinline__ void w4_report_handoff(int seen, int* err) {
+  if (__builtin_expect((seen & W4_EXPIRED) != 0, 0) && err)
+    __hip_atomic_store(err, FR_DEVERR_W4_HANDOFF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Publish `n` in this wave's counter once its earlier LDS operations have completed.
@@ -463,7 +475,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     // compiler's wait-count tracking wait for the freshly issued loads before the store.
     int fseen = 0;
     auto put = [&](Patch& P, int g) {
-      if (g - NBUF + 1 > fseen) fseen = lds_wait_min4(fre, g - NBUF + 1);
+      if (g - NBUF + 1 > fseen) fseen = lds_wait_min4(fre, g - NBUF + 1, p.poll_max);
       store(P, g);
       lds_publish(rdy + t, lane, g + 1);
     };
@@ -483,6 +495,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       put(pc, b + 2);
       if (b + 3 >= G) break;
     }
+    w4_report_handoff(fseen, p.err);
     return;
   }
 
@@ -512,7 +525,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   const float* vrd = ring + vslot(lane) * 4;
   // B fragments (V) of the next xi pair, carried across K-steps: step g + 1's first pair is read
   // during step g's last MFMAs, once the transform waves have published it
-  int rseen = lds_wait_min4(rdy, 1);  // step 0 is in the ring
+  int rseen = lds_wait_min4(rdy, 1, p.poll_max);  // step 0 is in the ring
   f4 a0n = *reinterpret_cast<const f4*>(vrd), a1n = *reinterpret_cast<const f4*>(vrd + 256);
   int g = 0;
   for (; SK ? g < G : j < nloc; ++j) {
@@ -540,7 +553,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         const f4 a0 = a0n, a1 = a1n;
         // the last pair reads step g + 1's first fragments: wait until it is published (the
         // counter seen last time usually already covers it: no poll)
-        if (x + 2 == NXI && g + 1 < G && rseen < g + 2) rseen = lds_wait_min4(rdy, g + 2);
+        if (x + 2 == NXI && g + 1 < G && rseen < g + 2) rseen = lds_wait_min4(rdy, g + 2, p.poll_max);
         const float* nb = x + 2 < NXI ? vb + (x + 2) * 256 : vn;
         a0n = *reinterpret_cast<const f4*>(nb);
         a1n = *reinterpret_cast<const f4*>(nb + 256);
@@ -713,6 +726,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       }
     }
   }
+  w4_report_handoff(rseen, p.err);
 }
 
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
@@ -862,6 +876,7 @@ bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
 
 hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
   Wino4Params p = p0;
+  if (p.poll_max <= 0) p.poll_max = WINO4_POLL_DEFAULT;
   if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
       (pre && !p.pre_t) || (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF ||
       (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) || (long long)NXI * p.Cout * p.Cin * 4 >= (1ll << 31))

@@ -8,7 +8,7 @@
 //                      -> optional e/(||e||+1e-8) (face_embedder.py:133-134, 177-180).
 //   l2norm_rows_kernel q/(||q||+1e-8) (gallery_manager.py:195).
 //   topk_kernel        argsort(S)[::-1][:k] (gallery_manager.py:197) with the
-//                      documented tie policy: score desc, then index asc.
+//                      documented tie policy: score desc, then gallery row desc.
 #include "frhip_kernels.h"
 
 #include <float.h>

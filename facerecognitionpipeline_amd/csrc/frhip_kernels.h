@@ -136,7 +136,16 @@ struct Wino4Params {
   int sk_mode;
   int no_split;  // 1: never split-K (tests compare the two schedules)
   int max_split;  // > 0: at most this many K parts per item in a split-K launch (serving sweeps)
+  // ring hand-off guard: a wave that has polled its LDS counters poll_max times without seeing
+  // the step it waits for stores FR_DEVERR_W4_HANDOFF into *err (a host-pinned word the
+  // runtime reads at its sync points; nullable) and carries on, so a lost hand-off ends the
+  // launch instead of hanging the GPU and is reported instead of passing as a result.
+  // poll_max <= 0 means the default (WINO4_POLL_DEFAULT).
+  int* err;
+  int poll_max;
 };
+constexpr int WINO4_POLL_DEFAULT = 1 << 16;
+constexpr int FR_DEVERR_W4_HANDOFF = 1;
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16
 size_t wino4_weight_floats(int Cout, int Cin);
 void wino4_canvas(Wino4Params& p);
@@ -160,7 +169,7 @@ hipError_t launch_l2norm_rows(const float* q, float* out, int n, int d, hipStrea
 // it, fused with the scores against the G x 512 gallery rows: scores [n][G]
 hipError_t launch_scores_small(const float* q, const float* gallery, int G, float* scores, int n, hipStream_t s);
 
-// Per row of a [n][G] score matrix: top-k by (score desc, index asc).
+// Per row of a [n][G] score matrix: top-k by (score desc, index desc), k in [1, G].
 hipError_t launch_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, hipStream_t s);
 
 // warpAffine INTER_LINEAR / BORDER_CONSTANT 0 of n crops from one uint8 RGB frame;

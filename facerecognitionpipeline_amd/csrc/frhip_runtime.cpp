@@ -74,6 +74,25 @@ int fail(fr_handle* h, int code, const std::string& msg) {
   return code;
 }
 
+int ensure_dev_err(fr_handle* h) {
+  if (h->dev_err) return FR_OK;
+  FR_HIP(h, hipHostMalloc((void**)&h->dev_err, sizeof(int), hipHostMallocCoherent | hipHostMallocMapped));
+  *(volatile int*)h->dev_err = 0;
+  return FR_OK;
+}
+
+int check_dev_err(fr_handle* h) {
+  if (!h->dev_err) return FR_OK;
+  const int v = *(volatile int*)h->dev_err;
+  if (!v) return FR_OK;
+  *(volatile int*)h->dev_err = 0;
+  return fail(h, FR_ERR_HIP,
+              (v & FR_DEVERR_W4_HANDOFF)
+                  ? "F(4x4) ring hand-off timed out in wino4_kernel: the results of the work queued on this handle "
+                    "before this call are invalid"
+                  : "device error word set (" + std::to_string(v) + ")");
+}
+
 
 
 void add_bn(std::map<std::string, size_t>& m, const std::string& p, int c, bool affine) {
@@ -269,6 +288,8 @@ struct ProfScope {
 static int g_wino4_streamk = 0;
 // cap on the F(4x4) split-K parts of small grids (frt_set_wino4_max_split: serving sweeps); 0 = none
 static int g_wino4_max_split = 0;
+// poll bound of wino4_kernel's ring hand-off waits (frt_set_wino4_poll_limit: tests force expiry)
+static int g_wino4_poll = WINO4_POLL_DEFAULT;
 
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
@@ -347,6 +368,8 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.part_floats = w4part ? fr_handle::W4PART_FLOATS : 0;
     wp.sk_mode = g_wino4_streamk;
     wp.max_split = g_wino4_max_split;
+    wp.err = h->dev_err;
+    wp.poll_max = g_wino4_poll;
     Wino4Params cv = wp;
     wino4_canvas(cv);
     // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
@@ -1221,6 +1244,7 @@ int fr_finalize(fr_handle* h) {
   }
   if (!missing.empty()) return fail(h, FR_ERR_MISSING_PARAM, "Missing key(s) in state_dict: " + missing);
   DeviceGuard dg(h->device);
+  if (int rc = ensure_dev_err(h)) return rc;
   clear_graphs(h);
   if (h->detector) {
     int rc = detector_finalize(h);
@@ -1382,6 +1406,7 @@ int fr_embed(fr_handle* h, const uint8_t* rgb, int n, int height, int width, flo
   if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
   if (int rc = check_crop_size(h, height, width)) return rc;
   if (n < 0 || (n > 0 && (!rgb || !out))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
+  if (int rc = check_dev_err(h)) return rc;  // reported by earlier asynchronous work
   DeviceGuard dg(h->device);
   return embed_any(h, rgb, n, height, width, out, normalize, (hipStream_t)stream);
 }
@@ -1423,7 +1448,7 @@ int fr_embed_host(fr_handle* h, const uint8_t* rgb, int n, int height, int width
                              hipMemcpyDeviceToHost, s));
   }
   FR_HIP(h, hipStreamSynchronize(s));
-  return FR_OK;
+  return check_dev_err(h);
 }
 
 int fr_gallery_set(fr_handle* h, const float* E, int G, int D, int src_is_device, void* stream) {
@@ -1555,6 +1580,7 @@ int fr_match_topk(fr_handle* h, const float* Q, int n, int k, int32_t* idx, floa
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
   if (n < 0 || (n > 0 && (!Q || !idx || !score))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
+  if (int rc = check_dev_err(h)) return rc;
   DeviceGuard dg(h->device);
   return match_device(h, Q, n, k, idx, score, (hipStream_t)stream);
 }
@@ -1580,7 +1606,7 @@ int fr_match_topk_host(fr_handle* h, const float* Q, int n, int k, int32_t* idx,
   FR_HIP(h, hipMemcpyAsync(idx, di, rb, hipMemcpyDeviceToHost, s));
   FR_HIP(h, hipMemcpyAsync(score, ds, rb, hipMemcpyDeviceToHost, s));
   FR_HIP(h, hipStreamSynchronize(s));
-  return FR_OK;
+  return check_dev_err(h);
 }
 
 int fr_embed_match(fr_handle* h, const uint8_t* rgb, int n, int k, int32_t* idx, float* score, float* emb_out,
@@ -1591,6 +1617,7 @@ int fr_embed_match(fr_handle* h, const uint8_t* rgb, int n, int k, int32_t* idx,
   if (!h->finalized) return fail(h, FR_ERR_STATE, "model not finalised (fr_finalize)");
   if (n < 0 || (n > 0 && (!rgb || !idx || !score))) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad n or NULL buffer");
   if (h->G <= 0) return fail(h, FR_ERR_STATE, "gallery is empty (fr_gallery_set first)");
+  if (int rc = check_dev_err(h)) return rc;  // reported by earlier asynchronous work
   DeviceGuard dg(h->device);
   hipStream_t s = (hipStream_t)stream;
   float* emb = emb_out;
@@ -1680,7 +1707,7 @@ int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* 
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("blur launch: ") + hipGetErrorString(e));
   FR_HIP(h, hipMemcpyAsync(scores, h->blur_out, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s));
   FR_HIP(h, hipStreamSynchronize(s));
-  return FR_OK;
+  return check_dev_err(h);
 }
 
 int fr_detect(fr_handle* h, const uint8_t* frames, int n, int height, int width, float det_thresh, int max_faces,
@@ -1694,7 +1721,9 @@ int fr_detect(fr_handle* h, const uint8_t* frames, int n, int height, int width,
     return fail(h, FR_ERR_INVALID_ARGUMENT, "bad frames / sizes / output buffers");
   if (n == 0) return FR_OK;
   DeviceGuard dg(h->device);
-  return detector_run(h, frames, n, height, width, det_thresh, max_faces, dets, counts, (hipStream_t)stream);
+  if (int rc = detector_run(h, frames, n, height, width, det_thresh, max_faces, dets, counts, (hipStream_t)stream))
+    return rc;
+  return check_dev_err(h);  // detector_run synchronised its stream
 }
 
 int fr_set_precision(fr_handle* h, int mode) {
@@ -1781,6 +1810,7 @@ int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* c
     h->pool.push_back(e.b);
   }
   h->events.clear();
+  if (int rc = check_dev_err(h)) return rc;  // every profiled launch has completed
   if (conv_ms) *conv_ms = h->last_ms[1] + h->last_ms[2];
   if (conv_flop) *conv_flop = h->last_flop[1] + h->last_flop[2];
   if (conv_launches) *conv_launches = h->last_n[1] + h->last_n[2];
@@ -1904,6 +1934,10 @@ int frt_set_wino4_max_split(int s) {
   g_wino4_max_split = s < 0 ? 0 : s;
   return FR_OK;
 }
+int frt_set_wino4_poll_limit(int n) {
+  g_wino4_poll = n < 0 ? WINO4_POLL_DEFAULT : n;
+  return FR_OK;
+}
 int frt_set_fuse_shortcut(fr_handle* h, int on) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -1938,6 +1972,9 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
   pre_t = u + wino4_weight_floats(cout, cin);
   hipError_t e = hipMemcpy(pre_t, t.data(), cin * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = launch_wino4_weights(w, pre_scale, u, cout, cin, s);
+  static int* frt_err = nullptr;  // this entry point's device error word (no handle to own one)
+  if (e == hipSuccess && !frt_err) e = hipHostMalloc((void**)&frt_err, sizeof(int), hipHostMallocCoherent | hipHostMallocMapped);
+  if (e == hipSuccess) *(volatile int*)frt_err = 0;
   if (e == hipSuccess) {
     Wino4Params p{};
     p.x = x;
@@ -1955,6 +1992,8 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.Cout = cout;
     p.sk_mode = g_wino4_streamk;
     p.no_split = !g_frt_wino4_split;
+    p.poll_max = g_wino4_poll;
+    p.err = frt_err;
     if (g_frt_wino4_split || g_wino4_streamk) {  // split-K / stream-K partial slots (64 KiB each)
       p.part_floats = 257ll * 2 * 16 * 16 * 64;
       if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;
@@ -1967,6 +2006,8 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
   (void)hipFree(part);
   if (e == hipSuccess) e = se;
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_winograd4: ") + hipGetErrorString(e));
+  if (*(volatile int*)frt_err & FR_DEVERR_W4_HANDOFF)
+    return fail(nullptr, FR_ERR_HIP, "frt_conv2d_winograd4: F(4x4) ring hand-off timed out in wino4_kernel");
   return FR_OK;
 }
 

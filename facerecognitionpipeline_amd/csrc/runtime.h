@@ -178,6 +178,11 @@ struct fr_handle {
   hipStream_t cap_stream = nullptr;
   std::vector<GraphEntry> graphs;
 
+  // device-side error word (host-pinned, coherent): kernels that detect a broken invariant
+  // store an FR_DEVERR_* code here (wino4_kernel: a ring hand-off that timed out); the runtime
+  // reads it at its sync points and at the entry of every compute call (check_dev_err)
+  int* dev_err = nullptr;
+
   // profiling
   bool prof = false;
   std::vector<frhip_rt::ProfEvent> events;
@@ -228,12 +233,18 @@ struct fr_handle {
     (void)hipFree(sk_cnt);
     (void)hipFree(align_m);
     (void)hipFree(blur_out);
+    if (dev_err) (void)hipHostFree(dev_err);
   }
 };
 
 namespace frhip_rt {
 
 int fail(fr_handle* h, int code, const std::string& msg);
+// The handle's device error word: allocated (zeroed) on first use; FR_OK or FR_ERR_HIP.
+int ensure_dev_err(fr_handle* h);
+// FR_ERR_HIP (and the word cleared) if a kernel of work that has completed by now reported a
+// broken invariant, else FR_OK.  Call after a stream sync to cover that call's own work.
+int check_dev_err(fr_handle* h);
 
 #define FR_HIP(h, call)                                                                          \
   do {                                                                                           \

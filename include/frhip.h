@@ -17,6 +17,12 @@
  *    on one handle must use the SAME stream: the handle's workspace (activations,
  *    stream-K slabs and tickets, staging buffers, captured graphs) is shared by
  *    all of its calls and only stream order keeps them apart.
+ *  - Device-side errors: a kernel that detects a broken invariant (wino4_kernel: an LDS ring
+ *    hand-off that timed out) records it in the handle's error word instead of hanging the GPU.
+ *    Calls that synchronise (fr_embed_host, fr_match_topk_host, fr_detect, fr_blur_scores,
+ *    fr_profile_read) then return FR_ERR_HIP for their own work; asynchronous calls (fr_embed,
+ *    fr_embed_match, fr_match_topk) return it at their next entry once the faulty work has
+ *    completed.  Results of the work queued before such an error are invalid.
  *  - One mutex per handle: a handle may be shared by threads (the reference
  *    server shares one FaceEmbedder/GalleryManager across Flask request
  *    threads, face_recognition_server.py:1102).
@@ -108,15 +114,18 @@ int fr_build_templates(fr_handle* h, const float* emb, const int32_t* offsets, i
                        float min_similarity, float* templates, int32_t* kept, void* stream);
 
 /* Batched GalleryManager.search (gallery_manager.py:189-205): q/(||q||+1e-8),
- * S = E.q (fp32), top-k by descending score (ties: lower gallery index first).
- * Q: device [n][512]; idx: device [n][k] int32 (gallery row, -1 if G<k... never
- * returned: k is clamped to G by the caller); score: device [n][k]. */
+ * S = E.q (fp32), top-k by descending score; equal scores by DESCENDING gallery row (a stable
+ * ascending argsort reversed, which is what the reference's np.argsort(S)[::-1] gives; DESIGN.md
+ * §3 "Tie policy").  k must be in [1, G] (G = fr_gallery_size), else FR_ERR_INVALID_ARGUMENT:
+ * the Python layer clamps top_k to G as search() does.
+ * Q: device [n][512]; idx: device [n][k] int32 gallery rows; score: device [n][k]. */
 int fr_match_topk(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float* score, void* stream);
 /* Host-buffer variant (synchronises). */
 int fr_match_topk_host(fr_handle* h, const float* Q, int n, int k, int32_t* idx, float* score);
 
 /* Fused unit of work of FaceMatcher.match_single_face (face_matcher.py:52-58),
- * batched: embed(normalize=1) then match.  emb_out may be NULL.  Device pointers. */
+ * batched: embed(normalize=1) then match (same k contract and tie policy as fr_match_topk).
+ * emb_out may be NULL.  Device pointers. */
 int fr_embed_match(fr_handle* h, const uint8_t* rgb, int n, int k, int32_t* idx, float* score, float* emb_out,
                    void* stream);
 
@@ -185,8 +194,9 @@ int fr_set_graph_batch(fr_handle* h, int max_n);
  * Embeddings are those of separate forwards of the parts (batch-invariant to ~1e-6).
  * min_n 0 = one lane.  fr_create's default: FR_LANES_MIN_DEFAULT crops per lane, at most
  * FR_LANES_MAX_DEFAULT lanes (measured on MI355X, IR-101 C3: batch 256 as 2 x 128 +6%, as 3 or 4
- * parts -1..-2%; batch 128 as 2 x 64 +8%; batch 64 as 2 x 32 -6%).  Lane 1's workspace (~1.2 GB
- * at max_batch 256) is allocated by the first forward that uses it; if that allocation fails the
+ * parts -1..-2%; batch 128 as 2 x 64 +8%; batch 64 as 2 x 32 -6%).  Lane 1's workspace (~1.7 GB
+ * at max_batch 256: 1.23 GB of activations for 128 crops, 0.27 GB of stream-K slabs, the
+ * shortcut, split-K and head-partial buffers) is allocated by the first forward that uses it; if that allocation fails the
  * forward runs as one lane and lanes stay off until the next fr_set_lanes. */
 #define FR_LANES_MIN_DEFAULT 64
 #define FR_LANES_MAX_DEFAULT 2
@@ -195,13 +205,13 @@ int fr_graph_count(fr_handle* h, int* count);
 
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).
  * enable=1 starts recording; fr_profile_read synchronises and returns, since the
- * last read: summed milliseconds and algorithmic FLOPs of the conv_mfma launches,
- * their launch count, and the summed milliseconds of all launches. */
+ * last read: summed milliseconds and algorithmic FLOPs of the conv launches (direct and
+ * Winograd), their launch count, and the summed milliseconds of all launches. */
 int fr_profile_enable(fr_handle* h, int enable);
 int fr_profile_read(fr_handle* h, double* conv_ms, double* conv_flop, int64_t* conv_launches, double* total_ms);
 /* Breakdown of the last fr_profile_read by kernel class: summed ms, algorithmic (direct-conv)
- * FLOPs, FLOPs the MFMA pipe executed (Winograd: 16 products per 2x2 tile instead of 36) and
- * launch count. */
+ * FLOPs, FLOPs the MFMA pipe executed (F(4x4,3x3), the default: 36 products per 4x4 canvas tile
+ * instead of the direct conv's 144; F(2x2,3x3): 16 per 2x2 tile instead of 36) and launch count. */
 #define FR_PROF_OTHER 0
 #define FR_PROF_CONV_DIRECT 1
 #define FR_PROF_CONV_WINOGRAD 2

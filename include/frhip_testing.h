@@ -46,6 +46,13 @@ int frt_set_wino4_streamk(int on);
 /* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
  * before the call keep their schedule). */
 int frt_set_wino4_max_split(int s);
+/* Poll bound of wino4_kernel's ring hand-off waits (default 65536; n < 0 restores it, 0 makes
+ * every wait that does not find its step ready at once expire).  An expired wait stores an error
+ * code into the launch's host-pinned error word: handle calls then fail with FR_ERR_HIP ("F(4x4)
+ * ring hand-off timed out") -- fr_embed_host / fr_match_topk_host / fr_detect / fr_profile_read
+ * after their sync, the asynchronous calls at their next entry -- and frt_conv2d_winograd4 after
+ * its sync.  Applies to launches issued after the call (captured graphs keep theirs). */
+int frt_set_wino4_poll_limit(int n);
 /* Handle h runs the stride-2 conv2 of a block with a conv shortcut and that shortcut as one
  * GEMM (on = 1, default: BN scales folded into the weights, extra K-steps over the block input)
  * or as two launches (0).  Drops captured graphs. */
@@ -62,7 +69,7 @@ int frt_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, c
 /* The host similarity fit of fr_align_faces: src/dst float [n][2] -> M double [2][3]. */
 int frt_fit_similarity(const float* src, const float* dst, int n, double* M);
 
-/* Row-wise top-k of a [n][G] score matrix (score desc, index asc). */
+/* Row-wise top-k of a [n][G] score matrix (score desc, equal scores by descending index; k in [1, G]). */
 int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, void* stream);
 
 /* Detector internals of fr_detect for n <= max_frames frames: letterbox + network only.

@@ -24,6 +24,8 @@ def lib():
         L.frt_set_wino4_streamk.argtypes = [_I]
         L.frt_set_wino4_max_split.restype = _I
         L.frt_set_wino4_max_split.argtypes = [_I]
+        L.frt_set_wino4_poll_limit.restype = _I
+        L.frt_set_wino4_poll_limit.argtypes = [_I]
         L.frt_set_fuse_shortcut.restype = _I
         L.frt_set_fuse_shortcut.argtypes = [_P, _I]
         L.frt_stem.restype = _I
