@@ -52,6 +52,7 @@ _SIGNATURES = {
     "fr_set_graph_batch": (_I, [_P, _I]),
     "fr_set_lanes": (_I, [_P, _I, _I]),
     "fr_graph_count": (_I, [_P, ctypes.POINTER(ctypes.c_int)]),
+    "fr_get_lanes": (_I, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "fr_profile_enable": (_I, [_P, _I]),
     "fr_profile_kernel": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
@@ -275,6 +276,13 @@ class Handle:
     def set_lanes(self, min_n: int, max_lanes: int = 2) -> None:
         """Run a forward of n crops as min(max_lanes, n // min_n) concurrent parts (0: one lane)."""
         check(self._lib.fr_set_lanes(self.h, int(min_n), int(max_lanes)), self.h)
+
+    def get_lanes(self) -> dict:
+        """The lane setting in force; ``fell_back`` is True when a failed workspace allocation
+        turned lanes off (until the next ``set_lanes``)."""
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self._lib.fr_get_lanes(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self.h)
+        return {"min_n": a.value, "max_lanes": b.value, "fell_back": bool(c.value)}
 
     def graph_count(self) -> int:
         c = ctypes.c_int()

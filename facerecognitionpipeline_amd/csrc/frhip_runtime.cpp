@@ -468,10 +468,12 @@ LaneWs lane0_ws(fr_handle* h) {
   return L;
 }
 
-// Frees lane l's (>= 1) activation workspace (after a failed ensure_lane)
+// Frees lane l's (>= 1) activation workspace (after a failed ensure_lane).  Only work queued on
+// the lane's own stream can still read it (earlier calls joined that stream back into theirs),
+// so a sync of that stream -- not of the device, which would stall other handles -- suffices.
 void release_lane(fr_handle* h, int l) {
   LaneWs& L = h->lane_ws[l];
-  (void)hipDeviceSynchronize();
+  if (h->lane_stream[l]) (void)hipStreamSynchronize(h->lane_stream[l]);
   for (auto& a : L.act) {
     if (a) (void)hipFree(a);
     a = nullptr;
@@ -602,7 +604,9 @@ int forward_chunk(fr_handle* h, const uint8_t* rgb, int n, float* out, int norma
       // (what worked before lanes existed) instead of failing the call; fr_set_lanes re-enables
       (void)hipGetLastError();  // clear the failed allocation's sticky error
       release_lane(h, l);
-      h->lane_min = 0;
+      h->lane_min = 0;  // visible through fr_get_lanes
+      h->lanes_fallback = true;
+      h->err.clear();  // the call succeeds: no stale allocation message for the next failure
       const int off0 = 0;
       return forward_lanes(h, rgb, &off0, &n, 1, out, normalize, &s, &L0);
     }
@@ -702,7 +706,9 @@ int resize_device(fr_handle* h, const uint8_t* src, int n, int H, int W, uint8_t
     if (h->rs_tabs.size() >= fr_handle::RS_TABS_MAX) {
       t = &*std::min_element(h->rs_tabs.begin(), h->rs_tabs.end(),
                              [](const fr_handle::ResizeTab& a, const fr_handle::ResizeTab& b) { return a.used < b.used; });
-      // the replaced table may still be read by a resize queued on s: copy in stream order
+      // the replaced table may still be read by a resize queued earlier, on s or on another
+      // stream: the copy waits for that launch (its event), then goes in stream order on s
+      if (t->last) FR_HIP(h, hipStreamWaitEvent(s, t->last, 0));
       FR_HIP(h, hipMemcpyAsync(t->tab, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice, s));
       FR_HIP(h, hipStreamSynchronize(s));  // the pageable host table must outlive the copy
       t->H = H;
@@ -712,7 +718,7 @@ int resize_device(fr_handle* h, const uint8_t* src, int n, int H, int W, uint8_t
       int* d = nullptr;
       FR_HIP(h, hipMalloc((void**)&d, host.size() * sizeof(int)));
       FR_HIP(h, hipMemcpy(d, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice));
-      h->rs_tabs.push_back({H, W, resize_simd_end(112 * 3), d, 0});
+      h->rs_tabs.push_back({H, W, resize_simd_end(112 * 3), d, 0, nullptr});
       t = &h->rs_tabs.back();
     }
   }
@@ -720,6 +726,9 @@ int resize_device(fr_handle* h, const uint8_t* src, int n, int H, int W, uint8_t
   ProfScope ps(h, s, 0.0, 0);
   hipError_t e = launch_letterbox(src, n, H, W, t->tab, t->tab + 4 * 112, 112, 112, t->simd_end, 112, 112, dst, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("resize launch: ") + hipGetErrorString(e));
+  // (never inside a graph capture: captured forwards start at in_stage, after the resize)
+  if (!t->last) FR_HIP(h, hipEventCreateWithFlags(&t->last, hipEventDisableTiming));
+  FR_HIP(h, hipEventRecord(t->last, s));
   return FR_OK;
 }
 
@@ -1770,6 +1779,16 @@ int fr_set_lanes(fr_handle* h, int min_n, int max_lanes) {
   if (max_lanes < 1 || max_lanes > MAX_LANES) return fail(h, FR_ERR_INVALID_ARGUMENT, "max_lanes must be in [1, 4]");
   h->lane_min = min_n;
   h->lane_max = max_lanes;
+  h->lanes_fallback = false;
+  return FR_OK;
+}
+
+int fr_get_lanes(fr_handle* h, int* min_n, int* max_lanes, int* fell_back) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (min_n) *min_n = h->lane_min;
+  if (max_lanes) *max_lanes = h->lane_max;
+  if (fell_back) *fell_back = h->lanes_fallback ? 1 : 0;
   return FR_OK;
 }
 

@@ -109,6 +109,7 @@ struct fr_handle {
     int H, W, simd_end;
     int* tab;
     unsigned long long used;  // last use (LRU clock)
+    hipEvent_t last;          // recorded after the table's last resize launch (on that call's stream)
   };
   static constexpr size_t RS_TABS_MAX = 16;  // coefficient tables kept per handle (LRU)
   std::vector<ResizeTab> rs_tabs;
@@ -158,6 +159,7 @@ struct fr_handle {
   // parts, lane 0 on the caller's stream with the workspace above, lane l >= 1 on lane_stream[l]
   // with lane_ws[l]
   int lane_min = 0, lane_max = 1;
+  bool lanes_fallback = false;  // lanes were turned off by a failed lane-workspace allocation
   frhip_rt::LaneWs lane_ws[frhip_rt::MAX_LANES];
   int lane_batch[frhip_rt::MAX_LANES] = {0, 0, 0, 0};  // crops lane l's buffers hold
   hipStream_t lane_stream[frhip_rt::MAX_LANES] = {nullptr, nullptr, nullptr, nullptr};
@@ -220,7 +222,10 @@ struct fr_handle {
     (void)hipFree(partial);
     (void)hipFree(in_stage);
     (void)hipFree(emb_stage);
-    for (auto& t : rs_tabs) (void)hipFree(t.tab);
+    for (auto& t : rs_tabs) {
+      (void)hipFree(t.tab);
+      if (t.last) (void)hipEventDestroy(t.last);
+    }
     (void)hipFree(rs_stage);
     (void)hipFree(rs_src);
     (void)hipFree(gallery);

@@ -168,6 +168,7 @@ class GalleryManager:
         # are atomic with respect to each other (the reference server shares one GalleryManager
         # across Flask request threads, face_recognition_server.py:1102)
         self._lock = threading.RLock()
+        self._save_lock = threading.Lock()  # one save() at a time: snapshot + both files, in order
         os.makedirs(os.path.dirname(gallery_path) or ".", exist_ok=True)
         if os.path.exists(self._arrays_path(gallery_path)):
             self.load()
@@ -387,20 +388,30 @@ class GalleryManager:
 
     def save(self, path: Optional[str] = None) -> None:
         path = path or self.gallery_path
-        # snapshot under the lock (a concurrent add/delete cannot tear the JSON / npz pair), write outside
-        with self._lock:
-            ids = list(self.students.keys())
-            arrays = {}
-            for i, s in enumerate(ids):
-                arrays[f"e{i}"] = np.array(self.students[s].embeddings)
-                arrays[f"t{i}"] = np.array(self.students[s].template_embedding)
-            meta = {"num_students": len(ids), "last_saved": datetime.now().isoformat(), "order": ids,
-                    "students": {s: {"student_id": r.student_id, "name": r.name, "num_samples": r.num_samples,
-                                     "enrollment_date": r.enrollment_date, "last_updated": r.last_updated,
-                                     "metadata": copy.deepcopy(r.metadata)} for s, r in self.students.items()}}
-        np.savez(self._arrays_path(path), **arrays)
-        with open(os.path.splitext(path)[0] + ".json", "w") as f:
-            json.dump(meta, f, indent=2)
+        # _save_lock orders whole saves (the later snapshot lands last, and no save interleaves its
+        # .npz with another's .json); the snapshot itself is taken under the gallery lock, so
+        # enrollment is blocked only while it is copied, not while the files are written
+        with self._save_lock:
+            with self._lock:
+                ids = list(self.students.keys())
+                arrays = {}
+                for i, s in enumerate(ids):
+                    arrays[f"e{i}"] = np.array(self.students[s].embeddings)
+                    arrays[f"t{i}"] = np.array(self.students[s].template_embedding)
+                meta = {"num_students": len(ids), "last_saved": datetime.now().isoformat(), "order": ids,
+                        "students": {s: {"student_id": r.student_id, "name": r.name, "num_samples": r.num_samples,
+                                         "enrollment_date": r.enrollment_date, "last_updated": r.last_updated,
+                                         "metadata": copy.deepcopy(r.metadata)} for s, r in self.students.items()}}
+            # both files written to temporaries first and then renamed, so a reader never sees a
+            # half-written file (a crash between the two renames can still pair a new .npz with the
+            # previous .json; load() then fails on the missing e{i}/t{i} or ids)
+            npz, js = self._arrays_path(path), os.path.splitext(path)[0] + ".json"
+            with open(npz + ".tmp", "wb") as f:
+                np.savez(f, **arrays)
+            with open(js + ".tmp", "w") as f:
+                json.dump(meta, f, indent=2)
+            os.replace(npz + ".tmp", npz)
+            os.replace(js + ".tmp", js)
 
     def load(self, path: Optional[str] = None) -> None:
         with self._lock:

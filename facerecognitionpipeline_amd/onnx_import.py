@@ -204,6 +204,10 @@ class _Walker:
     def __init__(self, nodes, inits):
         self.inits = inits
         self.consumers: Dict[str, List[Node]] = {}
+        # Identity / Cast nodes by output: some exporters feed (shared or deduplicated) weights
+        # through them instead of naming the initializer directly (init() follows the chain)
+        self.producer: Dict[str, Node] = {n.outputs[0]: n for n in nodes
+                                          if n.op in ("Identity", "Cast") and n.inputs and n.outputs}
         for n in nodes:
             if n.op == "Constant":
                 continue
@@ -225,8 +229,15 @@ class _Walker:
         if k >= len(node.inputs) or not node.inputs[k]:
             return None
         name = node.inputs[k]
+        hops = 0
+        while name not in self.inits and name in self.producer and hops < 64:
+            p = self.producer[name]
+            if p.op == "Cast" and p.attrs.get("to", 1) != 1:  # TensorProto.FLOAT
+                raise NotImplementedError(f"ONNX IResNet: {node} input {name!r} is a Cast to type {p.attrs.get('to')}")
+            name, hops = p.inputs[0], hops + 1
         if name not in self.inits:
-            raise NotImplementedError(f"ONNX IResNet: {node} input {name!r} is not an initializer")
+            raise NotImplementedError(f"ONNX IResNet: {node} input {node.inputs[k]!r} is not an initializer "
+                                      "(nor an Identity / Cast chain from one)")
         return np.asarray(self.inits[name], dtype=np.float32)
 
     def expect(self, node: Node, op: str) -> Node:

@@ -201,6 +201,9 @@ int fr_set_graph_batch(fr_handle* h, int max_n);
 #define FR_LANES_MIN_DEFAULT 64
 #define FR_LANES_MAX_DEFAULT 2
 int fr_set_lanes(fr_handle* h, int min_n, int max_lanes);
+/* The lane setting in force: min_n is 0 after a failed lane-workspace allocation turned lanes off,
+ * and fell_back is then 1 (until the next fr_set_lanes).  Any output pointer may be NULL. */
+int fr_get_lanes(fr_handle* h, int* min_n, int* max_lanes, int* fell_back);
 int fr_graph_count(fr_handle* h, int* count);
 
 /* Per-kernel-class timing with HIP events on the call stream (bench roofline).

@@ -76,8 +76,8 @@ def _value_info(name: str) -> bytes:
 
 
 class _G:
-    def __init__(self, sd, fused: bool, raw: bool):
-        self.sd, self.fused, self.raw = sd, fused, raw
+    def __init__(self, sd, fused: bool, raw: bool, wrap: str = ""):
+        self.sd, self.fused, self.raw, self.wrap = sd, fused, raw, wrap
         self.nodes, self.inits, self.k = [], [], 0
 
     def t(self) -> str:
@@ -87,7 +87,18 @@ class _G:
     def init(self, a) -> str:
         nm = f"w{len(self.inits)}"
         self.inits.append(tensor(nm, a, self.raw))
-        return nm
+        if not self.wrap:
+            return nm
+        # weights fed through Identity / Cast(to=FLOAT) nodes, as some torch.onnx exports do for
+        # shared or deduplicated parameters: "identity" wraps every one once; "mixed" rotates
+        # Identity, Cast and a two-Identity chain
+        forms = (("Identity",),) if self.wrap == "identity" else (("Identity",), ("Cast",), ("Identity", "Identity"))
+        cur = nm
+        for j, op in enumerate(forms[(len(self.inits) - 1) % len(forms)]):
+            out = f"{nm}_{op.lower()}{j}"
+            self.nodes.append(node(op, [cur], [out], out, _attr_int("to", 1) if op == "Cast" else b""))
+            cur = out
+        return cur
 
     def bn(self, x: str, key: str) -> str:
         y = self.t()
@@ -120,11 +131,12 @@ class _G:
 
 
 def iresnet_onnx(sd, architecture: str, fused: bool = True, raw: bool = True, fc: str = "gemm",
-                 features_folded: bool = False) -> bytes:
+                 features_folded: bool = False, wrap: str = "") -> bytes:
     """ModelProto bytes of the IResNet of state dict ``sd`` (arcface_torch keys).  ``fc``: "gemm"
     (Gemm, transB=1) or "matmul" (MatMul on the transposed weight + Add, another exporter form);
-    ``features_folded``: the BatchNorm1d after the FC folded into its weight and bias."""
-    g = _G(sd, fused, raw)
+    ``features_folded``: the BatchNorm1d after the FC folded into its weight and bias; ``wrap``:
+    "identity" / "mixed" feed the weights through Identity / Cast nodes (_G.init)."""
+    g = _G(sd, fused, raw, wrap)
     x = g.conv_bn("data", "conv1.weight", "bn1", 1)
     x = g.prelu(x, "prelu.weight")
     for s, (units, _depth) in enumerate(zip(ARCHITECTURES[architecture], STAGE_WIDTHS)):

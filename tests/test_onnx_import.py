@@ -83,3 +83,22 @@ def test_other_head_forms(sd50, tmp_path, fc, folded):
     want = iresnet.extract_embeddings_batch(iresnet.load_oracle("ir_50", sd50), crops)
     have = iresnet.extract_embeddings_batch(iresnet.load_oracle("ir_50", got), crops)
     assert np.abs(have - want).max() <= 1e-5
+
+
+@pytest.mark.parametrize("wrap", ["identity", "mixed"])
+def test_weights_behind_identity_or_cast_nodes(sd50, tmp_path, wrap):
+    """Weights fed through Identity / Cast(to=FLOAT) chains (shared-parameter exports) import like
+    directly named initializers; a Cast to another type is refused."""
+    p = tmp_path / "m.onnx"
+    p.write_bytes(iresnet_onnx(sd50, "ir_50", fused=False, wrap=wrap))
+    got = arcface_state_dict_from_onnx(str(p), "ir_50")
+    want = {k: v for k, v in sd50.items() if not k.endswith("num_batches_tracked")}
+    assert set(got) == set(want)
+    for k, v in want.items():
+        assert np.array_equal(got[k].reshape(v.shape), v), k
+    if wrap == "mixed":
+        # the Casts' attribute to=1 (FLOAT) -> 10 (FLOAT16): same length, the message stays valid
+        q = tmp_path / "half.onnx"
+        q.write_bytes(p.read_bytes().replace(b"\x0a\x02to\x18\x01", b"\x0a\x02to\x18\x0a"))
+        with pytest.raises(NotImplementedError, match="Cast to type 10"):
+            arcface_state_dict_from_onnx(str(q), "ir_50")
