@@ -58,6 +58,7 @@
 // accumulator of lane (tile l&15, row group l>>4) holds 4 consecutive couts of one tile.
 //   U: [36 xi][Cout/16][Cin/16][64 lane = 16 k + cout][4]
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 
 #include "frhip_kernels.h"
@@ -229,6 +230,17 @@ __device__ __forceinline__ void at6v(const f2 (&m)[6], f2 (&o)[4]) {
   const f2 c2 = {2.f, 2.f}, c4 = {4.f, 4.f}, c8 = {8.f, 8.f};
   const f2 p12 = m[1] + m[2], m12 = m[1] - m[2];
   const f2 p34 = m[3] + m[4], m34 = m[3] - m[4];
+  o[0] = m[0] + p12 + p34;
+  o[1] = __builtin_elementwise_fma(c2, m34, m12);
+  o[2] = __builtin_elementwise_fma(c4, p34, p12);
+  o[3] = __builtin_elementwise_fma(c8, m34, m12 + m[5]);
+}
+
+// the same on four couts (two packed f32 halves; per element the operations of at6 / at6v)
+__device__ __forceinline__ void at6q(const f4 (&m)[6], f4 (&o)[4]) {
+  const f4 c2 = {2.f, 2.f, 2.f, 2.f}, c4 = {4.f, 4.f, 4.f, 4.f}, c8 = {8.f, 8.f, 8.f, 8.f};
+  const f4 p12 = m[1] + m[2], m12 = m[1] - m[2];
+  const f4 p34 = m[3] + m[4], m34 = m[3] - m[4];
   o[0] = m[0] + p12 + p34;
   o[1] = __builtin_elementwise_fma(c2, m34, m12);
   o[2] = __builtin_elementwise_fma(c4, p34, p12);
@@ -528,6 +540,47 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   int rseen = lds_wait_min4(rdy, 1, p.poll_max);  // step 0 is in the ring
   f4 a0n = *reinterpret_cast<const f4*>(vrd), a1n = *reinterpret_cast<const f4*>(vrd + 256);
   int g = 0;
+  // Whole-item launches (MODE 0) split each item's epilogue in two.  Part A, at the end of item
+  // j: the output transform, the BN parameters and the residual loads.  Part B, one output pixel
+  // per xi pair of item j + 1's FIRST K-step (pixel i at pair i + 2): BN, PReLU, residual add and
+  // the 16-byte store.  So the residual loads' latency and the stores' write-back overlap MFMAs,
+  // and the next item's U refills no longer queue behind a burst of 16 stores (vmcnt counts loads
+  // and stores in issue order).  The pending pixel state (outputs, residual, offsets) replaces
+  // accumulators that are not live yet at the start of a K-step, so it costs no registers at the
+  // peak.  Before the first item nothing is pending (offsets past the range: stores dropped);
+  // the last item's part B runs after the loop.
+  constexpr bool DEFER = !SPLIT && !SK;
+  constexpr bool DRES = DEFER && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
+  const __amdgpu_buffer_rsrc_t yr_d = uniform_rsrc(p.y, p.B * H * W * Cout * 4);
+  f4 pv[16], pres[16], psc = {1.f, 1.f, 1.f, 1.f}, psh = {0.f, 0.f, 0.f, 0.f}, pal = psh, pcl = psh;
+  int po[16];
+  if constexpr (DEFER) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      pv[i] = pres[i] = f4{0.f, 0.f, 0.f, 0.f};
+      po[i] = BIGOFF;
+    }
+  }
+  // PReLU t > 0 ? t : a t as med3(t, a t, c): c = +inf for a slope a <= 1 (= max(t, a t)),
+  // -inf for a > 1 (= min(t, a t)); med3 returns one of its operands, so the value is the
+  // reference's exactly (up to the sign of a zero), in a packed multiply and a med3 per value
+  // instead of a multiply, a compare and a select
+  auto prelu_q = [](f4 v, f4 al, f4 cl) {
+    const f4 av = v * al;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = __builtin_amdgcn_fmed3f(v[r], av[r], cl[r]);
+    return v;
+  };
+  auto finish = [&](int i) {  // part B of pending pixel i
+    f4 v = __builtin_elementwise_fma(pv[i], psc, psh);
+    if constexpr (EPI == EPI_AFFINE_PRELU) v = prelu_q(v, pal, pcl);
+    if constexpr (DRES) {
+      v += pres[i];
+      if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = prelu_q(v, pal, pcl);
+    }
+    const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);
+  };
   for (; SK ? g < G : j < nloc; ++j) {
     const Item it = item_at(j);
     const int s0 = s_beg, s1 = SK ? min(KST, s0 + (G - g)) : KS;
@@ -537,7 +590,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     f4 acc[NXI];
 #pragma unroll
     for (int x = 0; x < NXI; ++x) acc[x] = f4{0.f, 0.f, 0.f, 0.f};
-    auto kstep = [&](int s) {
+    auto kstep = [&](int s, auto first_step) {
       // ring slot g % NBUF holds step g (published before this wave read its first pair)
       const float* vb = vrd + (g % NBUF) * VSTEP;
       const float* vn = vrd + ((g + 1) % NBUF) * VSTEP;
@@ -576,6 +629,10 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
         __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        // the previous item's pending output pixel x / 2 - 2 (after this pair's refills, so the
+        // refills of earlier pairs never wait for its store)
+        if constexpr (DEFER && decltype(first_step)::value)
+          if (x >= 4) finish(x / 2 - 2);
         __builtin_amdgcn_sched_barrier(0);
       }
       ++g;
@@ -586,8 +643,8 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     // in straight-line code, so the wait for its U fragments counts exactly the epilogue's
     // stores in between (a merged loop header made the compiler wait for every outstanding
     // load and store, vmcnt(0), at every K-step)
-    kstep(s0);
-    for (int s = s0 + 1; s < s1; ++s) kstep(s);
+    kstep(s0, std::true_type{});
+    for (int s = s0 + 1; s < s1; ++s) kstep(s, std::false_type{});
     ub = ub_next;
     ul = ulast(j + 1);
     s_beg = 0;
@@ -621,6 +678,40 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       for (int y = 0; y < 4; ++y)
 #pragma unroll
         for (int x = 0; x < 4; ++x) oo[y][x] = (int)((unsigned)ro[y] + (unsigned)co[x]);
+    }
+    if constexpr (DEFER) {
+      // part A: rows of A^T M A on all 4 couts (each frees 8 accumulator registers), the residual
+      // of output rows 0-1 in flight during the column pass, then rows 2-3
+      f4 z[6][4];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const f4 m6[6] = {acc[6 * a], acc[6 * a + 1], acc[6 * a + 2], acc[6 * a + 3], acc[6 * a + 4], acc[6 * a + 5]};
+        at6q(m6, z[a]);
+      }
+      if constexpr (DRES)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pres[i] = ld4(rr, oo[i >> 2][i & 3]);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const f4 c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
+        f4 o[4];
+        at6q(c6, o);
+#pragma unroll
+        for (int y = 0; y < 4; ++y) pv[4 * y + x] = o[y];
+      }
+      if constexpr (DRES)
+#pragma unroll
+        for (int i = 8; i < 16; ++i) pres[i] = ld4(rr, oo[i >> 2][i & 3]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) po[i] = oo[i >> 2][i & 3];
+      psc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
+      psh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
+      if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) {
+        pal = *reinterpret_cast<const f4*>(p.prelu + cout0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pcl[r] = pal[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
+      }
+      continue;
     }
     // residual rows 0-1 in flight during the output transform of couts 2-3, rows 2-3 while rows
     // 0-1 are stored (issued earlier they would spill beside the 144 accumulators)
@@ -726,6 +817,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       }
     }
   }
+  if constexpr (DEFER)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) finish(i);  // the last item's part B
   w4_report_handoff(rseen, p.err);
 }
 

@@ -13,9 +13,11 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
   python3 bench.py $BARGS > $OUT/trace_bench.log 2>&1 || { echo "trace pass failed rc=$?"; tail -20 $OUT/trace_bench.log; exit 3; }
 echo trace ok; tail -1 $OUT/trace_bench.log
 if [ "${PMC:-1}" = "1" ]; then
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$C -o run -- \
-    python3 bench.py $PARGS > $OUT/pmc_$C.log 2>&1 || { echo "pmc $C failed rc=$?"; tail -20 $OUT/pmc_$C.log; exit 3; }
+# one pass per counter set: FETCH_SIZE (3 TCC), WRITE_SIZE (2 TCC), MFMA busy + GPU clock (1 SQ + 1 GRBM)
+for C in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  D=$(echo $C | cut -d' ' -f1)
+  timeout -k 10 -s KILL 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$D -o run -- \
+    python3 bench.py $PARGS > $OUT/pmc_$D.log 2>&1 || { echo "pmc $C failed rc=$?"; tail -20 $OUT/pmc_$D.log; exit 3; }
   echo pmc $C ok
 done
 fi

@@ -116,6 +116,9 @@ def main():
     hdr = f"{'layer':38s} {'n/fwd':>5s} {'avg us':>9s} {'TF/s':>7s} {'%peak':>6s} {'%time':>6s} {'alg MB':>8s}"
     if pmc:
         hdr += f" {'HBM MB':>8s} {'HBM/alg':>7s}"
+    mf = "SQ_VALU_MFMA_BUSY_CYCLES" in pmc and "GRBM_GUI_ACTIVE" in pmc
+    if mf:
+        hdr += f" {'MHz':>6s} {'cyc/MFMA':>8s} {'MFMAbusy':>8s} {'fracTF':>6s}"
     print(hdr)
     counts = collections.Counter(n for n, _f, _b in L)
     total_time = sum(counts[n] * sum(v) / len(v) for n, v in per.items()) if per else 1.0
@@ -171,6 +174,26 @@ def main():
                     conv_alg += alg * cnt
                     conv_hbm += hbm * cnt
                     conv_n += cnt
+            # MFMA pipe: SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over the chip's 1,024 SIMDs) over
+            # the dispatch's cycles per XCD (GRBM_GUI_ACTIVE / 8, rocprofv3 sums the 8 XCDs) x 1,024.
+            # cyc/MFMA = busy cycles per f32 MFMA instruction (each 2,048 FLOP) counted from the
+            # layer's executed FLOPs: 32 if the counter's unit is what the guide says.  fracTF is
+            # the same launch's executed TF/s over the 157.3 TF peak (2.4 GHz), i.e. the bench's frac.
+            mb = pmc.get("SQ_VALU_MFMA_BUSY_CYCLES", {}).get(name, [])
+            ga = pmc.get("GRBM_GUI_ACTIVE", {}).get(name, [])
+            if mf and mb and ga and is_conv:
+                busy = sum(mb) / len(mb)
+                clk = sum(ga) / len(ga) / 8.0
+                n_mfma = exec_flop / 2048.0
+                row["mfma_busy_cycles"] = busy
+                row["gui_active_cycles_per_xcd"] = clk
+                row["mhz"] = clk / (sum(v) / len(v) * 1e-9) / 1e6 if v else 0.0
+                row["cycles_per_mfma"] = busy / n_mfma if n_mfma else 0.0
+                row["mfma_busy_frac"] = busy / (1024.0 * clk) if clk else 0.0
+                fa["mfma_busy"] += busy * cnt
+                fa["mfma_clk"] += clk * cnt
+                line += (f" {row['mhz']:6.0f} {row['cycles_per_mfma']:8.1f} {100 * row['mfma_busy_frac']:7.1f}%"
+                         f" {100 * row['exec_tflops'] / PEAK:5.1f}%")
         summary.append(row)
         print(line)
     print(f"forward: {tot_ns / 1e6:.3f} ms, {tot_flop / 1e12:.3f} TFLOP -> {tot_flop / tot_ns / 1e3:.1f} TF/s; "
@@ -193,6 +216,11 @@ def main():
              "alg_bytes_per_launch": fa["alg_bytes"] / fa["launches"]}
         if fa["pmc_launches"]:
             k["hbm_bytes_per_launch"] = fa["hbm_bytes"] / fa["pmc_launches"]
+        if fa["mfma_clk"]:
+            k["mfma_busy_frac"] = fa["mfma_busy"] / (1024.0 * fa["mfma_clk"])
+            k["exec_frac_of_peak"] = k["exec_tflops"] / PEAK
+            print(f"{family:9s}: MFMA busy {100 * k['mfma_busy_frac']:.1f}% of the SIMD cycles (PMC) vs executed "
+                  f"{100 * k['exec_frac_of_peak']:.1f}% of the 2.4-GHz peak (FLOP / time)")
         kernels[family] = k
         print(f"{family:9s}: {k['launches_per_forward']:3d} launches/fwd, {k['ms_per_forward']:.3f} ms/fwd, "
               f"avg {k['avg_launch_ms']:.4f} ms, alg {k['alg_tflops']:.1f} TF/s, executed {k['exec_tflops']:.1f} TF/s"
