@@ -89,8 +89,11 @@ constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum wi
 // output-geometry tables of the items in flight: the transform waves' load stream runs at most
 // NBUF + 2 K-steps (so items) ahead of the MFMA waves' consumption
 constexpr int NGEO = 8;
+// MODE 2: segments of a workgroup's stream (whole-item rounds + at most 3 tail segments), kept in
+// an LDS table (item, first step) so the schedule's scalars do not stay live across the K loop
+constexpr int MAXSEG = 64;
 static_assert(NGEO > NBUF + 2, "geometry table overwritten while an epilogue may still read it");
-static_assert((NBUF * VSTEP + NGEO * FT * 8 + 8) * 4 <= 160 * 1024, "LDS budget");
+static_assert((NBUF * VSTEP + NGEO * FT * 8 + 8 + 2 * MAXSEG) * 4 <= 160 * 1024, "LDS budget");
 static_assert(NXI % uring_depth<EPI_AFFINE_RES>() == 0 && NXI % uring_depth<EPI_AFFINE>() == 0,
               "U ring phase must repeat every K-step");
 
@@ -273,12 +276,14 @@ __device__ __forceinline__ Item item_of(const Wino4Params& p, int gi) {
 // MODE: 0 = whole items round-robin over the persistent grid; 1 = split-K (every item's K loop
 // cut into ksplit parts, raw partial outputs into compact slots [item][part][16 tiles]
 // [16 pixels][64 couts], summed in part order by wino4_part_fixup_kernel: small grids);
-// 2 = stream-K (the item-step space cut into equal contiguous ranges, one per workgroup; an item
-// cut at a range boundary leaves two parts).
+// 2 = stream-K: p.sk_dp rounds of whole items round-robin (data-parallel), then the remaining
+// (tail) items' K-steps cut into equal contiguous ranges, one per workgroup.  An item cut by the
+// ranges leaves one raw partial per workgroup that worked on it; the last-arriving wave (a ticket
+// per item and MFMA wave) sums them in workgroup order and finishes the item in this launch.
 template <bool PRE, int EPI, int MODE>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   constexpr bool SPLIT = MODE == 1, SK = MODE == 2;
-  __shared__ __attribute__((aligned(16))) float ring[NBUF * VSTEP + NGEO * FT * 8 + 8];
+  __shared__ __attribute__((aligned(16))) float ring[NBUF * VSTEP + NGEO * FT * 8 + 8 + 2 * MAXSEG];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout;
@@ -286,17 +291,27 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   const int KS = SPLIT ? p.ks_per : KST;          // stream steps per item
   const int nitems = p.nitem * p.ksplit;
   // MODE 0/1: this workgroup's items are blockIdx.x, blockIdx.x + gridDim.x, ... of the
-  // XCD-remapped order (item_at(j), j local).  SK: it owns item-steps [u_lo, u_hi) of the
-  // nT * KST space (its logical index XCD-remapped, so an XCD's workgroups hold one contiguous
-  // run of items); item_at(t) then takes the global item index t.
+  // XCD-remapped order (item_at(j), j local).  SK: segments j < sk_dp are the whole items
+  // blockIdx.x + j * gridDim.x of the XCD-remapped order of the first D = sk_dp * gridDim.x
+  // items; then it owns the tail item-steps [u_lo, u_hi) of the (nT - D) * KST space (its logical
+  // index XCD-remapped, so an XCD's workgroups hold one contiguous run of tail items): segment
+  // sk_dp + i is tail item tt_first + i, the first one from step s_tail0.
   const int nloc = (nitems - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
   const int nT = p.mblocks * p.nblocks;
+  const int D = SK ? p.sk_dp * (int)gridDim.x : 0;
+  const long long TT = SK ? (long long)(nT - D) * KST : 0;  // tail item-steps
   const int bl = SK ? xcd_remap(blockIdx.x, gridDim.x) : 0;
-  const int u_lo = SK ? (int)((long long)bl * nT * KST / gridDim.x) : 0;
-  const int u_hi = SK ? (int)((long long)(bl + 1) * nT * KST / gridDim.x) : 0;
-  const int t_first = u_lo / KST, t_last = SK ? (u_hi - 1) / KST : nloc - 1;
+  const int u_lo = SK ? (int)((long long)bl * TT / gridDim.x) : 0;
+  const int u_hi = SK ? (int)((long long)(bl + 1) * TT / gridDim.x) : 0;
+  const int tt_first = u_lo / KST, s_tail0 = u_lo - tt_first * KST;
+  const int nseg = SK ? p.sk_dp + (u_hi > u_lo ? (u_hi - 1) / KST - tt_first + 1 : 0) : nloc;
+  const int t_last = nseg - 1;  // last segment
+  int* const segtab = reinterpret_cast<int*>(ring + NBUF * VSTEP + NGEO * FT * 8 + 8);  // SK: [MAXSEG][item, step0]
+  auto seg_begin = [&](int j) {
+    return SK && j <= t_last ? __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j + 1]) : 0;
+  };
   auto item_at = [&](int j) {
-    if (SK) return item_of(p, j);
+    if (SK) return item_of(p, __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j]));
     const int t = xcd_remap(blockIdx.x + j * gridDim.x, nitems);
     const int sp = t / p.nitem, li = t - sp * p.nitem;
     Item it = item_of(p, p.item0 + li);
@@ -307,12 +322,17 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   // K-steps item `it` really has (split-K: the last split may be short; its stream is padded
   // with steps whose patches load as zeros, so every item is KS stream steps long)
   auto steps_of = [&](const Item& it) { return SPLIT ? min(KS, KST - it.split * KS) : KST; };
-  const int G = SK ? u_hi - u_lo : nloc * KS;  // K-steps in this workgroup's stream (one hand-off each)
+  const int G = SK ? p.sk_dp * KST + (u_hi - u_lo) : nloc * KS;  // K-steps in this workgroup's stream
 
   int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [NGEO items][16 tiles][8]
   int* const rdy = geo + NGEO * FT * 8;                           // [4] K-steps written, per transform wave
   int* const fre = rdy + 4;                                       // [4] K-steps read, per MFMA wave
   if (tid < 8) rdy[tid] = 0;
+  if (SK && tid < nseg) {
+    const int q = tid;
+    segtab[2 * q] = q < p.sk_dp ? xcd_remap(blockIdx.x + q * gridDim.x, D) : D + tt_first + (q - p.sk_dp);
+    segtab[2 * q + 1] = q == p.sk_dp ? s_tail0 : 0;
+  }
   __syncthreads();  // the kernel's only workgroup barrier
   if (G <= 0) return;
   if (wid >= 4) {
@@ -345,8 +365,8 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     // every image row when such a canvas row exists), so it may take the shift like an
     // in-image pixel.
     float rowm[6], colm[3];
-    int lj = SK ? t_first : 0, ls = SK ? u_lo - t_first * KST : 0, ks_real = KS, step0 = 0;
-    bool first = true;
+    int lj = 0, ls = seg_begin(0), ks_real = KS, step0 = 0;
+    bool fresh = true;  // SK: the next load starts segment lj
     auto enter_item = [&](int j) {
       const Item it = item_at(min(j, t_last));
       ks_real = steps_of(it);
@@ -404,8 +424,8 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     Patch pa, pb, pc;
     // issue the patch loads of the next step of the stream (steps are loaded in order)
     auto load = [&](Patch& P) {
-      if (ls == 0 || (SK && first)) enter_item(lj);
-      first = false;
+      if (SK ? fresh : ls == 0) enter_item(lj);
+      fresh = false;
       // split-K padding step: every load is out of range (num_records 0) and reads zeros, and
       // the BN shift is dropped
       // (readfirstlane: the stream counters are wave-uniform, but the compiler loses track of
@@ -429,8 +449,9 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         for (int e = 0; e < 3; ++e) P.colm[e] = colm[e];
       }
       if (++ls == KS) {
-        ls = 0;
         ++lj;
+        ls = seg_begin(lj);
+        fresh = true;
       }
     };
     // the ring address of (tile i, channels ch, ch+1): A-fragment slot lane 16 k + i
@@ -528,7 +549,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   };
   // segments of the stream: MODE 0/1 item j (local) steps [0, KS); SK item j (global) steps
   // [s0, s1) -- only the first and the last segment of a workgroup's range can be partial
-  int j = SK ? t_first : 0, s_beg = SK ? u_lo - t_first * KST : 0;
+  int j = 0, s_beg = seg_begin(0);
   constexpr int URING = uring_depth<EPI>();
   f4 uring[URING];
   int ub = ubase(j), ul = ulast(j);
@@ -549,7 +570,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   // accumulators that are not live yet at the start of a K-step, so it costs no registers at the
   // peak.  Before the first item nothing is pending (offsets past the range: stores dropped);
   // the last item's part B runs after the loop.
-  constexpr bool DEFER = !SPLIT && !SK;
+  constexpr bool DEFER = !SPLIT;  // MODE 2: its whole-item segments
   constexpr bool DRES = DEFER && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
   const __amdgpu_buffer_rsrc_t yr_d = uniform_rsrc(p.y, p.B * H * W * Cout * 4);
   f4 pv[16], pres[16], psc = {1.f, 1.f, 1.f, 1.f}, psh = {0.f, 0.f, 0.f, 0.f}, pal = psh, pcl = psh;
@@ -581,11 +602,16 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
     __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);
   };
-  for (; SK ? g < G : j < nloc; ++j) {
+  // One segment of the stream: its K-steps, then its epilogue.  TAIL (MODE 2 after the whole-
+  // item rounds): no deferred part B, every segment goes through a slot and a ticket (below).
+  // The two kinds are separate loops over separate instances of this body, so the tail's extra
+  // state never competes with the whole items' registers.
+  auto segment = [&](auto tail_c) {
+    constexpr bool TAIL = decltype(tail_c)::value;
     const Item it = item_at(j);
-    const int s0 = s_beg, s1 = SK ? min(KST, s0 + (G - g)) : KS;
+    const int s0 = s_beg, s1 = TAIL ? min(KST, s0 + (G - g)) : KS;
     const bool live = it.nb * 64 + w * 16 < Cout;  // Cout % 64 != 0: idle quarter of the last block
-    const int ub_next = ubase(j + 1);               // the next item's first step (prefetched
+    const int ub_next = ubase(j + 1);               // the next item's step 0; its first step (prefetched
                                                     // during this item's last one)
     f4 acc[NXI];
 #pragma unroll
@@ -596,7 +622,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       const float* vn = vrd + ((g + 1) % NBUF) * VSTEP;
       // U refills: xi + URING of this step, or xi + URING - 36 of the next step (or item)
       const int cur = ub + min(s, ul) * 1024;
-      const int nxt = s + 1 < s1 ? ub + min(s + 1, ul) * 1024 : ub_next;
+      const int nxt = s + 1 < s1 ? ub + min(s + 1, ul) * 1024 : ub_next + seg_begin(j + 1) * 1024;
       // xi in pairs: the two accumulation chains interleave (a 16x16x4 MFMA's result is not
       // ready for the next one on the same accumulator at issue rate).  A fragments one pair
       // ahead (the LDS reads of pair x + 2 are in flight during pair x's MFMAs); an idle
@@ -631,7 +657,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
         // the previous item's pending output pixel x / 2 - 2 (after this pair's refills, so the
         // refills of earlier pairs never wait for its store)
-        if constexpr (DEFER && decltype(first_step)::value)
+        if constexpr (DEFER && !TAIL && decltype(first_step)::value)
           if (x >= 4) finish(x / 2 - 2);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -647,19 +673,15 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     for (int s = s0 + 1; s < s1; ++s) kstep(s, std::false_type{});
     ub = ub_next;
     ul = ulast(j + 1);
-    s_beg = 0;
+    s_beg = seg_begin(j + 1);
     // an idle quarter (!live, Cout % 64 != 0) runs the epilogue too, with every store dropped
     // (no branch: a merge here costs the next K-step a full wait for stores)
-    const bool partial = SK && (s0 > 0 || s1 < KST);
     // ---- epilogue (lane-local): U is the A operand, so lane (tile n, row group rg) holds
     // couts 4rg .. 4rg+3 of tile n for every xi; Y = A^T M A per (tile, cout), BN (+PReLU |
     // +residual), one 16-byte store of the 4 couts per output pixel
     const int n = lane & 15, rg = lane >> 4;
     const int cout0 = min(it.nb * 64 + w * 16, Cout - 16) + 4 * rg;  // (clamped for an idle quarter)
-    const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(p.y, p.B * H * W * Cout * 4);
-    constexpr bool RES = !SPLIT && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
-    constexpr bool PRELU = !SPLIT && (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU);
-    const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, RES ? p.B * H * W * Cout * 4 : 0);
+    const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, DRES ? p.B * H * W * Cout * 4 : 0);
     // byte offsets of tile n's 16 outputs = a row part + a column part (8 multiplies, not 16).
     // Padding rows / columns and an idle quarter get BIGOFF, so every sum with them lies past the
     // buffer's range (unsigned) and the store / residual load is dropped by the range check,
@@ -682,171 +704,185 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
     if constexpr (DEFER) {
       // part A: rows of A^T M A on all 4 couts (each frees 8 accumulator registers), the residual
       // of output rows 0-1 in flight during the column pass, then rows 2-3
+      auto transform_to_pv = [&]() {
+        f4 z[6][4];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          const f4 m6[6] = {acc[6 * a], acc[6 * a + 1], acc[6 * a + 2], acc[6 * a + 3], acc[6 * a + 4], acc[6 * a + 5]};
+          at6q(m6, z[a]);
+        }
+        if constexpr (DRES)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) pres[i] = ld4(rr, oo[i >> 2][i & 3]);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const f4 c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
+          f4 o[4];
+          at6q(c6, o);
+#pragma unroll
+          for (int y = 0; y < 4; ++y) pv[4 * y + x] = o[y];
+        }
+      };
+      auto set_pending = [&]() {
+        if constexpr (DRES)
+#pragma unroll
+          for (int i = 8; i < 16; ++i) pres[i] = ld4(rr, oo[i >> 2][i & 3]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) po[i] = oo[i >> 2][i & 3];
+        psc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
+        psh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
+        if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) {
+          pal = *reinterpret_cast<const f4*>(p.prelu + cout0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pcl[r] = pal[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
+        }
+      };
+      if constexpr (TAIL) {
+        {
+          // a tail item (usually cut across workgroups): this wave's raw partial outputs (linear in
+          // the K-steps, so the parts sum to the item's output) into its compact slot [16 tiles][16
+          // pixels][64 couts], write-through (sc1), so the release below has no dirty slot lines to
+          // write back: slot 2 bl for the item this workgroup's range starts in, 2 bl + 1 for the
+          // item it ends in.  Few registers live here: outputs go straight to the slot and the
+          // finish works four pixels at a time.
+          const int slot = 2 * bl + (j == p.sk_dp ? 0 : 1);
+          const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
+          auto soff = [&](int sl, int i) { return ((((sl * FT + n) * 16 + i) * FN) + w * 16 + 4 * rg) * 4; };
+          {
+            f4 z[6][4];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+              const f4 m6[6] = {acc[6 * a], acc[6 * a + 1], acc[6 * a + 2], acc[6 * a + 3], acc[6 * a + 4], acc[6 * a + 5]};
+              at6q(m6, z[a]);
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+              const f4 c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
+              f4 o[4];
+              at6q(c6, o);
+#pragma unroll
+              for (int y = 0; y < 4; ++y) {
+                const u32x4 bits = {__float_as_uint(o[y].x), __float_as_uint(o[y].y), __float_as_uint(o[y].z),
+                                    __float_as_uint(o[y].w)};
+                __builtin_amdgcn_raw_buffer_store_b128(bits, sr, soff(slot, 4 * y + x), 0, CPOL_SC1);
+              }
+            }
+          }
+          // parts of tail item ti come from the workgroups first .. last whose ranges meet its
+          // steps [t_lo, t_hi); this wave's ticket (one per item and MFMA wave, G16 counter form)
+          // tells whether it arrived last.  The last one sums the parts in workgroup order
+          // (independent of the arrival order: deterministic) and finishes the item.
+          const int P = gridDim.x;
+          const int ti = __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j]) - p.sk_dp * P;  // tail index
+          const long long TTt = (long long)(p.mblocks * p.nblocks - p.sk_dp * P) * KST;
+          const long long t_lo = (long long)ti * KST, t_hi = t_lo + KST;
+          auto lo_of = [&](int x) { return (long long)x * TTt / P; };
+          int first = (int)(t_lo * P / TTt);
+          while (first + 1 < P && lo_of(first + 1) <= t_lo) ++first;
+          while (first > 0 && lo_of(first) > t_lo) --first;
+          int last = (int)((t_hi - 1) * P / TTt);
+          while (last + 1 < P && lo_of(last + 1) <= t_hi - 1) ++last;
+          while (last > 0 && lo_of(last) > t_hi - 1) --last;
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          int ticket = 0;
+          if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            ticket = __hip_atomic_fetch_add(p.cnt + ti * 4 + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          ticket = __builtin_amdgcn_readfirstlane(ticket);
+          if (ticket != last - first) return;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          if (lane == 0) p.cnt[ti * 4 + w] = 0;  // re-arm for the next launch (zeroed at allocation)
+          const f4 sc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
+          const f4 sh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
+          f4 al = {0.f, 0.f, 0.f, 0.f}, cl = al;
+          if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) {
+            al = *reinterpret_cast<const f4*>(p.prelu + cout0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cl[r] = al[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
+          }
+#pragma unroll
+          for (int i0 = 0; i0 < 16; i0 += 4) {
+            f4 sm[4] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+            for (int c = first; c <= last; ++c) {
+              const int cslot = 2 * c + (lo_of(c) < t_lo ? 1 : 0);
+#pragma unroll
+              for (int k = 0; k < 4; ++k) sm[k] += ld4(sr, soff(cslot, i0 + k));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int o = oo[(i0 + k) >> 2][(i0 + k) & 3];
+              f4 v = __builtin_elementwise_fma(sm[k], sc, sh);
+              if constexpr (EPI == EPI_AFFINE_PRELU) v = prelu_q(v, al, cl);
+              if constexpr (DRES) {
+                v += ld4(rr, o);
+                if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = prelu_q(v, al, cl);
+              }
+              const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+              __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, o, 0, 0);
+            }
+          }
+          return;
+        }
+      }
+      transform_to_pv();
+      set_pending();
+      return;
+    }
+    // MODE 1 (split-K): raw partial outputs (the same output transform, no epilogue) into compact
+    // slot [16 tiles][16 pixels][64 couts] of split it.split of launch item it.li, summed in split
+    // order and finished by wino4_part_fixup_kernel.  Write-through (sc1): the fixup on other XCDs
+    // reads the slots right after this launch, and a launch that leaves its slots dirty in L2 pays
+    // for their write-back at the kernel boundary (serving batch 1: embed + match 1.925 -> 1.851
+    // ms, same box)
+    if constexpr (SPLIT) {
       f4 z[6][4];
 #pragma unroll
       for (int a = 0; a < 6; ++a) {
         const f4 m6[6] = {acc[6 * a], acc[6 * a + 1], acc[6 * a + 2], acc[6 * a + 3], acc[6 * a + 4], acc[6 * a + 5]};
         at6q(m6, z[a]);
       }
-      if constexpr (DRES)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) pres[i] = ld4(rr, oo[i >> 2][i & 3]);
+      const int slot = it.li * p.ksplit + it.split;
+      const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const f4 c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
         f4 o[4];
         at6q(c6, o);
 #pragma unroll
-        for (int y = 0; y < 4; ++y) pv[4 * y + x] = o[y];
-      }
-      if constexpr (DRES)
-#pragma unroll
-        for (int i = 8; i < 16; ++i) pres[i] = ld4(rr, oo[i >> 2][i & 3]);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) po[i] = oo[i >> 2][i & 3];
-      psc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
-      psh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
-      if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) {
-        pal = *reinterpret_cast<const f4*>(p.prelu + cout0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pcl[r] = pal[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
-      }
-      continue;
-    }
-    // residual rows 0-1 in flight during the output transform of couts 2-3, rows 2-3 while rows
-    // 0-1 are stored (issued earlier they would spill beside the 144 accumulators)
-    f4 rv[4][4];
-    auto load_res = [&](int y0) {
-      if constexpr (RES)
-        if (!partial)
-#pragma unroll
-          for (int y = y0; y < y0 + 2; ++y)
-#pragma unroll
-            for (int x = 0; x < 4; ++x) rv[y][x] = ld4(rr, oo[y][x]);
-    };
-    // (stream-K carries more live registers: there row y + 1 goes out while row y is stored)
-    f2 outv[2][4][4];  // [cout pair q][y][x]: couts 2q, 2q + 1 (packed f32)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (!SK && q == 1) load_res(0);
-      f2 z[6][4];
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {  // rows: A^T along b
-        f2 m6[6];
-#pragma unroll
-        for (int b = 0; b < 6; ++b) m6[b] = f2{acc[6 * a + b][2 * q], acc[6 * a + b][2 * q + 1]};
-        at6v(m6, z[a]);
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {  // columns: A^T along a
-        const f2 c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
-        f2 o[4];
-        at6v(c6, o);
-#pragma unroll
-        for (int y = 0; y < 4; ++y) outv[q][y][x] = o[y];
-      }
-    }
-    if constexpr (!SK) load_res(2);
-    auto out4 = [&](int y, int x) {
-      return f4{outv[0][y][x].x, outv[0][y][x].y, outv[1][y][x].x, outv[1][y][x].y};
-    };
-    if (SPLIT || (SK && partial)) {
-      // raw partial outputs into compact slot [16 tiles][16 pixels][64 couts]: split-K part
-      // it.split of launch item it.li, or (stream-K) part 0 / 1 of the item cut at range
-      // boundary bd (the first part ends at this workgroup's range end, the second starts at its
-      // range start); summed in part order and finished by wino4_part_fixup_kernel
-      const int slot = SPLIT ? it.li * p.ksplit + it.split : (s0 == 0 ? bl + 1 : bl) * 2 + (s0 == 0 ? 0 : 1);
-      const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
-      // write-through (sc1): the fixup on other XCDs reads the slots right after this launch, and
-      // a launch that leaves its slots dirty in L2 pays for their write-back at the kernel
-      // boundary (serving batch 1: embed + match 1.925 -> 1.851 ms, same box)
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const f4 v = out4(y, x);
-          const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+        for (int y = 0; y < 4; ++y) {
+          const u32x4 bits = {__float_as_uint(o[y].x), __float_as_uint(o[y].y), __float_as_uint(o[y].z),
+                              __float_as_uint(o[y].w)};
           const int off = ((((slot * FT + n) * 16 + y * 4 + x) * FN) + w * 16 + 4 * rg) * 4;
           __builtin_amdgcn_raw_buffer_store_b128(bits, sr, off, 0, CPOL_SC1);
         }
-      continue;
-    }
-    f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f}, al = {0.f, 0.f, 0.f, 0.f}, cl = al;
-    if constexpr (!SPLIT) {
-      sc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
-      sh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
-    }
-    // PReLU t > 0 ? t : a t as med3(t, a t, c): c = +inf for a slope a <= 1 (= max(t, a t)),
-    // -inf for a > 1 (= min(t, a t)); med3 returns one of its operands, so the value is the
-    // reference's exactly (up to the sign of a zero), in a packed multiply and a med3 per value
-    // instead of a multiply, a compare and a select
-    if constexpr (PRELU) {
-      al = *reinterpret_cast<const f4*>(p.prelu + cout0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cl[r] = al[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
-    }
-    auto prelu4 = [&](f4 v) {
-      const f4 av = v * al;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = __builtin_amdgcn_fmed3f(v[r], av[r], cl[r]);
-      return v;
-    };
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      if constexpr (SK && RES) {
-        if (y == 0)
-#pragma unroll
-          for (int x = 0; x < 4; ++x) rv[0][x] = ld4(rr, oo[0][x]);
-        if (y + 1 < 4)
-#pragma unroll
-          for (int x = 0; x < 4; ++x) rv[y + 1][x] = ld4(rr, oo[y + 1][x]);
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        f4 v = out4(y, x);
-        if constexpr (!SPLIT) {
-          v = __builtin_elementwise_fma(v, sc, sh);
-          if constexpr (EPI == EPI_AFFINE_PRELU) v = prelu4(v);
-          if constexpr (RES) {
-            v += rv[y][x];
-            if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = prelu4(v);
-          }
-        }
-        const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(bits, yr, oo[y][x], 0, 0);
       }
     }
+  };
+  if constexpr (SK) {
+    for (; j < p.sk_dp; ++j) segment(std::false_type{});
+    // the last whole item's part B before the tail, whose segments defer nothing
+#pragma unroll
+    for (int i = 0; i < 16; ++i) finish(i);
+    while (g < G) {  // (segment advances g)
+      segment(std::true_type{});
+      ++j;
+    }
+  } else {
+    for (; j < nloc; ++j) segment(std::false_type{});
+    if constexpr (DEFER)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) finish(i);  // the last item's part B
   }
-  if constexpr (DEFER)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) finish(i);  // the last item's part B
   w4_report_handoff(rseen, p.err);
 }
 
-// G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
-// A-fragment (U) order wino4_kernel reads: [xi][Cout/16][Cin/16][lane = 16 k + cout%16][m] with
-// cin % 16 = 4k + m.
-// Split-K / stream-K finish: y = epilogue(sum of an item's raw partial outputs, in part order:
-// deterministic) at the item's in-image pixels.  Thread = (tile n, pixel, cout quad); grid
-// (FT * 16 * FN / 4 / 256, items).  SKF: blockIdx.y + 1 is a stream-K range boundary (the item
-// it cuts has parts in slots 2 bd, 2 bd + 1; an uncut boundary returns); else blockIdx.y is the
-// launch item li with parts in slots li * S .. li * S + S - 1.
-template <int EPI, bool SKF>
+// Split-K finish: y = epilogue(sum of an item's raw partial outputs, in part order: deterministic)
+// at the item's in-image pixels.  Thread = (tile n, pixel, cout quad); grid (FT * 16 * FN / 4 /
+// blockDim, items): blockIdx.y is the launch item li with parts in slots li * S .. li * S + S - 1.
+template <int EPI>
 __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
-  int gi, slot0, S;
-  if (SKF) {
-    const int bd = blockIdx.y + 1;
-    const long long N = (long long)p.mblocks * p.nblocks * KST;
-    const int u = (int)(bd * N / P);
-    if (u % KST == 0) return;
-    gi = u / KST;
-    slot0 = 2 * bd;
-    S = 2;
-  } else {
-    gi = p.item0 + blockIdx.y;
-    slot0 = blockIdx.y * p.ksplit;
-    S = p.ksplit;
-  }
+  const int gi = p.item0 + blockIdx.y, slot0 = blockIdx.y * p.ksplit, S = p.ksplit;
   const Item it = item_of(p, gi);
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = idx >> 8, px = (idx >> 4) & 15, cq = idx & 15;
@@ -900,6 +936,9 @@ __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
   __builtin_amdgcn_raw_buffer_store_b128(bits, yr, (int)(yo * 4), 0, CPOL_SC1);
 }
 
+// G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
+// A-fragment (U) order wino4_kernel reads: [xi][Cout/16][Cin/16][lane = 16 k + cout%16][m] with
+// cin % 16 = 4k + m.
 __global__ void wino4_weight_kernel(const float* __restrict__ w, const float* __restrict__ pre_scale,
                                     float* __restrict__ u, int Cout, int Cin) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1018,19 +1057,19 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
     }
     return std::max(S, 1);
   };
-  // stream-K (opt-in, p.sk_mode): each workgroup runs an equal share of the item-steps; cut items
-  // are finished by wino4_part_fixup_kernel.  Whole items keep every workgroup on the same K-step
-  // of its item, so an XCD's workgroups read the same U slice at a time; stream-K ranges start
-  // at arbitrary steps and read all of U at once, which pays only while U fits an XCD's 4 MB L2
-  // (measured, IR-101 B=256: stage 2 128->128, U 2.4 MB, neutral; stage 3 256->256, U 9.4 MB,
-  // 238 -> 324 us).  With fewer than 8 K-steps per item the two partial epilogues and the fixup
-  // outweigh the round (stage 1 64->64: 297 -> 314 us).
-  const double rounds = (double)nT / cus;
-  const bool sk = p.sk_mode && p.part && aligned && nT > cus && cus % 8 == 0 &&
-                  (p.sk_mode == 2 || (KST >= 8 && (long long)NXI * p.Cin * p.Cout * 4 <= (3ll << 20) &&
-                                      std::ceil(rounds) - rounds > 0.1)) &&
-                  (long long)(cus + 1) * 2 * SLOT <= p.part_floats;
+  // stream-K (p.sk_mode): whole items for floor(nT / cus) rounds, then the tail items' K-steps in
+  // equal contiguous ranges, one per workgroup, so the part-empty last round of whole items
+  // (IR-101 B=256: stage 3 3.52 rounds run as 4, stage 2 6.13 as 7) becomes a fraction of a round;
+  // a cut item is finished in the launch by its last-arriving wave.  Whole items keep every
+  // workgroup on the same K-step of its item, so an XCD's workgroups read the same U slice at a
+  // time; stream-K ranges start at arbitrary steps and read all of U at once (round 2, stream-K
+  // over ALL item-steps at stage 3, U 9.4 MB: 238 -> 324 us), so only the tail runs that way.
+  // sk_mode 2 (tests, experiments) cuts every item-step.
+  const int sk_dp = p.sk_mode == 2 ? 0 : nT / cus;
+  const bool sk = p.sk_mode && p.part && p.cnt && aligned && nT > cus && cus % 8 == 0 && nT % cus != 0 &&
+                  (long long)(nT - sk_dp * cus) * 4 <= p.cnt_cap && (long long)2 * cus * SLOT <= p.part_floats;
   // Whole-item launch of n items from item0 (MODE 0), or split-K launch (MODE 1) + fixup
+  p.sk_dp = sk_dp;
   Wino4Params pw = p;
   auto whole = [&](int item0, int n) {
     pw = p;
@@ -1052,11 +1091,8 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
     hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, MODE_>), dim3(MODE_ == 2 ? cus : std::min(nit, cus)),      \
                        dim3(512), 0, s, pw);                                                                \
     if (MODE_ == 1) /* 64-thread blocks: a serving grid's few items still spread over the CUs */          \
-      hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_, false>), dim3(FT * 16 * FN / 4 / 64, pw.nitem),     \
+      hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_>), dim3(FT * 16 * FN / 4 / 64, pw.nitem),     \
                          dim3(64), 0, s, pw, KST, cus);                                                     \
-    if (MODE_ == 2)                                                                                         \
-      hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_, true>), dim3(FT * 16 * FN / 4 / 256, cus - 1),      \
-                         dim3(256), 0, s, pw, KST, cus);                                                    \
   }
 #define FR_W4_CASE(PRE_, EPI_)                                                                              \
   if (pre == PRE_ && epi == EPI_) {                                                                         \

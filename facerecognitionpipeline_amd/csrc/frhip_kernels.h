@@ -130,10 +130,14 @@ struct Wino4Params {
   long long part_floats;
   int ksplit, ks_per;      // set by launch_wino4
   int item0, nitem;        // set by launch_wino4: the launch's range of the layer's item order
-  // 1: stream-K over the item-steps when whole items leave the last round >= 10% empty and U
-  // fits an XCD's L2 (uses part for the cut items' two raw partials); 2: stream-K whenever the
-  // grid has more items than CUs (experiments); 0: whole items only
+  // 0: whole items only; 1: whole-item rounds + a stream-K tail (the last, part-empty round's
+  // item-steps cut into equal ranges, cut items finished in-kernel) when the grid has more items
+  // than CUs and the last round is part-empty; 2: stream-K over all item-steps whenever the grid
+  // has more items than CUs (experiments); uses part for the cut items' raw partials
   int sk_mode;
+  int sk_dp;  // set by launch_wino4: whole-item rounds before a stream-K tail (MODE 2)
+  int* cnt;   // MODE 2 tail tickets [tail items][4 MFMA waves], zeroed once, re-armed in-kernel
+  int cnt_cap;
   int no_split;  // 1: never split-K (tests compare the two schedules)
   int max_split;  // > 0: at most this many K parts per item in a split-K launch (serving sweeps)
   // ring hand-off guard: a wave that has polled its LDS counters poll_max times without seeing

@@ -364,8 +364,11 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.W = W;
     wp.Cin = cw.cin;
     wp.Cout = cw.cout;
+    // the workspace's tail holds the stream-K tail tickets (zeroed at allocation, re-armed in-kernel)
     wp.part = w4part;
-    wp.part_floats = w4part ? fr_handle::W4PART_FLOATS : 0;
+    wp.part_floats = w4part ? fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS : 0;
+    wp.cnt = w4part ? reinterpret_cast<int*>(w4part + (fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS)) : nullptr;
+    wp.cnt_cap = w4part ? (int)fr_handle::W4CNT_INTS : 0;
     wp.sk_mode = g_wino4_streamk;
     wp.max_split = g_wino4_max_split;
     wp.err = h->dev_err;
@@ -504,7 +507,10 @@ int ensure_lane(fr_handle* h, int l, int batch) {
                                                 sizeof(float)));
     h->lane_batch[l] = batch;
   }
-  if (!L.w4part) FR_HIP(h, hipMalloc((void**)&L.w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
+  if (!L.w4part) {
+    FR_HIP(h, hipMalloc((void**)&L.w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
+    FR_HIP(h, hipMemset(L.w4part + (fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS), 0, fr_handle::W4CNT_INTS * sizeof(int)));
+  }
   if (ensure_stream_k(h->device, &h->cus, &L.sk_ws, &L.sk_ws_floats, &L.sk_cnt, &L.sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
   if (!h->lane_stream[l]) FR_HIP(h, hipStreamCreateWithFlags(&h->lane_stream[l], hipStreamNonBlocking));
@@ -1393,6 +1399,7 @@ int fr_finalize(fr_handle* h) {
     FR_HIP(h, hipMalloc((void**)&h->rs_stage, mb * 112 * 112 * 3));
     FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
+    FR_HIP(h, hipMemset(h->w4part + (fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS), 0, fr_handle::W4CNT_INTS * sizeof(int)));
   }
   if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
@@ -2013,9 +2020,15 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.no_split = !g_frt_wino4_split;
     p.poll_max = g_wino4_poll;
     p.err = frt_err;
-    if (g_frt_wino4_split || g_wino4_streamk) {  // split-K / stream-K partial slots (64 KiB each)
+    if (g_frt_wino4_split || g_wino4_streamk) {  // split-K / stream-K partial slots (64 KiB each) + tail tickets
       p.part_floats = 257ll * 2 * 16 * 16 * 64;
-      if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;
+      p.cnt_cap = 1 << 16;
+      if (hipMalloc((void**)&part, p.part_floats * sizeof(float) + p.cnt_cap * sizeof(int)) != hipSuccess)
+        e = hipErrorOutOfMemory;
+      else {
+        p.cnt = reinterpret_cast<int*>(part + p.part_floats);
+        e = hipMemset(p.cnt, 0, p.cnt_cap * sizeof(int));
+      }
       p.part = part;
     }
     if (e == hipSuccess) e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s);

@@ -154,6 +154,7 @@ struct fr_handle {
   float* wino4_arena = nullptr;  // F(4x4) filters, likewise
   float* w4part = nullptr;         // F(4x4) split-K partial outputs (small batches), W4PART_FLOATS
   static constexpr long long W4PART_FLOATS = 16ll << 20;
+  static constexpr long long W4CNT_INTS = 1 << 16;  // its last 256 KB: F(4x4) stream-K tail tickets
 
   // lanes (fr_set_lanes): a forward of n crops runs as min(lane_max, n / lane_min) concurrent
   // parts, lane 0 on the caller's stream with the workspace above, lane l >= 1 on lane_stream[l]

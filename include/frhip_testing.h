@@ -39,9 +39,11 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
  * cin % 16 == 0, cout % 16 == 0.  frt_conv2d_winograd4 gives launch_wino4 a split-K workspace
  * (small grids then split the K loop over items + a reduce pass) unless frt_set_wino4_split(0). */
 int frt_set_wino4_split(int on);
-/* F(4x4) stream-K schedule for large layers (default off, for handles too): 1 = by policy
- * (last round >= 10% empty, U fits an XCD's L2, >= 8 K-steps per item), 2 = whenever the grid
- * has more items than CUs, 0 = whole items round-robin over the persistent grid. */
+/* F(4x4) schedule of large layers (grids with more items than CUs), for handles too:
+ * 0 = whole items round-robin over the persistent grid; 1 = whole-item rounds, then the last
+ * part-empty round's item-steps in equal ranges per workgroup (cut items finished in the launch
+ * by their last-arriving wave); 2 = every item-step in equal ranges (experiments).
+ * Applies to launches issued after the call (captured graphs keep theirs). */
 int frt_set_wino4_streamk(int on);
 /* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
  * before the call keep their schedule). */

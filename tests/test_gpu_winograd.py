@@ -116,29 +116,35 @@ def test_winograd4_pre_bn_partial_canvas_row(B, H, W):
 
 
 @pytest.mark.parametrize("B,H,cin,cout", [
-    (256, 28, 128, 128),  # IR-101 stage 2: 1568 items = 6.13 rounds of 256 workgroups
+    (256, 28, 128, 128),  # IR-101 stage 2: 1568 items = 6 rounds + a 32-item tail (1 K-step per workgroup)
+    (256, 14, 256, 256),  # IR-101 stage 3: 900 items = 3 rounds + 132 (8.25 K-steps per workgroup)
+    (64, 56, 64, 64),     # stage 1 at B=64: 784 items + 16 * 4 tail steps: most workgroups' tail is empty
     (96, 28, 128, 128),   # 588 items = 2.3 rounds
     (160, 14, 128, 128),  # canvas of 14x14 images, 600 items
 ])
 @pytest.mark.parametrize("epi", [1, 2])
 def test_winograd4_stream_k(B, H, cin, cout, epi):
-    """Large grids whose items leave the last round part-empty run stream-K: equal item-step
-    ranges per workgroup, cut items finished from two raw partials by wino4_sk_fixup_kernel.
-    Matches the CPU conv, the whole-item schedule to the same bar, and is deterministic."""
+    """Large grids whose items leave the last round part-empty: whole-item rounds, then the tail
+    items' K-steps in equal ranges per workgroup (mode 1), or every item-step that way (mode 2);
+    the last-arriving wave of a cut item sums its raw partials in workgroup order and finishes it
+    in the launch.  Matches the CPU conv, the whole-item schedule to the same bar, and is
+    deterministic run to run."""
     L = _frt.lib()
     outs = {}
     try:
-        for mode in (1, 0):
+        for mode in (1, 2, 0):
             L.frt_set_wino4_streamk(mode)
             got, ref = _wino_case(B, H, cin, cout, epi, seed=1300 + H + cin + epi, m=4)
             _close(got, ref, rel=REL[4])
             outs[mode] = got
-        L.frt_set_wino4_streamk(1)
-        again, _ = _wino_case(B, H, cin, cout, epi, seed=1300 + H + cin + epi, m=4)
+        for mode in (1, 2):
+            L.frt_set_wino4_streamk(mode)
+            again, _ = _wino_case(B, H, cin, cout, epi, seed=1300 + H + cin + epi, m=4)
+            assert torch.equal(again, outs[mode]), f"stream-K mode {mode} is not run-to-run deterministic"
     finally:
         L.frt_set_wino4_streamk(0)
     _close(outs[1], outs[0], rel=REL[4])
-    assert torch.equal(again, outs[1]), "stream-K result is not run-to-run deterministic"
+    _close(outs[2], outs[0], rel=REL[4])
 
 
 def test_winograd4_small_cin():

@@ -7,6 +7,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <cmath>
+#include <algorithm>
 #include <vector>
 
 #include "frhip_kernels.h"
@@ -71,6 +73,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc((void**)&part, part_floats * sizeof(float)));
   p.part = part;
   p.part_floats = part_floats;
+  // stream-K tail tickets (zeroed once; the kernel re-arms them)
+  int* cnt = nullptr;
+  const int cnt_cap = 1 << 16;
+  CK(hipMalloc((void**)&cnt, 2 * cnt_cap * sizeof(int)));
+  CK(hipMemset(cnt, 0, 2 * cnt_cap * sizeof(int)));
+  p.cnt = cnt;
+  p.cnt_cap = cnt_cap;
   p.sk_mode = argc > 7 ? atoi(argv[7]) : 1;
   p.no_split = argc > 8 ? atoi(argv[8]) : 0;  // 1: whole items only (no tail split-K)
   // argv[9] lanes: 1 one stream; 2 two streams of B/2 each, launches interleaved (fr_set_lanes)
@@ -91,8 +100,10 @@ int main(int argc, char** argv) {
       pl[l].x = x + (size_t)l * hb * H * H * Cin;
       pl[l].y = y + (size_t)l * hb * H * H * Cout;
       pl[l].res = p.res ? res + (size_t)l * hb * H * H * Cout : nullptr;
-      pl[l].part = nullptr;  // no split-K schedules in the lane experiment
-      pl[l].part_floats = 0;
+      if (l) {  // each lane its own partial slots and tickets
+        CK(hipMalloc((void**)&pl[l].part, part_floats * sizeof(float)));
+        pl[l].cnt = cnt + cnt_cap;
+      }
     }
   }
   hipEvent_t e0, e1;
@@ -126,8 +137,27 @@ int main(int argc, char** argv) {
   Wino4Params c = p;
   wino4_canvas(c);
   const double exec = 2.0 * 36.0 * c.ntiles * (double)Cin * Cout;
-  printf("B=%d H=%d %d->%d epi=%d lanes=%d: %.1f us (%.1f TF executed)\n", B, H, Cin, Cout, epi, nl, 1e3 * t / iters,
-         exec / (1e-3 * t / iters) / 1e12);
+  // check: the same layer on whole items only (sk_mode 0, one stream) into a second buffer
+  float* y2 = nullptr;
+  CK(hipMalloc((void**)&y2, ny * sizeof(float)));
+  Wino4Params q = p;
+  q.y = y2;
+  q.sk_mode = 0;
+  CK(launch_wino4(q, pre, (Epi)epi, nullptr));
+  CK(hipDeviceSynchronize());
+  std::vector<float> h1(ny), h2(ny);
+  CK(hipMemcpy(h1.data(), y, ny * sizeof(float), hipMemcpyDeviceToHost));
+  CK(hipMemcpy(h2.data(), y2, ny * sizeof(float), hipMemcpyDeviceToHost));
+  double md = 0, mx = 0;
+  size_t ndiff = 0;
+  for (size_t i = 0; i < ny; ++i) {
+    const double d = std::fabs((double)h1[i] - h2[i]);
+    md = std::max(md, d);
+    mx = std::max(mx, (double)std::fabs(h2[i]));
+    ndiff += h1[i] != h2[i];
+  }
+  printf("B=%d H=%d %d->%d epi=%d lanes=%d sk=%d: %.1f us (%.1f TF executed) | vs whole items: max|d| %.3g (max|y| %.3g), %zu differ\n",
+         B, H, Cin, Cout, epi, nl, p.sk_mode, 1e3 * t / iters, exec / (1e-3 * t / iters) / 1e12, md, mx, ndiff);
   if (w4g_after_run) w4g_after_run();  // instrumented variants (w4g_variants.py "stamps") report here
   return 0;
 }
