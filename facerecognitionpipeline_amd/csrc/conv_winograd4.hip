@@ -783,15 +783,18 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
           int last = (int)((t_hi - 1) * P / TTt);
           while (last + 1 < P && lo_of(last + 1) <= t_hi - 1) ++last;
           while (last > 0 && lo_of(last) > t_hi - 1) --last;
+          // (with fewer tail steps than workgroups some ranges are empty: only non-empty ones hold parts)
+          int nparts = 0;
+          for (int c = first; c <= last; ++c) nparts += lo_of(c + 1) > lo_of(c) ? 1 : 0;
+          // hand-off without L2-wide fences (a release here wrote back every dirty line of the
+          // XCD's L2, an acquire invalidated it): the slot stores are device-scope write-through,
+          // so once they have completed (vmcnt) they are visible device-wide before the ticket,
+          // and the last arriver reads the parts with device-scope loads (sc1) after it
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           int ticket = 0;
-          if (lane == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            ticket = __hip_atomic_fetch_add(p.cnt + ti * 4 + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+          if (lane == 0) ticket = __hip_atomic_fetch_add(p.cnt + ti * 4 + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           ticket = __builtin_amdgcn_readfirstlane(ticket);
-          if (ticket != last - first) return;
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          if (ticket != nparts - 1) return;
           if (lane == 0) p.cnt[ti * 4 + w] = 0;  // re-arm for the next launch (zeroed at allocation)
           const f4 sc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
           const f4 sh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
@@ -801,21 +804,47 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) cl[r] = al[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
           }
+          auto ld4c = [&](int off) {  // device-scope (sc1) load of a part
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(sr, off, 0, CPOL_SC1);
+            return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+          };
+          // half the item's 16 pixels at a time, up to three parts' loads in flight per round (the
+          // sums stay in part order: deterministic), the half's residual issued with them
 #pragma unroll
-          for (int i0 = 0; i0 < 16; i0 += 4) {
-            f4 sm[4] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-            for (int c = first; c <= last; ++c) {
-              const int cslot = 2 * c + (lo_of(c) < t_lo ? 1 : 0);
+          for (int h = 0; h < 2; ++h) {
+            f4 sm[8], rv[8];
 #pragma unroll
-              for (int k = 0; k < 4; ++k) sm[k] += ld4(sr, soff(cslot, i0 + k));
+            for (int k = 0; k < 8; ++k) {
+              sm[k] = f4{0.f, 0.f, 0.f, 0.f};
+              if constexpr (DRES) rv[k] = ld4(rr, oo[(8 * h + k) >> 2][(8 * h + k) & 3]);
+            }
+            // the parts' workgroups in order, three at a time (empty ranges skipped)
+            int c = first;
+            while (c <= last) {
+              int cs[3], np3 = 0;
+              for (; c <= last && np3 < 3; ++c)
+                if (lo_of(c + 1) > lo_of(c)) cs[np3++] = c;
+              f4 part[3][8];
+#pragma unroll
+              for (int cc = 0; cc < 3; ++cc) {
+                const int pc = cs[min(cc, max(np3 - 1, 0))];
+                const int cslot = 2 * pc + (lo_of(pc) < t_lo ? 1 : 0);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) part[cc][k] = ld4c(soff(cslot, 8 * h + k));
+              }
+#pragma unroll
+              for (int cc = 0; cc < 3; ++cc)
+                if (cc < np3)
+#pragma unroll
+                  for (int k = 0; k < 8; ++k) sm[k] += part[cc][k];
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int o = oo[(i0 + k) >> 2][(i0 + k) & 3];
+            for (int k = 0; k < 8; ++k) {
+              const int o = oo[(8 * h + k) >> 2][(8 * h + k) & 3];
               f4 v = __builtin_elementwise_fma(sm[k], sc, sh);
               if constexpr (EPI == EPI_AFFINE_PRELU) v = prelu_q(v, al, cl);
               if constexpr (DRES) {
-                v += ld4(rr, o);
+                v += rv[k];
                 if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = prelu_q(v, al, cl);
               }
               const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
@@ -1009,7 +1038,7 @@ bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
 
 hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
   Wino4Params p = p0;
-  if (p.poll_max <= 0) p.poll_max = WINO4_POLL_DEFAULT;
+  p.poll_max = p.poll_max == 0 ? WINO4_POLL_DEFAULT : std::max(p.poll_max, 0);  // < 0: no polls (tests)
   if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
       (pre && !p.pre_t) || (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF ||
       (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) || (long long)NXI * p.Cout * p.Cin * 4 >= (1ll << 31))

@@ -144,7 +144,7 @@ struct Wino4Params {
   // the step it waits for stores FR_DEVERR_W4_HANDOFF into *err (a host-pinned word the
   // runtime reads at its sync points; nullable) and carries on, so a lost hand-off ends the
   // launch instead of hanging the GPU and is reported instead of passing as a result.
-  // poll_max <= 0 means the default (WINO4_POLL_DEFAULT).
+  // poll_max 0 means the default (WINO4_POLL_DEFAULT), < 0 no polls at all (tests).
   int* err;
   int poll_max;
 };

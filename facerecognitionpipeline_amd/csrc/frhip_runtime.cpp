@@ -372,7 +372,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.sk_mode = g_wino4_streamk;
     wp.max_split = g_wino4_max_split;
     wp.err = h->dev_err;
-    wp.poll_max = g_wino4_poll;
+    wp.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     Wino4Params cv = wp;
     wino4_canvas(cv);
     // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
@@ -2018,7 +2018,7 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.Cout = cout;
     p.sk_mode = g_wino4_streamk;
     p.no_split = !g_frt_wino4_split;
-    p.poll_max = g_wino4_poll;
+    p.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     p.err = frt_err;
     if (g_frt_wino4_split || g_wino4_streamk) {  // split-K / stream-K partial slots (64 KiB each) + tail tickets
       p.part_floats = 257ll * 2 * 16 * 16 * 64;
