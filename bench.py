@@ -424,7 +424,7 @@ def main():
         # bf16x3 executes 3 bf16 MFMA products per algorithmic f32 product: its executed fraction is
         # taken against the dense bf16 MFMA peak
         peak, mult = (FP32_MFMA_PEAK_TFLOPS, 1.0) if args.precision == "fp32" else (BF16_MFMA_PEAK_TFLOPS, 3.0)
-        traffic, traffic_src, alg_bytes = None, None, None
+        traffic, traffic_src, alg_bytes, mfma_busy = None, None, None, None
         tj = args.traffic_json
         if tj is None:
             import glob
@@ -437,6 +437,7 @@ def main():
             kj = pj.get("kernels", {}).get(dom, {})
             traffic = kj.get("hbm_bytes_per_launch")
             alg_bytes = kj.get("alg_bytes_per_launch")
+            mfma_busy = kj.get("mfma_busy_frac")
             if traffic is not None:
                 traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
         kernel_name = {"winograd": ("wino4_kernel (Winograd F(4x4,3x3) f32: fused input transform, 16x16x4 "
@@ -456,6 +457,9 @@ def main():
                     # so it is read from the committed profile of the same workload (traffic_source)
                     "traffic": traffic, "traffic_from_profile": traffic is not None,
                     "traffic_source": traffic_src, "alg_bytes_per_launch": alg_bytes,
+                    # PMC SQ_VALU_MFMA_BUSY_CYCLES / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8) of the same kernel in
+                    # the committed profile of this workload (its own rocprofv3 pass, like traffic)
+                    "mfma_busy_frac_from_profile": round(mfma_busy, 4) if mfma_busy is not None else None,
                     "launches": kp["launches"],
                     "flop_per_launch": (kp["exec_flop"] if dom == "winograd" else kp["flop"]) / kp["launches"],
                     "avg_launch_ms": round(kp["ms"] / kp["launches"], 5),
