@@ -20,8 +20,7 @@ for sh in order:
     for v in rows[sh]:
         if v not in vs:
             vs.append(v)
-print(f"{'shape':28s} " + " ".join(f"{v:>16s}" for v in vs) + "   change")
+print(f"{'shape':28s} " + " ".join(f"{v:>18s}" for v in vs) + "   (change vs the first)")
 for sh in order:
     med = [statistics.median(rows[sh][v]) for v in vs]
-    print(f"{sh:28s} " + " ".join(f"{x:10.1f} (n={len(rows[sh][v])})" for x, v in zip(med, vs))
-          + f"   {100 * (med[-1] / med[0] - 1):+.1f}%")
+    print(f"{sh:28s} " + " ".join(f"{x:9.1f} {100 * (x / med[0] - 1):+6.1f}%  " for x in med))
