@@ -1,0 +1,152 @@
+// Stride-2 3x3 conv of the first stage-1 block, Conv2d(64, 64, 3, stride 2, pad 1) + BN + the
+// MaxPool2d(1, 2) shortcut (net.BasicBlockIR res_layer[4] + shortcut_layer of an AdaFace unit whose
+// width does not change, reached through `self.model(batch)`, face_embedder.py:157), NHWC f32, on
+// v_mfma_f32_16x16x4_f32, as a band kernel.
+//
+// Why a kernel of its own: on the implicit-GEMM kernel this layer (N = 64 output channels, input
+// streamed from HBM at stride 2) ran at 58% of the fp32 MFMA peak -- each 32-channel K-step
+// re-gathers its 128 output pixels' taps through L1/L2 and there are only 64 columns to reuse
+// them over.  Here a workgroup owns a BAND of two output rows of one image (112 pixels x 64
+// couts): the five input rows the band's 3x3 windows touch are staged once per 32-channel half in
+// LDS (5 x 113 pixels x 32 channels, pixel pitch 36 floats: 16-byte aligned, and a stride-2 gather
+// of 16 pixels touches every bank at most twice), and all 9 taps read them from there.
+//   * 4 waves, wave w owns couts 16w .. 16w+15 for all 112 pixels (7 blocks of 16): the weights
+//     are the MFMA's A operand (16 couts x 4 channels per lane fragment, one 16-byte L2 load per
+//     tap and 16 channels), the staged input its B operand (16 pixels x 4 channels: one
+//     ds_read_b128 per pixel block, tap and 16 channels).  A lane's accumulator then holds 4
+//     consecutive couts of one output pixel: one 16-byte store per pixel.
+//   * MFMA e (0..3) of a 16-channel chunk consumes channels 4q + e (q = lane / 16) of both
+//     operands, so each lane reads 4 consecutive channels with one 16-byte access.
+//   * 2 workgroups per CU (79.5 KB of LDS each): while one stages its next half, the other's
+//     MFMAs run.
+// Numerics: exact f32 products, f32 accumulation (MFMA = fmaf chain); only the order of the K
+// sum differs from the direct kernel / the CPU reference.
+#include "frhip_kernels.h"
+
+namespace frhip {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int C = 64;          // input = output channels
+constexpr int HALF = 32;       // channels staged per pass
+constexpr int PITCH = 36;      // LDS floats per staged pixel (32 channels + 4: aligned, 2-way gathers)
+constexpr int ROWPX = 113;     // staged pixels per row (input columns -1 .. 111)
+constexpr int BROWS = 5;       // input rows of a band of 2 output rows
+constexpr int NBLK = 7;        // 16-pixel blocks of a band (2 x 56 output pixels)
+constexpr int BIGOFF = 0x7F000000;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* ptr, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, int off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+}
+
+// grid: B * ceil(Ho / 2) bands; 256 threads.  Wi = input width = 2 * Wo, Wo <= 56.
+__global__ __launch_bounds__(256, 2) void s2c64_kernel(S2Params p) {
+  __shared__ __attribute__((aligned(16))) float band[BROWS * ROWPX * PITCH];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Hi = p.H, Wi = p.W, Ho = p.Ho, Wo = p.Wo;
+  const int nb2 = (Ho + 1) / 2;
+  const int b = blockIdx.x / nb2, oy0 = 2 * (blockIdx.x - b * nb2);
+  const int iy0 = 2 * oy0 - 1;   // first staged input row
+  const int cols = 2 * Wo + 1;   // staged input columns -1 .. 2 Wo - 1
+  const __amdgpu_buffer_rsrc_t xr = rsrc(p.x, (long long)p.B * Hi * Wi * C * 4);
+  const __amdgpu_buffer_rsrc_t wr = rsrc(p.w, (long long)C * 9 * C * 4);
+  const __amdgpu_buffer_rsrc_t rr = rsrc(p.res, (long long)p.B * Hi * Wi * C * 4);
+  const __amdgpu_buffer_rsrc_t yr = rsrc(p.y, (long long)p.B * Ho * Wo * C * 4);
+
+  // the lane's output pixel of each block: band pixel p = 16 blk + (lane & 15) = (row oyl, col ox)
+  // -> staged pixel of tap (0, 0): row 2 oyl, column 2 ox (staged column = input column + 1)
+  const int q = lane >> 4;
+  int pbase[NBLK];
+#pragma unroll
+  for (int k = 0; k < NBLK; ++k) {
+    const int pp = 16 * k + (lane & 15);
+    const bool valid = pp < 2 * Wo;  // (a band pixel past 2 Wo gathers pixel 0's taps; never stored)
+    const int oyl = valid && pp >= Wo ? 1 : 0, ox = valid ? pp - oyl * Wo : 0;
+    pbase[k] = ((2 * oyl) * ROWPX + 2 * ox) * PITCH + 4 * q;
+  }
+  // weight fragment of (tap, 16-channel chunk ch16): cout 16 w + (lane & 15), channels ch16 + 4 q .. +3
+  const int wrow = ((16 * w + (lane & 15)) * 9) * C * 4 + 16 * q;
+  f4 acc[NBLK];
+#pragma unroll
+  for (int k = 0; k < NBLK; ++k) acc[k] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int h = 0; h < 2; ++h) {
+    if (h) __syncthreads();  // the first half's gathers are done before the band is overwritten
+    // stage input rows iy0 .. iy0 + 4, columns -1 .. 2 Wo - 1, channels 32 h .. 32 h + 31 (zero
+    // outside the image: the conv's padding; out-of-range buffer offsets read 0)
+    for (int i = tid; i < BROWS * cols * (HALF / 4); i += 256) {
+      const int c4 = i & 7, px = i >> 3;
+      const int r = px / cols, cx = px - r * cols;
+      const int iy = iy0 + r, ix = cx - 1;
+      const bool in = (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi;
+      const int off = in ? (((b * Hi + iy) * Wi + ix) * C + HALF * h + 4 * c4) * 4 : BIGOFF;
+      *reinterpret_cast<f4*>(band + (r * ROWPX + cx) * PITCH + 4 * c4) = ld4(xr, off);
+    }
+    __syncthreads();
+    // 9 taps x 2 chunks of 16 channels; the next step's weight fragment is in flight
+    f4 wf = ld4(wr, wrow + (HALF * h) * 4);
+#pragma unroll
+    for (int t = 0; t < 18; ++t) {
+      const int tap = t >> 1, c16 = t & 1, ky = tap / 3, kx = tap - 3 * ky;
+      const f4 a = wf;
+      if (t + 1 < 18) {
+        const int tn = (t + 1) >> 1, cn = (t + 1) & 1;
+        wf = ld4(wr, wrow + (tn * C + HALF * h + 16 * cn) * 4);
+      }
+      const int toff = (ky * ROWPX + kx) * PITCH + 16 * c16;
+      f4 bv[NBLK];
+#pragma unroll
+      for (int k = 0; k < NBLK; ++k) bv[k] = *reinterpret_cast<const f4*>(band + pbase[k] + toff);
+      // channel e of every block before channel e + 1: consecutive MFMAs never chain on one
+      // accumulator (a 16x16x4 f32 result is not ready for the next MFMA at issue rate)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int k = 0; k < NBLK; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], bv[k][e], acc[k], 0, 0, 0);
+    }
+  }
+  // epilogue: lane holds couts 16 w + 4 q .. +3 of band pixel 16 blk + (lane & 15)
+  const int co = 16 * w + 4 * q;
+  const f4 sc = *reinterpret_cast<const f4*>(p.post_scale + co);
+  const f4 sh = *reinterpret_cast<const f4*>(p.post_shift + co);
+#pragma unroll
+  for (int k = 0; k < NBLK; ++k) {
+    const int pp = 16 * k + (lane & 15);
+    const int oyl = pp >= Wo ? 1 : 0, ox = pp - oyl * Wo, oy = oy0 + oyl;
+    const bool in = pp < 2 * Wo && oy < Ho;
+    // y = BN(conv) + x[b, 2 oy, 2 ox] (MaxPool2d(1, 2) of the block input)
+    const int ro = in ? (((b * Hi + 2 * oy) * Wi + 2 * ox) * C + co) * 4 : BIGOFF;
+    const int yo = in ? (((b * Ho + oy) * Wo + ox) * C + co) * 4 : BIGOFF;
+    f4 v = acc[k] * sc + sh;
+    v += ld4(rr, ro);
+    const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(bits, yr, yo, 0, 0);
+  }
+}
+
+}  // namespace
+
+bool s2c64_supported(int Cin, int Cout, int kh, int kw, int stride, int pad, int H, int W) {
+  return Cin == C && Cout == C && kh == 3 && kw == 3 && stride == 2 && pad == 1 && H % 2 == 0 && W % 2 == 0 &&
+         W / 2 <= 56 && W / 2 >= 8;
+}
+
+hipError_t launch_s2c64(const S2Params& p0, hipStream_t s) {
+  S2Params p = p0;
+  if (!s2c64_supported(C, C, 3, 3, 2, 1, p.H, p.W) || p.B < 1 || !p.x || !p.w || !p.y || !p.res ||
+      !p.post_scale || !p.post_shift || (long long)p.B * p.H * p.W * C * 4 >= BIGOFF)
+    return hipErrorInvalidValue;
+  p.Ho = p.H / 2;
+  p.Wo = p.W / 2;
+  hipLaunchKernelGGL(s2c64_kernel, dim3(p.B * ((p.Ho + 1) / 2)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace frhip

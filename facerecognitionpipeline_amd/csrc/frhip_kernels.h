@@ -151,6 +151,22 @@ struct Wino4Params {
 constexpr int WINO4_POLL_DEFAULT = 1 << 16;
 constexpr int FR_DEVERR_W4_HANDOFF = 1;
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16
+
+// Stride-2 3x3 conv, 64 -> 64 channels, + BN + MaxPool2d(1,2) shortcut (conv_s2.hip): the first
+// block of the AdaFace stage 1.  y[b][oy][ox] = conv(x)*scale + shift + res[b][2oy][2ox], NHWC f32;
+// w [64][3][3][64]; res has x's shape.
+struct S2Params {
+  const float* x;
+  const float* w;
+  const float* post_scale;
+  const float* post_shift;
+  const float* res;
+  float* y;
+  int B, H, W;  // input
+  int Ho, Wo;   // set by launch_s2c64
+};
+bool s2c64_supported(int Cin, int Cout, int kh, int kw, int stride, int pad, int H, int W);
+hipError_t launch_s2c64(const S2Params& p, hipStream_t s);
 size_t wino4_weight_floats(int Cout, int Cin);
 void wino4_canvas(Wino4Params& p);
 // w: [Cout][3][3][Cin] -> u = G (w * pre_scale[cin]) G^T in fragment order (pre_scale nullable)

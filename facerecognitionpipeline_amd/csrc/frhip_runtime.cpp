@@ -288,6 +288,9 @@ struct ProfScope {
 static int g_wino4_streamk = 0;
 // cap on the F(4x4) split-K parts of small grids (frt_set_wino4_max_split: serving sweeps); 0 = none
 static int g_wino4_max_split = 0;
+// the stage-1 stride-2 conv2 on its band kernel (frt_set_s2_band: tests compare it with the
+// implicit-GEMM kernel)
+static int g_s2band = 1;
 // poll bound of wino4_kernel's ring hand-off waits (frt_set_wino4_poll_limit: tests force expiry)
 static int g_wino4_poll = WINO4_POLL_DEFAULT;
 
@@ -405,6 +408,27 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
     hipError_t e = launch_wino(wp, cw.pre_scale != nullptr, epi, s);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd launch: ") + hipGetErrorString(e));
+    return FR_OK;
+  }
+  // the stage-1 stride-2 conv2 + MaxPool shortcut (64 -> 64 channels) of a batch of >= 16 crops on
+  // its band kernel (conv_s2.hip: input rows staged once in LDS for all 9 taps); serving batches
+  // keep the split-K direct path below, which spreads a few images' work over every CU
+  if (g_s2band && !h->detector && h->prec == PREC_F32 && epi == EPI_AFFINE_RES_SUB && !cw.pre_scale && cw.cin2 == 0 &&
+      nsplit == 1 && B >= 16 && res_H == H && res_W == W &&
+      s2c64_supported(cw.cin, cw.cout, cw.kh, cw.kw, cw.stride, cw.pad, H, W)) {
+    S2Params sp{};
+    sp.x = x;
+    sp.w = cw.w;
+    sp.post_scale = cw.post_scale;
+    sp.post_shift = cw.post_shift;
+    sp.res = res;
+    sp.y = y;
+    sp.B = B;
+    sp.H = H;
+    sp.W = W;
+    ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
+    const hipError_t e = launch_s2c64(sp, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("stride-2 band conv launch: ") + hipGetErrorString(e));
     return FR_OK;
   }
   // Round-2 sweep with loads two K-steps ahead on the <= 32-accumulator tiles
@@ -1958,6 +1982,28 @@ int frt_set_wino4_streamk(int on) {
 }
 int frt_set_wino4_max_split(int s) {
   g_wino4_max_split = s < 0 ? 0 : s;
+  return FR_OK;
+}
+int frt_conv2d_s2band(const float* x, const float* w, float* y, int B, int H, int W, const float* post_scale,
+                      const float* post_shift, const float* res, void* stream) {
+  if (!s2c64_supported(64, 64, 3, 3, 2, 1, H, W) || B < 1)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_s2band: 64 -> 64 channels, even H, W <= 112");
+  S2Params sp{};
+  sp.x = x;
+  sp.w = w;
+  sp.post_scale = post_scale;
+  sp.post_shift = post_shift;
+  sp.res = res;
+  sp.y = y;
+  sp.B = B;
+  sp.H = H;
+  sp.W = W;
+  const hipError_t e = launch_s2c64(sp, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_s2band: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+int frt_set_s2_band(int on) {
+  g_s2band = on != 0;
   return FR_OK;
 }
 int frt_set_wino4_poll_limit(int n) {

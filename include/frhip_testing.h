@@ -55,6 +55,15 @@ int frt_set_wino4_max_split(int s);
  * after their sync, the asynchronous calls at their next entry -- and frt_conv2d_winograd4 after
  * its sync.  Applies to launches issued after the call (captured graphs keep theirs). */
 int frt_set_wino4_poll_limit(int n);
+/* The stage-1 stride-2 conv2 (64 -> 64, MaxPool2d(1,2) shortcut) of batches >= 16 on its band
+ * kernel (conv_s2.hip, on = 1, default) or on the implicit-GEMM kernel (0).  Handles issue the
+ * choice at launch time; graphs captured before the call keep theirs. */
+int frt_set_s2_band(int on);
+/* The band kernel alone: y [B][H/2][W/2][64] = conv3x3 s2 p1 (x [B][H][W][64], w [64][3][3][64])
+ * * post_scale + post_shift + res[b][2oy][2ox] (res [B][H][W][64]); even H, W in [16, 112].
+ * Asynchronous on stream. */
+int frt_conv2d_s2band(const float* x, const float* w, float* y, int B, int H, int W, const float* post_scale,
+                      const float* post_shift, const float* res, void* stream);
 /* Handle h runs the stride-2 conv2 of a block with a conv shortcut and that shortcut as one
  * GEMM (on = 1, default: BN scales folded into the weights, extra K-steps over the block input)
  * or as two launches (0).  Drops captured graphs. */

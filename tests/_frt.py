@@ -26,6 +26,10 @@ def lib():
         L.frt_set_wino4_max_split.argtypes = [_I]
         L.frt_set_wino4_poll_limit.restype = _I
         L.frt_set_wino4_poll_limit.argtypes = [_I]
+        L.frt_set_s2_band.restype = _I
+        L.frt_set_s2_band.argtypes = [_I]
+        L.frt_conv2d_s2band.restype = _I
+        L.frt_conv2d_s2band.argtypes = [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P]
         L.frt_set_fuse_shortcut.restype = _I
         L.frt_set_fuse_shortcut.argtypes = [_P, _I]
         L.frt_stem.restype = _I
@@ -100,3 +104,12 @@ def detector_forward(handle, frames):
         out.append(heads[off:off + n * h * w * 32].view(n, h, w, 32))
         off += n * h * w * 32
     return out, canvas
+
+
+def conv2d_s2band(x, w, B, H, W, post, res):
+    """The stage-1 stride-2 band conv: x, res NHWC [B,H,W,64] cuda f32, w [64][3][3][64]."""
+    y = torch.full((B, H // 2, W // 2, 64), float("nan"), device=x.device)
+    rc = lib().frt_conv2d_s2band(_p(x), _p(w), _p(y), B, H, W, _p(post[0]), _p(post[1]), _p(res),
+                                 torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc)
+    return y

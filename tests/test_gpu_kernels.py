@@ -86,6 +86,24 @@ def test_conv2_stride2_maxpool_shortcut():
     _close(got, ref)
 
 
+@pytest.mark.parametrize("B,H", [(2, 112), (3, 56), (1, 16), (17, 30)])
+def test_conv2_stride2_maxpool_band_kernel(B, H):
+    """The stage-1 stride-2 conv2 on its band kernel (conv_s2.hip): two output rows per workgroup,
+    input rows staged in LDS for the 9 taps.  Against PyTorch CPU at the direct kernel's bar, incl.
+    an odd output-row count (H = 30: a last band of one row) and an image of a single band."""
+    seed = 80 + H
+    x = _rand(B, 64, H, H, seed=seed)
+    w = _rand(64, 64, 3, 3, seed=seed + 1) / (64 * 9) ** 0.5
+    post_s, post_b = _rand(64, seed=seed + 4, lo=0.5, hi=1.5), _rand(64, seed=seed + 5, lo=-0.2, hi=0.2)
+    ref = F.conv2d(x, w, stride=2, padding=1) * post_s.view(1, -1, 1, 1) + post_b.view(1, -1, 1, 1)
+    ref = ref + x[:, :, ::2, ::2]
+    xd = _nhwc(x).to(DEV)
+    got = _frt.conv2d_s2band(xd, w.permute(0, 2, 3, 1).contiguous().to(DEV), B, H, H,
+                             (post_s.to(DEV), post_b.to(DEV)), xd)
+    torch.cuda.synchronize()
+    _close(got.cpu(), _nhwc(ref))
+
+
 def test_conv2_identity_residual_tile0():
     got, ref = _conv_case(2, 12, 64, 64, 3, 1, 1, epi=2, tile=0, use_pre=False, seed=35)
     _close(got, ref)

@@ -320,3 +320,21 @@ def test_fused_shortcut_matches_two_launches(arch_embedder):
         assert L.frt_set_fuse_shortcut(emb.model.h, 1) == 0
     assert (fused - two).abs().max().item() <= EMB_TOL
     assert torch.equal(emb.embed_tensor(crops), fused)
+
+
+def test_stride2_band_kernel_matches_implicit_gemm(arch_embedder):
+    """The stage-1 stride-2 conv2 (MaxPool2d(1,2) shortcut) of batches >= 16 runs on its band
+    kernel (conv_s2.hip); the whole network must agree with the implicit-GEMM form of that layer
+    within the embedding bar, and be run-to-run deterministic."""
+    from tests import _frt
+    _arch, emb = arch_embedder
+    crops = torch.from_numpy(W.synthetic_crops(24, seed=W.CROP_SEED_GALLERY)).cuda()
+    L = _frt.lib()
+    band = emb.embed_tensor(crops).clone()
+    assert L.frt_set_s2_band(0) == 0
+    try:
+        gemm = emb.embed_tensor(crops).clone()
+    finally:
+        assert L.frt_set_s2_band(1) == 0
+    assert (band - gemm).abs().max().item() <= EMB_TOL
+    assert torch.equal(emb.embed_tensor(crops), band)
