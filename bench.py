@@ -244,8 +244,18 @@ def launch_ranks(args) -> int:
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
-                                      start_new_session=True))
+        # same process group as this launcher: a signal to the group (a driver's timeout) reaches the
+        # ranks too, and SIGTERM / SIGINT to the launcher alone is forwarded below
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+
+    def forward(signum, _frame):
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(signum)
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
     rc = 0
     try:
         pending = list(procs)
@@ -259,12 +269,14 @@ def launch_ranks(args) -> int:
                     rc = code if code > 0 else 128 - code
                     # a dead rank leaves the others blocked in a collective: end them
                     for q in pending:
-                        os.killpg(q.pid, signal.SIGTERM)
+                        q.terminate()
             time.sleep(0.05)
     except BaseException:
         for q in procs:
             if q.poll() is None:
-                os.killpg(q.pid, signal.SIGKILL)
+                q.kill()
+        for q in procs:
+            q.wait()
         raise
     return rc
 
