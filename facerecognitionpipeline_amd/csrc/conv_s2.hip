@@ -17,10 +17,12 @@
 //     consecutive couts of one output pixel: one 16-byte store per pixel.
 //   * MFMA e (0..3) of a 16-channel chunk consumes channels 4q + e (q = lane / 16) of both
 //     operands, so each lane reads 4 consecutive channels with one 16-byte access.
-//   * 2 workgroups per CU (79.5 KB of LDS each): while one stages its next half, the other's
-//     MFMAs run.
+//   * persistent, 2 workgroups per CU (79.5 KB of LDS each); the next half's input is fetched into
+//     registers while this half's MFMAs run.
 // Numerics: exact f32 products, f32 accumulation (MFMA = fmaf chain); only the order of the K
 // sum differs from the direct kernel / the CPU reference.
+#include <algorithm>
+
 #include "frhip_kernels.h"
 
 namespace frhip {
@@ -45,16 +47,20 @@ __device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, int off) {
   return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
 }
 
-// grid: B * ceil(Ho / 2) bands; 256 threads.  Wi = input width = 2 * Wo, Wo <= 56.
+constexpr int NSTG = (BROWS * ROWPX * (HALF / 4) + 255) / 256;  // staged float4 per thread and half
+
+// Persistent: workgroup g takes bands g, g + gridDim.x, ... (band = 2 output rows of one image).
+// Per band and 32-channel half: the NEXT half's (or band's) input is fetched into registers, one
+// float4 per MFMA step, while this half's MFMAs run, and written to LDS between two barriers when
+// they are done.  Buffer loads retire in issue order (one vmcnt), so each step's weight fragment
+// is issued two steps ahead and BEFORE that step's staging load.  256 threads.
 __global__ __launch_bounds__(256, 2) void s2c64_kernel(S2Params p) {
   __shared__ __attribute__((aligned(16))) float band[BROWS * ROWPX * PITCH];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Hi = p.H, Wi = p.W, Ho = p.Ho, Wo = p.Wo;
-  const int nb2 = (Ho + 1) / 2;
-  const int b = blockIdx.x / nb2, oy0 = 2 * (blockIdx.x - b * nb2);
-  const int iy0 = 2 * oy0 - 1;   // first staged input row
-  const int cols = 2 * Wo + 1;   // staged input columns -1 .. 2 Wo - 1
+  const int nb2 = (Ho + 1) / 2, nbands = p.B * nb2;
+  const int cols = 2 * Wo + 1;  // staged input columns -1 .. 2 Wo - 1
   const __amdgpu_buffer_rsrc_t xr = rsrc(p.x, (long long)p.B * Hi * Wi * C * 4);
   const __amdgpu_buffer_rsrc_t wr = rsrc(p.w, (long long)C * 9 * C * 4);
   const __amdgpu_buffer_rsrc_t rr = rsrc(p.res, (long long)p.B * Hi * Wi * C * 4);
@@ -71,63 +77,102 @@ __global__ __launch_bounds__(256, 2) void s2c64_kernel(S2Params p) {
     const int oyl = valid && pp >= Wo ? 1 : 0, ox = valid ? pp - oyl * Wo : 0;
     pbase[k] = ((2 * oyl) * ROWPX + 2 * ox) * PITCH + 4 * q;
   }
-  // weight fragment of (tap, 16-channel chunk ch16): cout 16 w + (lane & 15), channels ch16 + 4 q .. +3
+  // weight fragment of (tap, 16-channel chunk): cout 16 w + (lane & 15), channels chunk + 4 q .. +3
   const int wrow = ((16 * w + (lane & 15)) * 9) * C * 4 + 16 * q;
-  f4 acc[NBLK];
-#pragma unroll
-  for (int k = 0; k < NBLK; ++k) acc[k] = f4{0.f, 0.f, 0.f, 0.f};
 
-  for (int h = 0; h < 2; ++h) {
-    if (h) __syncthreads();  // the first half's gathers are done before the band is overwritten
-    // stage input rows iy0 .. iy0 + 4, columns -1 .. 2 Wo - 1, channels 32 h .. 32 h + 31 (zero
-    // outside the image: the conv's padding; out-of-range buffer offsets read 0)
-    for (int i = tid; i < BROWS * cols * (HALF / 4); i += 256) {
-      const int c4 = i & 7, px = i >> 3;
-      const int r = px / cols, cx = px - r * cols;
-      const int iy = iy0 + r, ix = cx - 1;
-      const bool in = (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi;
-      const int off = in ? (((b * Hi + iy) * Wi + ix) * C + HALF * h + 4 * c4) * 4 : BIGOFF;
-      *reinterpret_cast<f4*>(band + (r * ROWPX + cx) * PITCH + 4 * c4) = ld4(xr, off);
-    }
-    __syncthreads();
-    // 9 taps x 2 chunks of 16 channels; the next step's weight fragment is in flight
-    f4 wf = ld4(wr, wrow + (HALF * h) * 4);
+  // staging of input rows 2 oy0 - 1 .. 2 oy0 + 3, columns -1 .. 2 Wo - 1, channels 32 h .. +31
+  // (zero outside the image -- the conv's padding -- through out-of-range buffer offsets)
+  // per staged float4 u of this thread, band-independent and packed so that the per-band
+  // address math stays 18 registers:  bits 0..17 byte offset of (row r, staged column cx, c4)
+  // relative to the band's row -1 / column -1,  bits 18..20 r,  bit 21 valid (inside the staged
+  // window and not the left padding column)
+  int pk[NSTG];
 #pragma unroll
-    for (int t = 0; t < 18; ++t) {
-      const int tap = t >> 1, c16 = t & 1, ky = tap / 3, kx = tap - 3 * ky;
-      const f4 a = wf;
-      if (t + 1 < 18) {
-        const int tn = (t + 1) >> 1, cn = (t + 1) & 1;
-        wf = ld4(wr, wrow + (tn * C + HALF * h + 16 * cn) * 4);
-      }
-      const int toff = (ky * ROWPX + kx) * PITCH + 16 * c16;
-      f4 bv[NBLK];
-#pragma unroll
-      for (int k = 0; k < NBLK; ++k) bv[k] = *reinterpret_cast<const f4*>(band + pbase[k] + toff);
-      // channel e of every block before channel e + 1: consecutive MFMAs never chain on one
-      // accumulator (a 16x16x4 f32 result is not ready for the next MFMA at issue rate)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int k = 0; k < NBLK; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], bv[k][e], acc[k], 0, 0, 0);
-    }
+  for (int u = 0; u < NSTG; ++u) {
+    const int i = tid + 256 * u;
+    const int c4 = i & 7, px = i >> 3;
+    const int r = px / cols, cx = px - r * cols;
+    const bool v = i < BROWS * cols * 8 && cx >= 1;
+    pk[u] = ((r * Wi + cx) * C + 4 * c4) * 4 | r << 18 | (v ? 1 << 21 : 0);
   }
-  // epilogue: lane holds couts 16 w + 4 q .. +3 of band pixel 16 blk + (lane & 15)
-  const int co = 16 * w + 4 * q;
-  const f4 sc = *reinterpret_cast<const f4*>(p.post_scale + co);
-  const f4 sh = *reinterpret_cast<const f4*>(p.post_shift + co);
+  f4 stg[NSTG];
+  // (bi >= nbands: no band left; the load is issued anyway, out of range -- a branch around it
+  // would make the compiler's vmcnt bookkeeping assume the shorter queue and wait on the staging)
+  auto fetch1 = [&](int u, int bi, int h) {
+    int k = pk[u];
+    asm volatile("" : "+v"(k));  // decode per use: keeps LICM from hoisting 18 x 3 decoded values
+    const int b = bi / nb2, iy0 = 4 * (bi - b * nb2) - 1;
+    const int r = (k >> 18) & 7, iy = iy0 + r;
+    const bool in = (k & (1 << 21)) && (unsigned)iy < (unsigned)Hi && bi < nbands;
+    const int base = ((b * Hi + iy0) * Wi - 1) * C * 4 + HALF * h * 4;
+    stg[u] = ld4(xr, in ? base + (k & 0x3FFFF) : BIGOFF);
+  };
+  auto commit = [&]() {
 #pragma unroll
-  for (int k = 0; k < NBLK; ++k) {
-    const int pp = 16 * k + (lane & 15);
-    const int oyl = pp >= Wo ? 1 : 0, ox = pp - oyl * Wo, oy = oy0 + oyl;
-    const bool in = pp < 2 * Wo && oy < Ho;
-    // y = BN(conv) + x[b, 2 oy, 2 ox] (MaxPool2d(1, 2) of the block input)
-    const int ro = in ? (((b * Hi + 2 * oy) * Wi + 2 * ox) * C + co) * 4 : BIGOFF;
-    const int yo = in ? (((b * Ho + oy) * Wo + ox) * C + co) * 4 : BIGOFF;
-    f4 v = acc[k] * sc + sh;
-    v += ld4(rr, ro);
-    const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(bits, yr, yo, 0, 0);
+    for (int u = 0; u < NSTG; ++u) {
+      const int i = tid + 256 * u;
+      if (i < BROWS * cols * 8) {
+        const int c4 = i & 7, px = i >> 3, r = (pk[u] >> 18) & 7;
+        *reinterpret_cast<f4*>(band + (px + r * (ROWPX - cols)) * PITCH + 4 * c4) = stg[u];
+      }
+    }
+  };
+  static_assert(NSTG == 18, "one staged float4 per (tap, 16-channel chunk) step");
+
+  int bi = blockIdx.x;
+#pragma unroll
+  for (int u = 0; u < NSTG; ++u) fetch1(u, bi, 0);
+  for (; bi < nbands; bi += gridDim.x) {
+    const int b = bi / nb2, oy0 = 2 * (bi - b * nb2);
+    f4 acc[NBLK];
+#pragma unroll
+    for (int k = 0; k < NBLK; ++k) acc[k] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();  // every wave is done with the staged half it read last
+      commit();
+      __syncthreads();
+      // the next half (or the next band's first half) to stage
+      const int nbi = h == 0 ? bi : bi + (int)gridDim.x, nh = h ^ 1;
+      auto wload = [&](int t) { return ld4(wr, wrow + ((t >> 1) * C + HALF * h + 16 * (t & 1)) * 4); };
+      f4 wf[18];
+      wf[0] = wload(0);
+      wf[1] = wload(1);
+#pragma unroll
+      for (int t = 0; t < 18; ++t) {
+        // issue order per step: weights of step t + 2, then one float4 of the next staging.  A
+        // wait for step t's weights then covers only staging loads issued >= 2 steps earlier.
+        if (t + 2 < 18) wf[t + 2] = wload(t + 2);
+        fetch1(t, nbi, nh);
+        const int tap = t >> 1, c16 = t & 1, ky = tap / 3, kx = tap - 3 * ky;
+        const int toff = (ky * ROWPX + kx) * PITCH + 16 * c16;
+        f4 bv[NBLK];
+#pragma unroll
+        for (int k = 0; k < NBLK; ++k) bv[k] = *reinterpret_cast<const f4*>(band + pbase[k] + toff);
+        // channel e of every block before channel e + 1: consecutive MFMAs never chain on one
+        // accumulator (a 16x16x4 f32 result is not ready for the next MFMA at issue rate)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int k = 0; k < NBLK; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[t][e], bv[k][e], acc[k], 0, 0, 0);
+      }
+    }
+    // epilogue: lane holds couts 16 w + 4 q .. +3 of band pixel 16 blk + (lane & 15)
+    const int co = 16 * w + 4 * q;
+    const f4 sc = *reinterpret_cast<const f4*>(p.post_scale + co);
+    const f4 sh = *reinterpret_cast<const f4*>(p.post_shift + co);
+#pragma unroll
+    for (int k = 0; k < NBLK; ++k) {
+      const int pp = 16 * k + (lane & 15);
+      const int oyl = pp >= Wo ? 1 : 0, ox = pp - oyl * Wo, oy = oy0 + oyl;
+      const bool in = pp < 2 * Wo && oy < Ho;
+      // y = BN(conv) + x[b, 2 oy, 2 ox] (MaxPool2d(1, 2) of the block input)
+      const int ro = in ? (((b * Hi + 2 * oy) * Wi + 2 * ox) * C + co) * 4 : BIGOFF;
+      const int yo = in ? (((b * Ho + oy) * Wo + ox) * C + co) * 4 : BIGOFF;
+      f4 v = acc[k] * sc + sh;
+      v += ld4(rr, ro);
+      const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+      __builtin_amdgcn_raw_buffer_store_b128(bits, yr, yo, 0, 0);
+    }
   }
 }
 
@@ -145,7 +190,11 @@ hipError_t launch_s2c64(const S2Params& p0, hipStream_t s) {
     return hipErrorInvalidValue;
   p.Ho = p.H / 2;
   p.Wo = p.W / 2;
-  hipLaunchKernelGGL(s2c64_kernel, dim3(p.B * ((p.Ho + 1) / 2)), dim3(256), 0, s, p);
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (cus <= 0) cus = 256;
+  const int nbands = p.B * ((p.Ho + 1) / 2);
+  hipLaunchKernelGGL(s2c64_kernel, dim3(std::min(nbands, 2 * cus)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
