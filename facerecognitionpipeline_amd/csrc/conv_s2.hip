@@ -47,6 +47,10 @@ __device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, int off) {
   return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
 }
 
+#ifndef S2_WLEAD
+#define S2_WLEAD 4
+#endif
+constexpr int WLEAD = S2_WLEAD;  // weight fragments in flight ahead of their step
 constexpr int NSTG = (BROWS * ROWPX * (HALF / 4) + 255) / 256;  // staged float4 per thread and half
 
 // Persistent: workgroup g takes bands g, g + gridDim.x, ... (band = 2 output rows of one image).
@@ -119,6 +123,16 @@ __global__ __launch_bounds__(256, 2) void s2c64_kernel(S2Params p) {
   };
   static_assert(NSTG == 18, "one staged float4 per (tap, 16-channel chunk) step");
 
+  // weight fragment of step s (0..35 = half, tap, 16-channel chunk); the same for every band, so
+  // one ring runs across halves and bands, WLEAD steps ahead
+  auto wload = [&](int s) {
+    const int h = s / 18, t = s - 18 * h;
+    return ld4(wr, wrow + ((t >> 1) * C + HALF * h + 16 * (t & 1)) * 4);
+  };
+  f4 wf[36];
+#pragma unroll
+  for (int s = 0; s < WLEAD; ++s) wf[s] = wload(s);
+
   int bi = blockIdx.x;
 #pragma unroll
   for (int u = 0; u < NSTG; ++u) fetch1(u, bi, 0);
@@ -127,33 +141,41 @@ __global__ __launch_bounds__(256, 2) void s2c64_kernel(S2Params p) {
     f4 acc[NBLK];
 #pragma unroll
     for (int k = 0; k < NBLK; ++k) acc[k] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
     for (int h = 0; h < 2; ++h) {
       __syncthreads();  // every wave is done with the staged half it read last
       commit();
       __syncthreads();
       // the next half (or the next band's first half) to stage
       const int nbi = h == 0 ? bi : bi + (int)gridDim.x, nh = h ^ 1;
-      auto wload = [&](int t) { return ld4(wr, wrow + ((t >> 1) * C + HALF * h + 16 * (t & 1)) * 4); };
-      f4 wf[18];
-      wf[0] = wload(0);
-      wf[1] = wload(1);
+      auto toff = [](int t) {
+        const int tap = t >> 1, c16 = t & 1, ky = tap / 3, kx = tap - 3 * ky;
+        return (ky * ROWPX + kx) * PITCH + 16 * c16;
+      };
+      f4 bv[NBLK];
+#pragma unroll
+      for (int k = 0; k < NBLK; ++k) bv[k] = *reinterpret_cast<const f4*>(band + pbase[k] + toff(0));
 #pragma unroll
       for (int t = 0; t < 18; ++t) {
-        // issue order per step: weights of step t + 2, then one float4 of the next staging.  A
-        // wait for step t's weights then covers only staging loads issued >= 2 steps earlier.
-        if (t + 2 < 18) wf[t + 2] = wload(t + 2);
+        // issue order per step: the weights of step s + WLEAD, then one float4 of the next
+        // staging; waiting for step s's weights then covers only staging loads issued at least
+        // WLEAD steps earlier
+        const int s = 18 * h + t;
+        wf[(s + WLEAD) % 36] = wload((s + WLEAD) % 36);
         fetch1(t, nbi, nh);
-        const int tap = t >> 1, c16 = t & 1, ky = tap / 3, kx = tap - 3 * ky;
-        const int toff = (ky * ROWPX + kx) * PITCH + 16 * c16;
-        f4 bv[NBLK];
-#pragma unroll
-        for (int k = 0; k < NBLK; ++k) bv[k] = *reinterpret_cast<const f4*>(band + pbase[k] + toff);
         // channel e of every block before channel e + 1: consecutive MFMAs never chain on one
-        // accumulator (a 16x16x4 f32 result is not ready for the next MFMA at issue rate)
+        // accumulator (a 16x16x4 f32 result is not ready for the next MFMA at issue rate).  A
+        // block's fragment of step t + 1 is read from LDS right after its last MFMA of step t,
+        // so the read's latency hides behind the step's remaining MFMAs, not at the step's start.
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 3; ++e)
 #pragma unroll
-          for (int k = 0; k < NBLK; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[t][e], bv[k][e], acc[k], 0, 0, 0);
+          for (int k = 0; k < NBLK; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[s][e], bv[k][e], acc[k], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < NBLK; ++k) {
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[s][3], bv[k][3], acc[k], 0, 0, 0);
+          if (t + 1 < 18) bv[k] = *reinterpret_cast<const f4*>(band + pbase[k] + toff(t + 1));
+        }
       }
     }
     // epilogue: lane holds couts 16 w + 4 q .. +3 of band pixel 16 blk + (lane & 15)
