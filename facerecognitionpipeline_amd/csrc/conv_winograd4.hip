@@ -280,29 +280,34 @@ __device__ __forceinline__ Item item_of(const Wino4Params& p, int gi) {
 // (tail) items' K-steps cut into equal contiguous ranges, one per workgroup.  An item cut by the
 // ranges leaves one raw partial per workgroup that worked on it; the last-arriving wave (a ticket
 // per item and MFMA wave) sums them in workgroup order and finishes the item in this launch.
-template <bool PRE, int EPI, int MODE>
-__global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
+// The kernel body, for wino4_kernel (bid, nblk = blockIdx.x, gridDim.x) and for the layers of
+// wino4_chain_kernel (CH: the input patches are loaded device-coherent, sc1, since earlier layers
+// of the same launch wrote them from other CUs).  ring: the workgroup's LDS (W4_LDS_FLOATS).
+constexpr int W4_LDS_FLOATS = NBUF * VSTEP + NGEO * FT * 8 + 8 + 2 * MAXSEG;
+template <bool PRE, int EPI, int MODE, bool CH>
+__device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, const int bid, const int nblk) {
   constexpr bool SPLIT = MODE == 1, SK = MODE == 2;
-  __shared__ __attribute__((aligned(16))) float ring[NBUF * VSTEP + NGEO * FT * 8 + 8 + 2 * MAXSEG];
+  constexpr int XPOL = CH ? CPOL_SC1 : 0;
+  __builtin_assume(bid >= 0 && bid < nblk && nblk <= 65535);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout;
   const int KST = Cin / KC;                       // K-steps of the whole reduction
   const int KS = SPLIT ? p.ks_per : KST;          // stream steps per item
   const int nitems = p.nitem * p.ksplit;
-  // MODE 0/1: this workgroup's items are blockIdx.x, blockIdx.x + gridDim.x, ... of the
+  // MODE 0/1: this workgroup's items are bid, bid + nblk, ... of the
   // XCD-remapped order (item_at(j), j local).  SK: segments j < sk_dp are the whole items
-  // blockIdx.x + j * gridDim.x of the XCD-remapped order of the first D = sk_dp * gridDim.x
+  // bid + j * nblk of the XCD-remapped order of the first D = sk_dp * nblk
   // items; then it owns the tail item-steps [u_lo, u_hi) of the (nT - D) * KST space (its logical
   // index XCD-remapped, so an XCD's workgroups hold one contiguous run of tail items): segment
   // sk_dp + i is tail item tt_first + i, the first one from step s_tail0.
-  const int nloc = (nitems - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int nloc = (nitems - bid + nblk - 1) / nblk;
   const int nT = p.mblocks * p.nblocks;
-  const int D = SK ? p.sk_dp * (int)gridDim.x : 0;
+  const int D = SK ? p.sk_dp * nblk : 0;
   const long long TT = SK ? (long long)(nT - D) * KST : 0;  // tail item-steps
-  const int bl = SK ? xcd_remap(blockIdx.x, gridDim.x) : 0;
-  const int u_lo = SK ? (int)((long long)bl * TT / gridDim.x) : 0;
-  const int u_hi = SK ? (int)((long long)(bl + 1) * TT / gridDim.x) : 0;
+  const int bl = SK ? xcd_remap(bid, nblk) : 0;
+  const int u_lo = SK ? (int)((long long)bl * TT / nblk) : 0;
+  const int u_hi = SK ? (int)((long long)(bl + 1) * TT / nblk) : 0;
   const int tt_first = u_lo / KST, s_tail0 = u_lo - tt_first * KST;
   const int nseg = SK ? p.sk_dp + (u_hi > u_lo ? (u_hi - 1) / KST - tt_first + 1 : 0) : nloc;
   const int t_last = nseg - 1;  // last segment
@@ -312,7 +317,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   };
   auto item_at = [&](int j) {
     if (SK) return item_of(p, __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j]));
-    const int t = xcd_remap(blockIdx.x + j * gridDim.x, nitems);
+    const int t = xcd_remap(bid + j * nblk, nitems);
     const int sp = t / p.nitem, li = t - sp * p.nitem;
     Item it = item_of(p, p.item0 + li);
     it.split = sp;
@@ -330,7 +335,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   if (tid < 8) rdy[tid] = 0;
   if (SK && tid < nseg) {
     const int q = tid;
-    segtab[2 * q] = q < p.sk_dp ? xcd_remap(blockIdx.x + q * gridDim.x, D) : D + tt_first + (q - p.sk_dp);
+    segtab[2 * q] = q < p.sk_dp ? xcd_remap(bid + q * nblk, D) : D + tt_first + (q - p.sk_dp);
     segtab[2 * q + 1] = q == p.sk_dp ? s_tail0 : 0;
   }
   __syncthreads();  // the kernel's only workgroup barrier
@@ -415,10 +420,16 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       }
     };
     // a patch buffer: the lane's 6x3 values (2 channels each) and, for PRE, the folded shift
-    // t = shift / scale of its channels at its item's in-image rows (trow) and columns (colm)
+    // t = shift / scale of its channels (tt) with its item's in-image row / column masks (rowm,
+    // colm; the masks are copied because the next item's geometry may replace them before this
+    // patch is stored).  tt is only multiplied in at store time: using it at load time made the
+    // compiler wait for it -- and, loads retiring in order, for the patch loads issued before it --
+    // right after issuing them, so each load() stalled for its own patch's round trip (batch 1:
+    // two serialized round trips before step 0 reached the ring).
     struct Patch {
       f2 d[6][3];
-      f2 trow[6];
+      f2 tt;
+      float rowm[6];
       float colm[3];
     };
     Patch pa, pb, pc;
@@ -438,13 +449,13 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       for (int a = 0; a < 6; ++a)
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);
+          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, XPOL);
           P.d[a][b] = f2{__uint_as_float(v.x), __uint_as_float(v.y)};
         }
       if constexpr (PRE) {
-        const f2 tt = live ? *reinterpret_cast<const f2*>(p.pre_t + step * KC + ch) : f2{0.f, 0.f};
+        P.tt = live ? *reinterpret_cast<const f2*>(p.pre_t + step * KC + ch) : f2{0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 6; ++e) P.trow[e] = tt * rowm[e];
+        for (int e = 0; e < 6; ++e) P.rowm[e] = rowm[e];
 #pragma unroll
         for (int e = 0; e < 3; ++e) P.colm[e] = colm[e];
       }
@@ -465,9 +476,11 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
         // BN(x) = scale (x + t) with the scale folded into U: add t at in-image pixels only,
         // the conv's zero padding and the canvas separators stay 0 (BN -> zero-padded Conv2d)
 #pragma unroll
-        for (int a = 0; a < 6; ++a)
+        for (int a = 0; a < 6; ++a) {
+          const f2 trow = P.tt * P.rowm[a];
 #pragma unroll
-          for (int b = 0; b < 3; ++b) d[a][b] = __builtin_elementwise_fma(P.trow[a], f2{P.colm[b], P.colm[b]}, d[a][b]);
+          for (int b = 0; b < 3; ++b) d[a][b] = __builtin_elementwise_fma(trow, f2{P.colm[b], P.colm[b]}, d[a][b]);
+        }
 #pragma unroll
       for (int b = 0; b < 3; ++b) {  // the lane's columns: d[.][b] <- (B^T d)[.][b]
         f2 c[6], o[6];
@@ -512,6 +525,19 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
       store(P, g);
       lds_publish(rdy + t, lane, g + 1);
     };
+    if (G <= 2) {
+      // one or two K-steps (split-K serving launches): no loads past the stream's end.  The
+      // general loop below issues two extra patch loads ahead; for a stream this short they
+      // only fetch the clamped last item again, and entering that item's geometry waited (a
+      // register of its address arithmetic still had a patch load outstanding) for the patches
+      // already in flight: a round trip before step 0 could reach the ring.
+      load(pa);
+      if (G == 2) load(pb);
+      put(pa, 0);
+      if (G == 2) put(pb, 1);
+      w4_report_handoff(fseen, p.err);
+      return;
+    }
     load(pa);
     load(pb);
     for (int b = 0;; b += 3) {
@@ -772,7 +798,7 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
           // steps [t_lo, t_hi); this wave's ticket (one per item and MFMA wave, G16 counter form)
           // tells whether it arrived last.  The last one sums the parts in workgroup order
           // (independent of the arrival order: deterministic) and finishes the item.
-          const int P = gridDim.x;
+          const int P = nblk;
           const int ti = __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j]) - p.sk_dp * P;  // tail index
           const long long TTt = (long long)(p.mblocks * p.nblocks - p.sk_dp * P) * KST;
           const long long t_lo = (long long)ti * KST, t_hi = t_lo + KST;
@@ -906,14 +932,22 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   w4_report_handoff(rseen, p.err);
 }
 
-// Split-K finish: y = epilogue(sum of an item's raw partial outputs, in part order: deterministic)
-// at the item's in-image pixels.  Thread = (tile n, pixel, cout quad); grid (FT * 16 * FN / 4 /
-// blockDim, items): blockIdx.y is the launch item li with parts in slots li * S .. li * S + S - 1.
-template <int EPI>
-__global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
-  const int gi = p.item0 + blockIdx.y, slot0 = blockIdx.y * p.ksplit, S = p.ksplit;
+template <bool PRE, int EPI, int MODE>
+__global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
+  __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
+  wino4_body<PRE, EPI, MODE, false>(p, ring, blockIdx.x, gridDim.x);
+}
+
+// Split-K finish of one output element group: y = epilogue(sum of an item's raw partial outputs,
+// in part order: deterministic) at the item's in-image pixels.  idx = (tile n, pixel, cout quad)
+// of launch item li, whose parts are in slots li * S .. li * S + S - 1.  CH (wino4_chain_kernel):
+// the parts and the residual were written by other CUs of the same launch, so they are loaded
+// device-coherent (sc1); the arithmetic is the same code either way, so a chained layer's output
+// is bitwise the fixup kernel's.
+template <int EPI, bool CH>
+__device__ __forceinline__ void w4_fixup_elem(const Wino4Params& p, int li, int idx) {
+  const int gi = p.item0 + li, slot0 = li * p.ksplit, S = p.ksplit;
   const Item it = item_of(p, gi);
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = idx >> 8, px = (idx >> 4) & 15, cq = idx & 15;
   const int cout0 = it.nb * FN + 4 * cq;
   const int T = it.mb * FT + n;
@@ -928,6 +962,7 @@ __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
   const long long pix = (long long)(rs * p.NC * H + y) * W + (long long)cs * H * W + x;
   if (pix >= (long long)p.B * H * W) return;
   const float4* slab = reinterpret_cast<const float4*>(p.part);
+  const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
   float v[4] = {0.f, 0.f, 0.f, 0.f};
   // sixteen slot loads in flight at a time (every part of a split-K item: S <= 16 K-steps of
   // 16 channels per part at the serving sizes), summed in part order (deterministic): a loop of
@@ -936,9 +971,15 @@ __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
   for (int s0 = 0; s0 < S; s0 += 16) {
     float4 a[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
-      a[u] = s0 + u < S ? slab[((((long long)slot0 + s0 + u) * FT + n) * 16 + px) * (FN / 4) + cq]
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < 16; ++u) {
+      const long long q = ((((long long)slot0 + s0 + u) * FT + n) * 16 + px) * (FN / 4) + cq;
+      if constexpr (CH) {
+        const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(sr, s0 + u < S ? (int)(q * 16) : BIGOFF, 0, CPOL_SC1);
+        a[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
+      } else {
+        a[u] = s0 + u < S ? slab[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 16; ++u)
       if (s0 + u < S) {
@@ -949,12 +990,26 @@ __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
       }
   }
   const long long yo = pix * p.Cout + cout0;
+  float rv[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) {
+    if constexpr (CH) {
+      const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, p.B * H * W * p.Cout * 4);
+      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(yo * 4), 0, CPOL_SC1);
+      rv[0] = __uint_as_float(w.x);
+      rv[1] = __uint_as_float(w.y);
+      rv[2] = __uint_as_float(w.z);
+      rv[3] = __uint_as_float(w.w);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rv[r] = p.res[yo + r];
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float t = v[r] * p.post_scale[cout0 + r] + p.post_shift[cout0 + r];
     if constexpr (EPI == EPI_AFFINE_PRELU) t = t > 0.f ? t : t * p.prelu[cout0 + r];
     if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) {
-      t += p.res[yo + r];
+      t += rv[r];
       if constexpr (EPI == EPI_AFFINE_RES_PRELU) t = t > 0.f ? t : t * p.prelu[cout0 + r];
     }
     v[r] = t;
@@ -963,6 +1018,91 @@ __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
   const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(p.y, p.B * H * W * p.Cout * 4);
   const u32x4 bits = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
   __builtin_amdgcn_raw_buffer_store_b128(bits, yr, (int)(yo * 4), 0, CPOL_SC1);
+}
+
+// Split-K finish launch: grid (FT * 16 * FN / 4 / blockDim, items), blockIdx.y = launch item.
+template <int EPI>
+__global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
+  w4_fixup_elem<EPI, false>(p, blockIdx.y, blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// ---- Chained split-K layers (serving batches) ------------------------------------------------
+// A run of consecutive F(4x4) layers of an IR stage (conv1: pre-BN + BN + PReLU, conv2: BN +
+// identity residual), each a split-K launch (MODE 1) of at most one round of workgroups, runs as
+// ONE persistent launch: workgroup b computes its split of layer l (the same body as
+// wino4_kernel's, patches loaded device-coherent), stores the raw partial into its slot, waits on
+// its item's arrival counter until all S splits have stored theirs, then finishes slice b of the
+// item's outputs (w4_fixup_elem: the fixup kernel's arithmetic) and counts itself into layer l's
+// counter.  Layer l + 1 starts once layer l's counter has every workgroup of layer l: its patches,
+// and for conv2 the residual two layers back, are complete.  That removes, per layer, the fixup
+// launch and both kernel boundaries (each ~1.5-2 us plus the cold start of a fresh grid).
+//   * Co-residency: the grid is at most one workgroup per CU (LDS 147 KiB each) and the runtime
+//     only chains when nothing else shares the CUs (one lane); every wait is bounded (poll_max),
+//     an expired one is reported like a ring hand-off (FR_DEVERR_W4_HANDOFF) and the launch ends.
+//   * Hand-off form (MI355X_MICROARCH.md, visibility table, first row): every partial / output
+//     store is sc1 (write-through) and drained by its wave (vmcnt(0)) before a workgroup barrier;
+//     one lane then adds to the agent-scope counter; the consumer polls it with sc1 loads and
+//     reads every handed-off byte with sc1 loads, behind a workgroup barrier.
+//   * sync: [0] workgroups finished, [1 + l] layer l's finished workgroups, [cbase_l + li] item
+//     li's stored splits.  The last workgroup to finish zeroes them all for the next launch.
+constexpr int W4CH_EPI_PRE = 0;  // kind: conv1 (PRE, EPI_AFFINE_PRELU)
+__device__ __forceinline__ bool w4_poll_ge(int* c, int target, int poll_max) {
+  int n = 0;
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (++n > poll_max) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(512, 1) void wino4_chain_kernel(const W4Link* __restrict__ links, int nl, int* sync,
+                                                             int ncnt, int* err, int poll_max) {
+  __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
+  __shared__ int last;
+  const int tid = threadIdx.x, bid = blockIdx.x;
+  bool ok = true;
+  for (int l = 0; l < nl; ++l) {
+    const W4Link& L = links[l];
+    const int nwg = L.nwg;
+    if (bid >= nwg) continue;
+    if (l > 0) {  // every workgroup of layer l - 1 has stored its slice of that layer's output
+      if (tid == 0) ok = w4_poll_ge(sync + l, links[l - 1].nwg, poll_max) && ok;
+      __syncthreads();
+    }
+    if (L.kind == W4CH_EPI_PRE)
+      wino4_body<true, EPI_AFFINE_PRELU, 1, true>(L.p, ring, bid, nwg);
+    else
+      wino4_body<false, EPI_AFFINE_RES, 1, true>(L.p, ring, bid, nwg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial-slot stores
+    __syncthreads();
+    const Wino4Params& p = L.p;
+    // this workgroup's (split, item): item_at(0) of the body
+    const int t = xcd_remap(bid, nwg);
+    const int sp = t / p.nitem, li = t - sp * p.nitem, S = p.ksplit;
+    if (tid == 0) {
+      __hip_atomic_fetch_add(sync + L.cbase + li, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = w4_poll_ge(sync + L.cbase + li, S, poll_max) && ok;
+    }
+    __syncthreads();
+    // slice sp of the item's FT * 16 * FN / 4 output groups
+    constexpr int NE = FT * 16 * FN / 4;
+    const int e1 = (sp + 1) * NE / S;
+    for (int e = sp * NE / S + tid; e < e1; e += 512) {
+      if (L.kind == W4CH_EPI_PRE)
+        w4_fixup_elem<EPI_AFFINE_PRELU, true>(p, li, e);
+      else
+        w4_fixup_elem<EPI_AFFINE_RES, true>(p, li, e);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(sync + 1 + l, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // the last workgroup to get here re-arms every counter (all waits of this launch are over)
+  if (tid == 0) last = __hip_atomic_fetch_add(sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (last)
+    for (int i = tid; i < ncnt; i += 512) __hip_atomic_store(sync + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0 && !ok && err) __hip_atomic_store(err, FR_DEVERR_W4_HANDOFF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
@@ -1036,13 +1176,14 @@ bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
   return kh == 3 && kw == 3 && stride == 1 && pad == 1 && Cin % 16 == 0 && Cin >= 16 && Cout % 16 == 0 && Cout >= 16;
 }
 
-hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
-  Wino4Params p = p0;
+namespace {
+// validation + canvas + item blocks of a layer (launch_wino4, wino4_chain_plan)
+bool w4_setup(Wino4Params& p, bool pre) {
   p.poll_max = p.poll_max == 0 ? WINO4_POLL_DEFAULT : std::max(p.poll_max, 0);  // < 0: no polls (tests)
   if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
       (pre && !p.pre_t) || (long long)p.B * p.H * p.W * p.Cin * 4 >= BIGOFF ||
       (long long)p.B * p.H * p.W * p.Cout * 4 >= (1ll << 31) || (long long)NXI * p.Cout * p.Cin * 4 >= (1ll << 31))
-    return hipErrorInvalidValue;
+    return false;
   wino4_canvas(p);
   if (pre && p.NC > 1 && p.B % p.NC && p.Pr == p.H) {
     // a partial last canvas row directly below full ones: give every image row a separator
@@ -1057,35 +1198,73 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   // instead of all of it, for patches read twice (stage 4: 238 -> 232 us, PMC-modelled traffic
   // 677 -> 453 MB per launch)
   p.nbg = std::max(1, std::min(p.mblocks, std::max(32 / p.nblocks, 8)));
+  return true;
+}
+
+constexpr long long SLOT = (long long)FT * 16 * FN;  // floats of one compact partial slot
+
+bool w4_aligned(const Wino4Params& p) {
+  return ((reinterpret_cast<uintptr_t>(p.y) | reinterpret_cast<uintptr_t>(p.res) | reinterpret_cast<uintptr_t>(p.part)) &
+          15) == 0;
+}
+
+int w4_cus() {
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return cus > 0 ? cus : 256;
+}
+
+// K parts for a split-K launch of n items: as many as fit one round of workgroups, bounded by
+// the K-steps and the slot workspace; ks_per steps each
+int w4_split_of(const Wino4Params& p, int n, int cus, int& ks_per) {
+  const int KST = p.Cin / KC;
+  int S = (int)std::min<long long>(std::min(KST, cus / n), p.part_floats / (SLOT * n));
+  // a grid of one-K-step splits over more than half the chip loses to half the grid with two
+  // steps each (half the slots for the fixup to sum): IR-101 batch 4, 2.37 -> 2.18 ms per
+  // embed + match; batch 1 (64 workgroups at stage 3) and batch 8 (two-step splits over the
+  // whole chip; halving them again cost +2.6%) keep theirs
+  if (S * n > cus / 2 && (KST + S - 1) / S < 2) S = std::max(1, std::min(S, (cus / 2) / n));
+  if (p.max_split > 0) S = std::min(S, p.max_split);
+  ks_per = KST;
+  if (S > 1) {
+    ks_per = (KST + S - 1) / S;
+    S = (KST + ks_per - 1) / ks_per;
+  }
+  return std::max(S, 1);
+}
+}  // namespace
+
+bool wino4_chain_plan(Wino4Params& p, bool pre, Epi epi, int cus) {
+  if (!((pre && epi == EPI_AFFINE_PRELU) || (!pre && epi == EPI_AFFINE_RES)) || !w4_setup(p, pre)) return false;
+  const int KST = p.Cin / KC, nT = p.mblocks * p.nblocks;
+  if (!p.part || p.no_split || !w4_aligned(p) || KST < 2 || nT > cus / 2) return false;
+  int ks_per = KST;
+  const int S = w4_split_of(p, nT, cus, ks_per);
+  if (S < 2 || nT * S > cus) return false;
+  p.item0 = 0;
+  p.nitem = nT;
+  p.ksplit = S;
+  p.ks_per = ks_per;
+  return true;
+}
+
+hipError_t launch_wino4_chain(const W4Link* links, int nl, int grid, int* sync, int ncnt, int* err, int poll_max,
+                              hipStream_t s) {
+  if (!links || nl < 1 || grid < 1 || !sync || ncnt < 1 + nl) return hipErrorInvalidValue;
+  poll_max = poll_max == 0 ? WINO4_POLL_DEFAULT : std::max(poll_max, 0);
+  hipLaunchKernelGGL(wino4_chain_kernel, dim3(grid), dim3(512), 0, s, links, nl, sync, ncnt, err, poll_max);
+  return hipGetLastError();
+}
+
+hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
+  Wino4Params p = p0;
+  if (!w4_setup(p, pre)) return hipErrorInvalidValue;
   const int KST = p.Cin / KC;
   const int nT = p.mblocks * p.nblocks;
-  constexpr long long SLOT = (long long)FT * 16 * FN;  // floats of one compact partial slot
-  const bool aligned = ((reinterpret_cast<uintptr_t>(p.y) | reinterpret_cast<uintptr_t>(p.res) |
-                         reinterpret_cast<uintptr_t>(p.part)) & 15) == 0;
-  int cus = 256;
-  {
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
+  const bool aligned = w4_aligned(p);
+  const int cus = w4_cus();
   const bool can_split = p.part && !p.no_split && aligned && KST > 1;
-  // K parts for a split-K launch of n items: as many as fit one round of workgroups, bounded by
-  // the K-steps and the slot workspace; ks_per steps each
-  auto split_of = [&](int n, int& ks_per) {
-    int S = (int)std::min<long long>(std::min(KST, cus / n), p.part_floats / (SLOT * n));
-    // a grid of one-K-step splits over more than half the chip loses to half the grid with two
-    // steps each (half the slots for the fixup to sum): IR-101 batch 4, 2.37 -> 2.18 ms per
-    // embed + match; batch 1 (64 workgroups at stage 3) and batch 8 (two-step splits over the
-    // whole chip; halving them again cost +2.6%) keep theirs
-    if (S * n > cus / 2 && (KST + S - 1) / S < 2) S = std::max(1, std::min(S, (cus / 2) / n));
-    if (p.max_split > 0) S = std::min(S, p.max_split);
-    ks_per = KST;
-    if (S > 1) {
-      ks_per = (KST + S - 1) / S;
-      S = (KST + ks_per - 1) / ks_per;
-    }
-    return std::max(S, 1);
-  };
+  auto split_of = [&](int n, int& ks_per) { return w4_split_of(p, n, cus, ks_per); };
   // stream-K (p.sk_mode): whole items for floor(nT / cus) rounds, then the tail items' K-steps in
   // equal contiguous ranges, one per workgroup, so the part-empty last round of whole items
   // (IR-101 B=256: stage 3 3.52 rounds run as 4, stage 2 6.13 as 7) becomes a fraction of a round;

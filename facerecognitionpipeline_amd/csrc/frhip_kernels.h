@@ -152,6 +152,21 @@ constexpr int WINO4_POLL_DEFAULT = 1 << 16;
 constexpr int FR_DEVERR_W4_HANDOFF = 1;
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16
 
+// One layer of a chained launch (wino4_chain_kernel, conv_winograd4.hip): a split-K (MODE 1)
+// layer planned by wino4_chain_plan.  kind 0: IR conv1 (pre-BN, BN, PReLU), 1: IR conv2 (BN +
+// identity residual).  nwg: its workgroups (items x splits); cbase: its item counters in sync.
+struct W4Link {
+  Wino4Params p;
+  int kind, nwg, cbase, pad_;
+};
+// Plans `p` (pre: conv1 kind) as one layer of a chain: true when it is a split-K launch of at most
+// one round of workgroups on `cus` CUs (the serving sizes); fills the canvas / split fields.
+bool wino4_chain_plan(Wino4Params& p, bool pre, Epi epi, int cus);
+// One launch of nl planned layers (links: device copy), grid = max nwg <= CUs; sync: ncnt
+// zeroed ints (1 + nl + the layers' items), left zeroed by the launch.
+hipError_t launch_wino4_chain(const W4Link* links, int nl, int grid, int* sync, int ncnt, int* err, int poll_max,
+                              hipStream_t s);
+
 // Stride-2 3x3 conv, 64 -> 64 channels, + BN + MaxPool2d(1,2) shortcut (conv_s2.hip): the first
 // block of the AdaFace stage 1.  y[b][oy][ox] = conv(x)*scale + shift + res[b][2oy][2ox], NHWC f32;
 // w [64][3][3][64]; res has x's shape.

@@ -294,9 +294,75 @@ static int g_s2band = 1;
 // poll bound of wino4_kernel's ring hand-off waits (frt_set_wino4_poll_limit: tests force expiry)
 static int g_wino4_poll = WINO4_POLL_DEFAULT;
 
+// Launches the collected chain: its layers' link table (uploaded once per (n, run): a table
+// found with the same contents is reused, so a graph capture of the forward never uploads) and
+// one wino4_chain_kernel launch; a single layer, a table that does not fit the counters, or a
+// capture without an uploaded table launch the layers one by one instead.
+int chain_flush(fr_handle* h, hipStream_t s) {
+  if (h->chain_pending.empty()) return FR_OK;
+  std::vector<W4Link> links;
+  std::vector<Wino4Params> raw;
+  std::vector<bool> pre;
+  links.swap(h->chain_pending);
+  raw.swap(h->chain_raw);
+  pre.swap(h->chain_pre);
+  const int seq = h->chain_seq++;
+  const int nl = (int)links.size();
+  int ncnt = 1 + nl, grid = 0;
+  for (auto& lk : links) {
+    lk.cbase = ncnt;
+    ncnt += lk.p.nitem;
+    grid = std::max(grid, lk.nwg);
+  }
+  W4Link* dev = nullptr;
+  if (nl >= 2 && ncnt <= fr_handle::CHAIN_SYNC_INTS && grid <= h->cus && h->chain_sync) {
+    for (auto& t : h->chain_tabs)
+      if (t.n == h->chain_n && t.seq == seq && t.host.size() == links.size() &&
+          std::memcmp(t.host.data(), links.data(), links.size() * sizeof(W4Link)) == 0)
+        dev = t.dev;
+    if (!dev && !h->capturing) {
+      fr_handle::ChainTab* t = nullptr;
+      for (auto& e : h->chain_tabs)
+        if (e.n == h->chain_n && e.seq == seq) t = &e;
+      if (t && t->host.size() != links.size()) {
+        FR_HIP(h, hipStreamSynchronize(s));  // no launch of this stream still reads the old table
+        FR_HIP(h, hipFree(t->dev));
+        t->dev = nullptr;
+      }
+      if (!t) {
+        h->chain_tabs.push_back({h->chain_n, seq, {}, nullptr});
+        t = &h->chain_tabs.back();
+      }
+      if (!t->dev) FR_HIP(h, hipMalloc((void**)&t->dev, links.size() * sizeof(W4Link)));
+      // stream-ordered: launches queued before this one that read the previous contents finish first
+      FR_HIP(h, hipStreamSynchronize(s));
+      FR_HIP(h, hipMemcpy(t->dev, links.data(), links.size() * sizeof(W4Link), hipMemcpyHostToDevice));
+      t->host = links;
+      dev = t->dev;
+    }
+  }
+  if (dev) {
+    const hipError_t e = launch_wino4_chain(dev, nl, grid, h->chain_sync, ncnt, h->dev_err,
+                                            g_wino4_poll > 0 ? g_wino4_poll : -1, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 chain launch: ") + hipGetErrorString(e));
+    return FR_OK;
+  }
+  for (int l = 0; l < nl; ++l) {
+    const hipError_t e = launch_wino4(raw[l], pre[l], links[l].kind == 0 ? EPI_AFFINE_PRELU : EPI_AFFINE_RES, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
+  }
+  return FR_OK;
+}
+
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
              const LaneWs* L, const float* x2) {
+  // a layer that does not join the chain being collected: the chain goes out first
+  // (the Winograd branch below decides for itself; everything else flushes here)
+  const bool w4_candidate = h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 &&
+                            wino4_supported(cw.cin, cw.cout, cw.kh, cw.kw, cw.stride, cw.pad);
+  if (!w4_candidate)
+    if (int rc = chain_flush(h, s)) return rc;
   float* const sk_ws = L ? L->sk_ws : h->sk_ws;
   int* const sk_cnt = L ? L->sk_cnt : h->sk_cnt;
   float* const w4part = L ? L->w4part : h->w4part;
@@ -376,6 +442,23 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.max_split = g_wino4_max_split;
     wp.err = h->dev_err;
     wp.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
+    // a serving forward's conv1 / conv2: collected into the current chain when it plans as a
+    // one-round split-K launch (the chain launches at the next layer that cannot join it)
+    if (h->chain_collect && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE_RES)) {
+      Wino4Params plan = wp;
+      if (wino4_chain_plan(plan, cw.pre_scale != nullptr, epi, h->cus)) {
+        W4Link lk;
+        std::memset(&lk, 0, sizeof lk);
+        std::memcpy(&lk.p, &plan, sizeof plan);
+        lk.kind = cw.pre_scale != nullptr ? 0 : 1;
+        lk.nwg = plan.nitem * plan.ksplit;
+        h->chain_pending.push_back(lk);
+        h->chain_raw.push_back(wp);
+        h->chain_pre.push_back(cw.pre_scale != nullptr);
+        return FR_OK;
+      }
+    }
+    if (int rc = chain_flush(h, s)) return rc;
     Wino4Params cv = wp;
     wino4_canvas(cv);
     // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
@@ -385,6 +468,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
     return FR_OK;
   }
+  if (int rc = chain_flush(h, s)) return rc;
   // Winograd F(2x2,3x3) for the stride-1 3x3 convs (f32 parity path only)
   if (h->winograd && h->prec == PREC_F32 && cw.wino &&
       ((epi == EPI_AFFINE_PRELU && cw.pre_scale) || (epi == EPI_AFFINE_RES && !cw.pre_scale && res_H == p.Ho))) {
@@ -549,6 +633,21 @@ int ensure_lane(fr_handle* h, int l, int batch) {
 // other lane's launch of the same layer is already queued.
 int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* cnt, int nl, float* out,
                   int normalize, const hipStream_t* st, const LaneWs* L) {
+  // serving forwards (one lane, n <= chain_max_n): chained F(4x4) layers (chain_flush).  Not
+  // under profiling (per-launch events) and never for a second lane: a chained launch assumes its
+  // workgroups have the CUs to themselves.
+  struct ChainScope {
+    fr_handle* h;
+    ~ChainScope() {
+      h->chain_collect = false;
+      h->chain_pending.clear();
+      h->chain_raw.clear();
+      h->chain_pre.clear();
+    }
+  } chain_scope{h};
+  h->chain_collect = nl == 1 && cnt[0] <= h->chain_max_n && !h->prof && h->chain_sync != nullptr && !h->detector;
+  h->chain_seq = 0;
+  h->chain_n = cnt[0];
   for (int l = 0; l < nl; ++l) {
     const int n = cnt[l];
     ProfScope ps(h, st[l], 2.0 * n * 112.0 * 112.0 * 64 * 27, 0);
@@ -587,6 +686,8 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
     cur = nxt;
     HW = Ho;
   }
+  if (int rc = chain_flush(h, st[0])) return rc;
+  h->chain_collect = false;
   for (int l = 0; l < nl; ++l) {
     const int n = cnt[l];
     const long long split_stride = (long long)n * 512;
@@ -1424,6 +1525,8 @@ int fr_finalize(fr_handle* h) {
     FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
     FR_HIP(h, hipMemset(h->w4part + (fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS), 0, fr_handle::W4CNT_INTS * sizeof(int)));
+    FR_HIP(h, hipMalloc((void**)&h->chain_sync, fr_handle::CHAIN_SYNC_INTS * sizeof(int)));
+    FR_HIP(h, hipMemset(h->chain_sync, 0, fr_handle::CHAIN_SYNC_INTS * sizeof(int)));
   }
   if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
@@ -2008,6 +2111,14 @@ int frt_set_s2_band(int on) {
 }
 int frt_set_wino4_poll_limit(int n) {
   g_wino4_poll = n < 0 ? WINO4_POLL_DEFAULT : n;
+  return FR_OK;
+}
+int frt_set_wino4_chain(fr_handle* h, int max_n) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  DeviceGuard dg(h->device);
+  h->chain_max_n = std::max(0, max_n);
+  clear_graphs(h);
   return FR_OK;
 }
 int frt_set_fuse_shortcut(fr_handle* h, int on) {

@@ -64,6 +64,13 @@ int frt_set_s2_band(int on);
  * Asynchronous on stream. */
 int frt_conv2d_s2band(const float* x, const float* w, float* y, int B, int H, int W, const float* post_scale,
                       const float* post_shift, const float* res, void* stream);
+/* Handle h chains the F(4x4) layers of forwards of n <= max_n crops (default 0 = never):
+ * every run of consecutive conv1 / conv2 layers that plan as one-round split-K launches goes out
+ * as one wino4_chain_kernel launch (per layer: the split's partial, an in-launch reduction by the
+ * item's workgroups, a counter the next layer waits on) instead of a conv launch + a fixup launch
+ * per layer.  Outputs are bitwise those of the unchained forward; measured slower than the
+ * per-layer launches at batch 1, hence off.  Drops captured graphs. */
+int frt_set_wino4_chain(fr_handle* h, int max_n);
 /* Handle h runs the stride-2 conv2 of a block with a conv shortcut and that shortcut as one
  * GEMM (on = 1, default: BN scales folded into the weights, extra K-steps over the block input)
  * or as two launches (0).  Drops captured graphs. */

@@ -32,6 +32,8 @@ def lib():
         L.frt_conv2d_s2band.argtypes = [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P]
         L.frt_set_fuse_shortcut.restype = _I
         L.frt_set_fuse_shortcut.argtypes = [_P, _I]
+        L.frt_set_wino4_chain.restype = _I
+        L.frt_set_wino4_chain.argtypes = [_P, _I]
         L.frt_stem.restype = _I
         L.frt_stem.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P, _P]
         L.frt_topk.restype = _I

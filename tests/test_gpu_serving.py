@@ -117,6 +117,35 @@ def test_match_batcher_equals_match_single_face(embedder, tmp_path):
         embedder.model.set_graph_batch(0)
 
 
+def test_chained_layers_bit_identical_to_per_layer_launches(embedder):
+    """With frt_set_wino4_chain(h, 8), serving forwards (n <= 8) run each stage's F(4x4) layers
+    as ONE chained launch (wino4_chain_kernel: split partials, in-launch reduction by the item's
+    workgroups, a counter per layer; off by default, slower than per-layer launches).  Its reduction is the fixup kernel's code, so embeddings must be bitwise those of
+    the per-layer launches, eagerly and under graph replay, run after run (the counters re-arm)."""
+    from tests import _frt
+
+    L = _frt.lib()
+    h = embedder.model
+    crops = torch.from_numpy(W.synthetic_crops(12, seed=W.CROP_SEED_GALLERY)).cuda()
+    ns = (1, 2, 3, 5, 8, 12)  # 12 > the chain's default max: per-layer launches either way
+    try:
+        assert L.frt_set_wino4_chain(h.h, 0) == 0
+        per_layer = {n: embedder.embed_tensor(crops[:n]).clone() for n in ns}
+        assert L.frt_set_wino4_chain(h.h, 8) == 0
+        for rep in range(3):
+            for n in ns:
+                got = embedder.embed_tensor(crops[:n])
+                assert torch.equal(got, per_layer[n]), (n, rep, (got - per_layer[n]).abs().max().item())
+        h.set_graph_batch(8)
+        for rep in range(3):  # rep 0 eager + capture, then replays of the chained graphs
+            for n in (1, 3, 8):
+                assert torch.equal(embedder.embed_tensor(crops[:n]), per_layer[n]), (n, rep)
+        assert h.graph_count() == 3
+    finally:
+        h.set_graph_batch(0)
+        assert L.frt_set_wino4_chain(h.h, 0) == 0
+
+
 def test_small_batches_match_oracle(embedder):
     """Serving batch sizes take the split-K F(4x4) path and small stream-K grids: every
     embedding stays within the pipeline's 1e-5 bar of the CPU oracle."""

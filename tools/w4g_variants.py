@@ -34,6 +34,22 @@ def nouload(s):
 TRANS_PUT = "      store(P, g);\n"
 
 
+def waitonly(s):
+    """the transform waves wait for their patch loads (one sum of the patch written to the ring),
+    but run none of the transform's arithmetic: separates the patch-load latency from the
+    transform code's cost"""
+    assert TRANS_PUT in s
+    return s.replace(TRANS_PUT, """      {
+        f2 sm = P.d[0][0];
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+          for (int b = 0; b < 3; ++b) sm += P.d[a][b];
+        *reinterpret_cast<f2*>(ring + (g % NBUF) * VSTEP + dst_off) = sm;
+      }
+""")
+
+
 def notrans(s):
     """the transform waves keep loading and publishing, but transform and write nothing"""
     assert TRANS_PUT in s
@@ -504,6 +520,8 @@ VARIANTS = {
     "halfu": halfu,
     "noepi": noepi,
     "notrans": notrans,
+    "waitonly": waitonly,
+    "nofixup": lambda s: s.replace("    if (MODE_ == 1) /* 64-thread blocks", "    if (false) /* 64-thread blocks"),
     "noload": lambda s: s.replace("""          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);""",
                                   """          const u32x2 v = {(unsigned)(poff[a][b] + soff), 0u};"""),
     "nomfma": lambda s: (s.replace(MFMA8, "        acc[x][0] += a0.x * u0.x + a1.w * u1.w;\n") if MFMA8 in s else s + "#error MFMA8"),
