@@ -50,6 +50,42 @@ def waitonly(s):
 """)
 
 
+GEO_EDITS = [
+    ("        roff[e] = rin[e] ? (rs * p.NC * H + y) * W * Cin * 4 : BIGOFF;",
+     "        roff[e] = rin[e] ? vmul24(vmad24(vmul24(rs, p.NC), H, y), W * Cin * 4) : BIGOFF;"),
+    ("        coff[e] = cin[e] ? ((cs * H * W + x) * Cin + ch) * 4 : BIGOFF;",
+     "        coff[e] = cin[e] ? vmad24(vmad24(cs, H * W, x), Cin, ch) * 4 : BIGOFF;"),
+    ("          gt[e] = (y >= 0 && rs * p.NC < p.B && T < p.ntiles) ? (rs * p.NC * H + y) * W : -1;",
+     "          gt[e] = (y >= 0 && rs * p.NC < p.B && T < p.ntiles) ? vmul24(vmad24(vmul24(rs, p.NC), H, y), W) : -1;"),
+    ("          gt[4 + e] = (x >= 0 && cs < p.NC) ? cs * H * W + x : -1;",
+     "          gt[4 + e] = (x >= 0 && cs < p.NC) ? vmad24(cs, H * W, x) : -1;"),
+]
+GEO_HELPERS = """
+__device__ __forceinline__ int vmad24(int a, int b, int c) {
+  int r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ int vmul24(int a, int b) {
+  int r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+"""
+
+
+def nomad(s):
+    """item geometry with explicit 24-bit mul / mad instructions (no v_mad_u64_u32, whose unused
+    high addend register can carry an outstanding load and cost a vmcnt wait at item entry)"""
+    a = "__device__ __forceinline__ int canvas_coord("
+    assert a in s
+    s = s.replace(a, GEO_HELPERS + a, 1)
+    for x, y in GEO_EDITS:
+        assert x in s, x
+        s = s.replace(x, y)
+    return s
+
+
 def notrans(s):
     """the transform waves keep loading and publishing, but transform and write nothing"""
     assert TRANS_PUT in s
@@ -194,16 +230,16 @@ def res12(s):
 STAMP_HDR = """
 // ---- stamps variant: per-wave cycle accounting (s_memtime), written once per wave by lane 0 ----
 __device__ unsigned long long w4dbg[1024 * 8 * 4];
-#define W4_WAIT(c_, n_)                                             \\
+#define W4_WAIT(c_, n_, pm_)                                        \\
   ({                                                                \\
     const unsigned long long t0_ = __builtin_amdgcn_s_memtime();    \\
-    const int r_ = lds_wait_min4(c_, n_);                           \\
+    const int r_ = lds_wait_min4(c_, n_, pm_);                      \\
     bar_cyc += __builtin_amdgcn_s_memtime() - t0_;                  \\
     r_;                                                             \\
   })
 #define W4_PUT()                                                                        \\
   if (lane == 0) {                                                                      \\
-    unsigned long long* d_ = w4dbg + ((size_t)blockIdx.x * 8 + wid) * 4;                \\
+    unsigned long long* d_ = w4dbg + ((size_t)bid * 8 + wid) * 4;                \\
     d_[0] = __builtin_amdgcn_s_memtime() - t_start;                                     \\
     d_[1] = bar_cyc;                                                                    \\
     d_[2] = epi_cyc;                                                                    \\
@@ -247,13 +283,18 @@ def stamps(s):
     assert a in s
     s = s.replace(a, a + "  unsigned long long bar_cyc = 0, epi_cyc = 0;\n"
                          "  const unsigned long long t_start = __builtin_amdgcn_s_memtime();\n", 1)
-    a = "      if (b + 3 >= G) break;\n    }\n    return;"
+    a = "      if (b + 3 >= G) break;\n    }\n    w4_report_handoff(fseen, p.err);\n    return;"
     assert a in s
-    s = s.replace(a, "      if (b + 3 >= G) break;\n    }\n    W4_PUT();\n    return;")
+    s = s.replace(a, "      if (b + 3 >= G) break;\n    }\n    W4_PUT();\n    w4_report_handoff(fseen, p.err);\n    return;")
     assert EPI_START in s
     s = s.replace(EPI_START, "    const unsigned long long t_e0 = __builtin_amdgcn_s_memtime();\n" + EPI_START, 1)
-    assert EPI_END in s
-    s = s.replace(EPI_END, "\n    epi_cyc += __builtin_amdgcn_s_memtime() - t_e0;\n  }\n  W4_PUT();\n}\n\n// G g G^T", 1)
+    # part A of the deferred epilogue (whole items); part B runs inside the next item's MFMAs
+    a = "      transform_to_pv();\n      set_pending();\n      return;"
+    assert a in s
+    s = s.replace(a, "      transform_to_pv();\n      set_pending();\n      epi_cyc += __builtin_amdgcn_s_memtime() - t_e0;\n      return;")
+    a = "  w4_report_handoff(rseen, p.err);\n}\n"
+    assert s.count(a) == 1
+    s = s.replace(a, "  W4_PUT();\n  w4_report_handoff(rseen, p.err);\n}\n")
     return s + STAMP_HOST
 
 
@@ -521,6 +562,7 @@ VARIANTS = {
     "noepi": noepi,
     "notrans": notrans,
     "waitonly": waitonly,
+    "nomad": nomad,
     "nofixup": lambda s: s.replace("    if (MODE_ == 1) /* 64-thread blocks", "    if (false) /* 64-thread blocks"),
     "noload": lambda s: s.replace("""          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);""",
                                   """          const u32x2 v = {(unsigned)(poff[a][b] + soff), 0u};"""),
