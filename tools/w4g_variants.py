@@ -562,6 +562,14 @@ VARIANTS = {
     "noepi": noepi,
     "notrans": notrans,
     "waitonly": waitonly,
+    "partb_nostore": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    if (v.x == 12345.678f && p.B < 0) __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);"),
+    "partb_small": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i] & 0xfff0, 0, 0);"),
+    "partb_nt": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 2);"),
+    # deferred epilogue pieces removed (wrong results, timing only)
+    "nopartb": lambda s: s.replace("          if (x >= 4) finish(x / 2 - 2);", "          if (x >= 4 && p.B < 0) finish(x / 2 - 2);"),
+    "nores2": lambda s: s.replace("pres[i] = ld4(rr, oo[i >> 2][i & 3]);", "pres[i] = f4{0.f, 0.f, 0.f, 0.f};"),
+    "stamps_nopartb": lambda s: stamps(s.replace("          if (x >= 4) finish(x / 2 - 2);", "          if (x >= 4 && p.B < 0) finish(x / 2 - 2);")),
+    "noprio": lambda s: s.replace("    if constexpr (PRE) __builtin_amdgcn_s_setprio(1);\n", ""),
     "nomad": nomad,
     "nofixup": lambda s: s.replace("    if (MODE_ == 1) /* 64-thread blocks", "    if (false) /* 64-thread blocks"),
     "noload": lambda s: s.replace("""          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);""",
