@@ -562,6 +562,9 @@ VARIANTS = {
     "noepi": noepi,
     "notrans": notrans,
     "waitonly": waitonly,
+    "partb_sc1": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 16);"),
+    "partb_sc0": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 1);"),
+    "partb_sc01": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 17);"),
     "partb_nostore": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    if (v.x == 12345.678f && p.B < 0) __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);"),
     "partb_small": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i] & 0xfff0, 0, 0);"),
     "partb_nt": lambda s: s.replace("    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);", "    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 2);"),
