@@ -22,7 +22,7 @@ LIB = os.path.join(PKG, "libfrhip.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = "gfx950"
-SOURCES = ["conv_winograd4.hip", "conv_winograd.hip", "conv_s2.hip","conv_f32_w4.hip", "conv_f32_w8.hip", "conv_bf16x3.hip", "conv_det.hip", "conv_mfma.hip",
+SOURCES = ["conv_winograd4.hip", "conv_winograd.hip", "conv_s2.hip", "conv_small.hip","conv_f32_w4.hip", "conv_f32_w8.hip", "conv_bf16x3.hip", "conv_det.hip", "conv_mfma.hip",
            "embed_misc.hip", "align.hip", "gallery.hip", "detect.hip", "frhip_runtime.cpp", "detector.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]

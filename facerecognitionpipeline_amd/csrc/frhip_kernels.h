@@ -167,6 +167,14 @@ bool wino4_chain_plan(Wino4Params& p, bool pre, Epi epi, int cus);
 hipError_t launch_wino4_chain(const W4Link* links, int nl, int grid, int* sync, int ncnt, int* err, int poll_max,
                               hipStream_t s);
 
+// Serving-batch 3x3 convs (conv_small.hip): pad 1, stride 1 or 2, optional fused shortcut
+// (Cin2 / x2, weight rows 9*Cin + Cin2), one workgroup per 16 pixels x 16 couts with the whole K
+// reduction inside it (no split-K, no fixup).  pre: pre-BN + EPI_AFFINE_PRELU (conv1); else
+// EPI_AFFINE / EPI_AFFINE_RES / EPI_AFFINE_RES_SUB.  Reads p.x, w, y, pre_*, post_*, prelu, res,
+// res_H/W, B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, M, x2, Cin2.
+bool convs_supported(const ConvParams& p, bool pre, Epi epi);
+hipError_t launch_convs(const ConvParams& p, bool pre, Epi epi, hipStream_t s);
+
 // Stride-2 3x3 conv, 64 -> 64 channels, + BN + MaxPool2d(1,2) shortcut (conv_s2.hip): the first
 // block of the AdaFace stage 1.  y[b][oy][ox] = conv(x)*scale + shift + res[b][2oy][2ox], NHWC f32;
 // w [64][3][3][64]; res has x's shape.

@@ -407,6 +407,16 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     p.sk_cnt_cap = L ? L->sk_cnt_cap : h->sk_cnt_cap;
   }
   const double flop = 2.0 * p.M * (double)p.Cout * (cw.kh * cw.kw * cw.cin + cw.cin2);
+  // serving batches (n <= convs_max_n): every body 3x3 conv as one launch with the whole K per
+  // 16x16 tile (conv_small.hip); f32 parity path only
+  if (B <= h->convs_max_n && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.kh == 3 &&
+      convs_supported(p, cw.pre_scale != nullptr, epi)) {
+    if (int rc = chain_flush(h, s)) return rc;
+    ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
+    const hipError_t e = launch_convs(p, cw.pre_scale != nullptr, epi, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("serving conv launch: ") + hipGetErrorString(e));
+    return FR_OK;
+  }
   // Tile per layer shape, from tools/conv_sweep.py on MI355X at B=256 with the stream-K
   // schedule (profiles/r01/sweep.txt): 8-wave 128x64 for the 64-channel
   // stage and the 128-channel residual convs, 8-wave 128x128 for the 1x1 shortcuts,
@@ -2111,6 +2121,50 @@ int frt_set_s2_band(int on) {
 }
 int frt_set_wino4_poll_limit(int n) {
   g_wino4_poll = n < 0 ? WINO4_POLL_DEFAULT : n;
+  return FR_OK;
+}
+int frt_conv2d_small(const float* x, const float* x2, const float* w, float* y, int B, int H, int W, int cin,
+                     int cin2, int cout, int stride, const float* pre_scale, const float* pre_shift,
+                     const float* post_scale, const float* post_shift, const float* prelu, const float* res, int epi,
+                     void* stream) {
+  if (B < 1 || H < 1 || W < 1 || (stride != 1 && stride != 2) || epi < 0 || epi > 3 || cin2 < 0 ||
+      ((pre_scale != nullptr) != (epi == EPI_AFFINE_PRELU)) || (pre_scale && !pre_shift))
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_small: bad arguments");
+  ConvParams p{};
+  p.x = x;
+  p.x2 = cin2 > 0 ? x2 : nullptr;
+  p.Cin2 = cin2;
+  p.w = w;
+  p.y = y;
+  p.pre_scale = pre_scale;
+  p.pre_shift = pre_shift;
+  p.post_scale = post_scale;
+  p.post_shift = post_shift;
+  p.prelu = prelu;
+  p.res = res;
+  p.B = B;
+  p.H = H;
+  p.W = W;
+  p.Cin = cin;
+  p.Cout = cout;
+  p.KH = p.KW = 3;
+  p.stride = stride;
+  p.pad = 1;
+  p.Ho = (H - 1) / stride + 1;
+  p.Wo = (W - 1) / stride + 1;
+  p.res_H = H;
+  p.res_W = W;
+  p.M = B * p.Ho * p.Wo;
+  const hipError_t e = launch_convs(p, pre_scale != nullptr, (Epi)epi, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_small: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+int frt_set_small_conv(fr_handle* h, int max_n) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  DeviceGuard dg(h->device);
+  h->convs_max_n = std::max(0, max_n);
+  clear_graphs(h);
   return FR_OK;
 }
 int frt_set_wino4_chain(fr_handle* h, int max_n) {

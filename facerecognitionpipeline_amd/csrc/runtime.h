@@ -191,6 +191,10 @@ struct fr_handle {
   // item's slowest split, then the reduction -- cost more than the two kernel boundaries they
   // replace).
   int chain_max_n = 0;
+  // forwards of n <= convs_max_n crops run every body 3x3 conv on conv_small.hip's kernel (one
+  // launch per layer, whole K per 16x16 tile) instead of F(4x4) split-K + fixup / the split-K
+  // direct convs (frt_set_small_conv)
+  int convs_max_n = 1;
   bool chain_collect = false;
   int chain_seq = 0;  // index of the next run in the current forward
   std::vector<frhip::W4Link> chain_pending;

@@ -64,6 +64,19 @@ int frt_set_s2_band(int on);
  * Asynchronous on stream. */
 int frt_conv2d_s2band(const float* x, const float* w, float* y, int B, int H, int W, const float* post_scale,
                       const float* post_shift, const float* res, void* stream);
+/* Handle h runs every body 3x3 conv of forwards of n <= max_n crops (default 1; 0 = never) on the
+ * serving-batch kernel (conv_small.hip: one launch per layer, 16 pixels x 16 couts per workgroup
+ * with the whole K reduction inside it) instead of F(4x4) split-K + fixup and the split-K direct
+ * convs.  Drops captured graphs. */
+int frt_set_small_conv(fr_handle* h, int max_n);
+/* The serving-batch kernel alone: y = epi(conv3x3 pad 1 stride s (x) [+ conv1x1 stride s (x2)
+ * against weight columns 9*cin .. + cin2]), w [cout][9*cin + cin2]; pre-BN only with epi 1;
+ * epi 0, 1, 2 (res shaped like y) or 3 (res [B][H][W][cout], read at (s oy, s ox)).
+ * cin, cout, cin2 % 16 == 0.  Asynchronous on stream. */
+int frt_conv2d_small(const float* x, const float* x2, const float* w, float* y, int B, int H, int W, int cin,
+                     int cin2, int cout, int stride, const float* pre_scale, const float* pre_shift,
+                     const float* post_scale, const float* post_shift, const float* prelu, const float* res, int epi,
+                     void* stream);
 /* Handle h chains the F(4x4) layers of forwards of n <= max_n crops (default 0 = never):
  * every run of consecutive conv1 / conv2 layers that plan as one-round split-K launches goes out
  * as one wino4_chain_kernel launch (per layer: the split's partial, an in-launch reduction by the

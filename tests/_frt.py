@@ -34,6 +34,10 @@ def lib():
         L.frt_set_fuse_shortcut.argtypes = [_P, _I]
         L.frt_set_wino4_chain.restype = _I
         L.frt_set_wino4_chain.argtypes = [_P, _I]
+        L.frt_set_small_conv.restype = _I
+        L.frt_set_small_conv.argtypes = [_P, _I]
+        L.frt_conv2d_small.restype = _I
+        L.frt_conv2d_small.argtypes = [_P, _P, _P, _P] + [_I] * 7 + [_P] * 6 + [_I, _P]
         L.frt_stem.restype = _I
         L.frt_stem.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P, _P]
         L.frt_topk.restype = _I
@@ -113,5 +117,18 @@ def conv2d_s2band(x, w, B, H, W, post, res):
     y = torch.full((B, H // 2, W // 2, 64), float("nan"), device=x.device)
     rc = lib().frt_conv2d_s2band(_p(x), _p(w), _p(y), B, H, W, _p(post[0]), _p(post[1]), _p(res),
                                  torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc)
+    return y
+
+
+def conv2d_small(x, w, B, H, W, cin, cout, stride=1, x2=None, cin2=0, pre=None, post=None, prelu=None, res=None,
+                 epi=0):
+    """conv_small.hip's serving kernel: x NHWC cuda f32, w [cout][9*cin + cin2] cuda f32."""
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y = torch.full((B, Ho, Wo, cout), float("nan"), device=x.device)
+    ps, ph = (pre if pre is not None else (None, None))
+    qs, qh = post
+    rc = lib().frt_conv2d_small(_p(x), _p(x2), _p(w), _p(y), B, H, W, cin, cin2, cout, stride, _p(ps), _p(ph),
+                                _p(qs), _p(qh), _p(prelu), _p(res), epi, torch.cuda.current_stream().cuda_stream)
     _lib.check(rc)
     return y

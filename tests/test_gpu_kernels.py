@@ -104,6 +104,54 @@ def test_conv2_stride2_maxpool_band_kernel(B, H):
     _close(got.cpu(), _nhwc(ref))
 
 
+@pytest.mark.parametrize("B,H,cin,cout,stride,cin2,epi,pre", [
+    (1, 14, 256, 256, 1, 0, 1, True),     # IR stage-3 conv1 at batch 1: pre-BN + BN + PReLU
+    (1, 14, 256, 256, 1, 0, 2, False),    # stage-3 conv2 + identity residual
+    (2, 7, 512, 512, 1, 0, 2, False),     # stage 4, M = 98 (ragged last pixel block)
+    (1, 56, 64, 64, 2, 0, 3, False),      # stage-1 unit-1 conv2: stride 2 + MaxPool2d(1,2) shortcut
+    (1, 28, 128, 128, 2, 64, 0, False),   # stage-2 unit-1 conv2 + fused 1x1 s2 conv shortcut
+    (3, 9, 32, 48, 1, 0, 1, True),        # odd sizes: 3 images of 9x9, Cout not a multiple of 128
+])
+def test_serving_conv_kernel(B, H, cin, cout, stride, cin2, epi, pre):
+    """conv_small.hip's serving kernel (one workgroup per 16 pixels x 16 couts, whole K inside):
+    against PyTorch CPU f32, incl. the fused shortcut (weights [cout][9 cin + cin2], the second
+    input read at the output's stride) and ragged pixel blocks."""
+    seed = 200 + H + cin + stride
+    x = _rand(B, cin, H, H, seed=seed)
+    w = _rand(cout, cin, 3, 3, seed=seed + 1) / (cin * 9) ** 0.5
+    pre_s, pre_b = _rand(cin, seed=seed + 2, lo=0.5, hi=1.5), _rand(cin, seed=seed + 3, lo=-0.2, hi=0.2)
+    post_s, post_b = _rand(cout, seed=seed + 4, lo=0.5, hi=1.5), _rand(cout, seed=seed + 5, lo=-0.2, hi=0.2)
+    al = _rand(cout, seed=seed + 6, lo=0.1, hi=0.4)
+    xin = x * pre_s.view(1, -1, 1, 1) + pre_b.view(1, -1, 1, 1) if pre else x
+    acc = F.conv2d(xin, w, stride=stride, padding=1)
+    Ho = acc.shape[2]
+    wk = w.permute(0, 2, 3, 1).reshape(cout, 9 * cin)
+    x2d = None
+    if cin2:
+        x2 = _rand(B, cin2, H, H, seed=seed + 8)
+        w2 = _rand(cout, cin2, seed=seed + 9) / cin2 ** 0.5
+        acc = acc + F.conv2d(x2, w2.view(cout, cin2, 1, 1), stride=stride)
+        wk = torch.cat([wk, w2], 1)
+        x2d = _nhwc(x2).to(DEV)
+    ref = acc * post_s.view(1, -1, 1, 1) + post_b.view(1, -1, 1, 1)
+    res = None
+    if epi == 1:
+        ref = torch.where(ref > 0, ref, ref * al.view(1, -1, 1, 1))
+    if epi == 2:
+        r = _rand(B, cout, Ho, Ho, seed=seed + 7)
+        ref = ref + r
+        res = _nhwc(r).to(DEV)
+    if epi == 3:
+        ref = ref + x[:, :, ::2, ::2]
+        res = _nhwc(x).to(DEV)
+    got = _frt.conv2d_small(_nhwc(x).to(DEV), wk.contiguous().to(DEV), B, H, H, cin, cout, stride=stride, x2=x2d,
+                            cin2=cin2, pre=(pre_s.to(DEV), pre_b.to(DEV)) if pre else None,
+                            post=(post_s.to(DEV), post_b.to(DEV)), prelu=al.to(DEV) if epi == 1 else None,
+                            res=res, epi=epi)
+    torch.cuda.synchronize()
+    _close(got.cpu(), _nhwc(ref))
+
+
 def test_conv2_identity_residual_tile0():
     got, ref = _conv_case(2, 12, 64, 64, 3, 1, 1, epi=2, tile=0, use_pre=False, seed=35)
     _close(got, ref)

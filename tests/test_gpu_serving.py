@@ -129,6 +129,7 @@ def test_chained_layers_bit_identical_to_per_layer_launches(embedder):
     crops = torch.from_numpy(W.synthetic_crops(12, seed=W.CROP_SEED_GALLERY)).cuda()
     ns = (1, 2, 3, 5, 8, 12)  # 12 > the chain's default max: per-layer launches either way
     try:
+        assert L.frt_set_small_conv(h.h, 0) == 0  # batch 1 otherwise takes conv_small.hip's kernel
         assert L.frt_set_wino4_chain(h.h, 0) == 0
         per_layer = {n: embedder.embed_tensor(crops[:n]).clone() for n in ns}
         assert L.frt_set_wino4_chain(h.h, 8) == 0
@@ -144,6 +145,35 @@ def test_chained_layers_bit_identical_to_per_layer_launches(embedder):
     finally:
         h.set_graph_batch(0)
         assert L.frt_set_wino4_chain(h.h, 0) == 0
+        assert L.frt_set_small_conv(h.h, 1) == 0
+
+
+def test_serving_conv_path_vs_winograd_path(embedder):
+    """Batch 1 runs every body 3x3 conv on conv_small.hip's kernel (frt_set_small_conv, default
+    n <= 1); with it off the same forward takes the F(4x4) split-K + fixup and split-K direct
+    path.  Both are f32 with exact products: embeddings agree within the pipeline's 1e-5 bar, and
+    each path is run-to-run deterministic (also under graph replay)."""
+    from tests import _frt
+
+    L = _frt.lib()
+    h = embedder.model
+    crops = torch.from_numpy(W.synthetic_crops(4, seed=W.CROP_SEED_GALLERY)).cuda()
+    try:
+        for n in (1, 2, 4):
+            assert L.frt_set_small_conv(h.h, 4) == 0
+            a = embedder.embed_tensor(crops[:n]).clone()
+            assert torch.equal(embedder.embed_tensor(crops[:n]), a)
+            assert L.frt_set_small_conv(h.h, 0) == 0
+            b = embedder.embed_tensor(crops[:n]).clone()
+            assert (a - b).abs().max().item() <= 1e-5, n
+        assert L.frt_set_small_conv(h.h, 1) == 0
+        h.set_graph_batch(4)
+        one = embedder.embed_tensor(crops[:1]).clone()
+        for _ in range(3):
+            assert torch.equal(embedder.embed_tensor(crops[:1]), one)
+    finally:
+        h.set_graph_batch(0)
+        assert L.frt_set_small_conv(h.h, 1) == 0
 
 
 def test_small_batches_match_oracle(embedder):

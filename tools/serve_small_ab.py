@@ -1,0 +1,56 @@
+"""Serving latency with conv_small.hip's kernel for every body 3x3 conv (frt_set_small_conv)
+against the F(4x4) split-K path, per batch size (embed + match, IR-101, G = 1000, top-3).
+
+    python tools/serve_small_ab.py [--ns 1,2,4,8,16]
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from facerecognitionpipeline_amd import weights as W  # noqa: E402
+from facerecognitionpipeline_amd.face_embedder import FaceEmbedder  # noqa: E402
+from tests import _frt  # noqa: E402
+
+
+def timed(fn, iters):
+    fn()
+    fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ns", default="1,2,4,8,16")
+    args = ap.parse_args()
+    emb = FaceEmbedder(architecture="ir_101", model_path="synthetic", max_batch=64, graph_batch=0)
+    h = emb.model
+    G = 1000
+    gal = emb.embed_tensor(torch.from_numpy(W.synthetic_crops(G, seed=W.CROP_SEED_GALLERY)).cuda())
+    h.gallery_set(gal)
+    probes = torch.from_numpy(W.probe_crops(W.synthetic_crops(64, seed=W.CROP_SEED_GALLERY), 64)).cuda()
+    L = _frt.lib()
+    for n in [int(x) for x in args.ns.split(",")]:
+        rgb = probes[:n].contiguous()
+        idx = torch.empty((n, 3), dtype=torch.int32, device="cuda")
+        sc = torch.empty((n, 3), dtype=torch.float32, device="cuda")
+        row = []
+        for mode in (0, n):
+            assert L.frt_set_small_conv(h.h, mode) == 0
+            row.append(timed(lambda: h.embed_match(rgb, 3, idx, sc), 50))
+        print(f"n={n:3d} embed+match: F(4x4) split-K path {row[0]:.3f} ms, serving conv kernel {row[1]:.3f} ms "
+              f"({row[0] / row[1]:.2f}x)", flush=True)
+    assert L.frt_set_small_conv(h.h, 1) == 0
+
+
+if __name__ == "__main__":
+    main()
