@@ -127,6 +127,18 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
     xa[d] = ld4(xr, xo);
     mt[d] = me;
   }
+  // the epilogue's operands, loaded now so their latency overlaps the K loop (wave 0 uses them)
+  const int c4 = cb * 16 + 4 * q;
+  f4 e_sc = {0.f, 0.f, 0.f, 0.f}, e_sh = e_sc, e_al = e_sc, e_res = e_sc;
+  if (w == 0) {
+    e_sc = *reinterpret_cast<const f4*>(p.post_scale + c4);
+    e_sh = *reinterpret_cast<const f4*>(p.post_shift + c4);
+    if constexpr (EPI == EPI_AFFINE_PRELU) e_al = *reinterpret_cast<const f4*>(p.prelu + c4);
+    if constexpr (EPI == EPI_AFFINE_RES)
+      if (mval) e_res = *reinterpret_cast<const f4*>(p.res + (long long)mm * Cout + c4);
+    if constexpr (EPI == EPI_AFFINE_RES_SUB)  // res[b, S oy, S ox] (MaxPool2d(1, 2) of the block input)
+      if (mval) e_res = *reinterpret_cast<const f4*>(p.res + ((long long)(b * p.res_H + oy * S) * p.res_W + ox * S) * Cout + c4);
+  }
   // pre-BN scale / shift into LDS while the first fragments are in flight
   if constexpr (PRE) {
     for (int c = tid; c < Cin; c += 64 * NWV) {
@@ -177,24 +189,13 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
 #pragma unroll
   for (int k = 0; k < NWV - 1; ++k) sum += red[k][lane];
   // epilogue: lane holds couts c4 .. c4 + 3 of pixel m
-  const int c4 = cb * 16 + 4 * q;
   if (!mval) return;
-  const f4 sc = *reinterpret_cast<const f4*>(p.post_scale + c4);
-  const f4 sh = *reinterpret_cast<const f4*>(p.post_shift + c4);
-  f4 v = __builtin_elementwise_fma(sum, sc, sh);
+  f4 v = __builtin_elementwise_fma(sum, e_sc, e_sh);
   if constexpr (EPI == EPI_AFFINE_PRELU) {
-    const f4 al = *reinterpret_cast<const f4*>(p.prelu + c4);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : v[k] * al[k];
+    for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : v[k] * e_al[k];
   }
-  if constexpr (EPI == EPI_AFFINE_RES) {
-    const long long ro = (long long)mm * Cout + c4;
-    v += *reinterpret_cast<const f4*>(p.res + ro);
-  }
-  if constexpr (EPI == EPI_AFFINE_RES_SUB) {  // + res[b, 2 oy, 2 ox] (MaxPool2d(1, 2) of the block input)
-    const long long ro = ((long long)(b * p.res_H + oy * S) * p.res_W + ox * S) * Cout + c4;
-    v += *reinterpret_cast<const f4*>(p.res + ro);
-  }
+  if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_SUB) v += e_res;
   *reinterpret_cast<f4*>(p.y + (long long)mm * Cout + c4) = v;
 }
 

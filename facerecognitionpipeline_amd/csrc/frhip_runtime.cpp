@@ -409,7 +409,9 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   const double flop = 2.0 * p.M * (double)p.Cout * (cw.kh * cw.kw * cw.cin + cw.cin2);
   // serving batches (n <= convs_max_n): every body 3x3 conv as one launch with the whole K per
   // 16x16 tile (conv_small.hip); f32 parity path only
-  if (B <= h->convs_max_n && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.kh == 3 &&
+  // (layers of at most 1024 output pixels: stage 1's 56x56 and 112x112 maps, 196 / 784 pixel
+  // blocks x 4 cout blocks, stay on F(4x4) split-K, which is faster there: 54 vs ~20 us at @112)
+  if (B <= h->convs_max_n && p.M <= 1024 && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.kh == 3 &&
       convs_supported(p, cw.pre_scale != nullptr, epi)) {
     if (int rc = chain_flush(h, s)) return rc;
     ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
