@@ -17,8 +17,10 @@
 //     one workgroup per CU; `tools/convs_bench.py`.)
 //   * XCD-aware order: the workgroups of one 16-channel output block (which read the same
 //     weights) sit on one XCD, so each weight is fetched from HBM once per layer, not once per XCD.
-//   * pre-BN (conv1): the per-channel scale / shift are staged in LDS and applied to in-image taps
-//     only when a fragment is consumed (zero padding stays zero).
+//   * pre-BN (conv1): the previous conv2's launch writes BN(y) beside y (ConvParams::y2, the same
+//     fma the per-tap form does, so bitwise the same operand) and conv1 runs without PRE on it;
+//     where that is not set up (PRE), the per-channel scale / shift are staged in LDS and applied
+//     to in-image taps only when a fragment is consumed (zero padding stays zero).
 //   * fragments: weights are the MFMA's A operand (16 couts x 4 channels, lane (cout, quad q)),
 //     input its B operand (16 pixels x 4 channels); MFMA e of a chunk consumes channel 4q + e of
 //     both, so a lane reads 4 consecutive channels per 16-byte load; the accumulator of lane
@@ -129,8 +131,12 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
   }
   // the epilogue's operands, loaded now so their latency overlaps the K loop (wave 0 uses them)
   const int c4 = cb * 16 + 4 * q;
-  f4 e_sc = {0.f, 0.f, 0.f, 0.f}, e_sh = e_sc, e_al = e_sc, e_res = e_sc;
+  f4 e_sc = {0.f, 0.f, 0.f, 0.f}, e_sh = e_sc, e_al = e_sc, e_res = e_sc, e_s2 = e_sc, e_t2 = e_sc;
   if (w == 0) {
+    if (p.y2) {
+      e_s2 = *reinterpret_cast<const f4*>(p.y2_scale + c4);
+      e_t2 = *reinterpret_cast<const f4*>(p.y2_shift + c4);
+    }
     e_sc = *reinterpret_cast<const f4*>(p.post_scale + c4);
     e_sh = *reinterpret_cast<const f4*>(p.post_shift + c4);
     if constexpr (EPI == EPI_AFFINE_PRELU) e_al = *reinterpret_cast<const f4*>(p.prelu + c4);
@@ -197,12 +203,13 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
   }
   if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_SUB) v += e_res;
   *reinterpret_cast<f4*>(p.y + (long long)mm * Cout + c4) = v;
+  if (p.y2) *reinterpret_cast<f4*>(p.y2 + (long long)mm * Cout + c4) = __builtin_elementwise_fma(v, e_s2, e_t2);
 }
 
 }  // namespace
 
 bool convs_supported(const ConvParams& p, bool pre, Epi epi) {
-  const bool epi_ok = (pre && epi == EPI_AFFINE_PRELU) ||
+  const bool epi_ok = epi == EPI_AFFINE_PRELU ||
                       (!pre && (epi == EPI_AFFINE || epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_SUB));
   return epi_ok && p.KH == 3 && p.KW == 3 && p.pad == 1 && (p.stride == 1 || p.stride == 2) && p.Cin % 16 == 0 &&
          p.Cout % 16 == 0 && p.Cin2 % 16 == 0 && p.Cin2 <= 16 * NWV * SCMAX && (p.Cin2 == 0 || p.x2) && (!pre || p.Cin <= MAXC) && p.M >= 1 &&
@@ -212,11 +219,14 @@ bool convs_supported(const ConvParams& p, bool pre, Epi epi) {
 
 hipError_t launch_convs(const ConvParams& p, bool pre, Epi epi, hipStream_t s) {
   if (!convs_supported(p, pre, epi) || !p.x || !p.w || !p.y || !p.post_scale || !p.post_shift ||
-      (epi == EPI_AFFINE_PRELU && !p.prelu) || ((epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_SUB) && !p.res))
+      (epi == EPI_AFFINE_PRELU && !p.prelu) || ((epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_SUB) && !p.res) ||
+      (p.y2 && (!p.y2_scale || !p.y2_shift)))
     return hipErrorInvalidValue;
   const int grid = ((p.M + 15) / 16) * (p.Cout / 16);
   if (pre)
     hipLaunchKernelGGL((convs_kernel<true, EPI_AFFINE_PRELU>), dim3(grid), dim3(64 * NWV), 0, s, p);
+  else if (epi == EPI_AFFINE_PRELU)
+    hipLaunchKernelGGL((convs_kernel<false, EPI_AFFINE_PRELU>), dim3(grid), dim3(64 * NWV), 0, s, p);
   else if (epi == EPI_AFFINE)
     hipLaunchKernelGGL((convs_kernel<false, EPI_AFFINE>), dim3(grid), dim3(64 * NWV), 0, s, p);
   else if (epi == EPI_AFFINE_RES)

@@ -50,6 +50,11 @@ struct ConvParams {
   // shortcut as one GEMM (both BN scales folded into the weights, the shifts into post_shift)
   const float* x2;
   int Cin2, steps1;
+  // serving conv kernel only (conv_small.hip): also y2 = y * y2_scale[c] + y2_shift[c] (the next
+  // block's pre-activation BN, applied once here instead of per tap in its conv1); null: none
+  float* y2;
+  const float* y2_scale;
+  const float* y2_shift;
 };
 
 // Tile family of a conv launch.

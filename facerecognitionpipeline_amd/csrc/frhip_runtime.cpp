@@ -414,9 +414,15 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   if (B <= h->convs_max_n && p.M <= 1024 && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.kh == 3 &&
       convs_supported(p, cw.pre_scale != nullptr, epi)) {
     if (int rc = chain_flush(h, s)) return rc;
+    if (h->convs_y2 && epi != EPI_AFFINE_PRELU) {
+      p.y2 = h->convs_y2;
+      p.y2_scale = h->convs_y2_scale;
+      p.y2_shift = h->convs_y2_shift;
+    }
     ProfScope ps(h, s, flop, FR_PROF_CONV_DIRECT);
     const hipError_t e = launch_convs(p, cw.pre_scale != nullptr, epi, s);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("serving conv launch: ") + hipGetErrorString(e));
+    if (p.y2) h->convs_y2_done = true;
     return FR_OK;
   }
   // Tile per layer shape, from tools/conv_sweep.py on MI355X at B=256 with the stream-K
@@ -668,13 +674,41 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("stem launch: ") + hipGetErrorString(e));
   }
   int cur = 0, HW = 112;
-  for (const auto& b : h->blocks) {
+  struct Y2Scope {
+    fr_handle* h;
+    ~Y2Scope() { h->convs_y2 = nullptr; }
+  } y2_scope{h};
+  bool pre_done = false;  // the previous conv2 wrote this block's pre-BN input into L[0].sc_buf
+  for (size_t bi = 0; bi < h->blocks.size(); ++bi) {
+    const BlockW& b = h->blocks[bi];
     const int nxt = cur == 0 ? 1 : 0;
     const int Ho = HW / b.spec.stride;
     for (int l = 0; l < nl; ++l) {
-      int rc = run_conv(h, b.conv1, L[l].act[cur], L[l].act[2], cnt[l], HW, HW, EPI_AFFINE_PRELU, nullptr, 0, 0, 1,
-                        0, st[l], &L[l]);
+      int rc;
+      if (pre_done) {
+        // BN(x) is already in sc_buf: conv1 without pre-BN (and not on the F(4x4) / F(2x2)
+        // filters, which have the pre-BN scale folded in)
+        ConvW c1 = b.conv1;
+        c1.pre_scale = c1.pre_shift = nullptr;
+        c1.wino = c1.wino4 = c1.wino4_t = nullptr;
+        rc = run_conv(h, c1, L[l].sc_buf, L[l].act[2], cnt[l], HW, HW, EPI_AFFINE_PRELU, nullptr, 0, 0, 1, 0, st[l],
+                      &L[l]);
+      } else {
+        rc = run_conv(h, b.conv1, L[l].act[cur], L[l].act[2], cnt[l], HW, HW, EPI_AFFINE_PRELU, nullptr, 0, 0, 1,
+                      0, st[l], &L[l]);
+      }
       if (rc) return rc;
+    }
+    // a one-lane forward's conv2 on the serving conv kernel also writes the next block's pre-BN
+    // input (sc_buf is free then unless this block's unfused shortcut uses it)
+    const bool fused = b.has_sc_conv && h->fuse_shortcut && b.conv2_sc.w;
+    h->convs_y2 = nullptr;
+    h->convs_y2_done = false;
+    if (nl == 1 && h->convs_pre_epilogue && bi + 1 < h->blocks.size() && (fused || !b.has_sc_conv) &&
+        h->blocks[bi + 1].conv1.pre_scale && (size_t)Ho * Ho * b.spec.depth <= (size_t)56 * 56 * 64) {
+      h->convs_y2 = L[0].sc_buf;
+      h->convs_y2_scale = h->blocks[bi + 1].conv1.pre_scale;
+      h->convs_y2_shift = h->blocks[bi + 1].conv1.pre_shift;
     }
     for (int l = 0; l < nl; ++l) {
       float* x = L[l].act[cur];
@@ -695,6 +729,9 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
       }
       if (rc) return rc;
     }
+    pre_done = h->convs_y2_done;
+    h->convs_y2 = nullptr;
+    h->convs_y2_done = false;
     cur = nxt;
     HW = Ho;
   }
@@ -2166,6 +2203,14 @@ int frt_set_small_conv(fr_handle* h, int max_n) {
   std::lock_guard<std::mutex> lk(h->mu);
   DeviceGuard dg(h->device);
   h->convs_max_n = std::max(0, max_n);
+  clear_graphs(h);
+  return FR_OK;
+}
+int frt_set_small_conv_pre_epilogue(fr_handle* h, int on) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  DeviceGuard dg(h->device);
+  h->convs_pre_epilogue = on != 0;
   clear_graphs(h);
   return FR_OK;
 }

@@ -195,6 +195,13 @@ struct fr_handle {
   // launch per layer, whole K per 16x16 tile) instead of F(4x4) split-K + fixup / the split-K
   // direct convs (frt_set_small_conv)
   int convs_max_n = 1;
+  // a one-lane forward's conv2 on that kernel also writes the next block's pre-BN input into
+  // convs_y2 (forward_lanes sets these three; run_conv sets convs_y2_done when it did), and that
+  // block's conv1 then runs without pre-BN on it (frt_set_small_conv_pre_epilogue: A/B)
+  float* convs_y2 = nullptr;
+  const float *convs_y2_scale = nullptr, *convs_y2_shift = nullptr;
+  bool convs_y2_done = false;
+  bool convs_pre_epilogue = true;
   bool chain_collect = false;
   int chain_seq = 0;  // index of the next run in the current forward
   std::vector<frhip::W4Link> chain_pending;

@@ -176,6 +176,38 @@ def test_serving_conv_path_vs_winograd_path(embedder):
         assert L.frt_set_small_conv(h.h, 1) == 0
 
 
+def test_pre_bn_in_previous_epilogue_is_bitwise_the_per_tap_form(embedder):
+    """On the serving conv path a conv2 also writes BN(y) for the next block's conv1, which then
+    runs without its pre-BN (frt_set_small_conv_pre_epilogue, default on).  The epilogue applies
+    the same fma the per-tap form applies to the same stored value, so the embeddings are bitwise
+    those with it off, eagerly and under graph replay, also for an n = 4 forward when the serving
+    path takes up to 4 crops."""
+    from tests import _frt
+
+    L = _frt.lib()
+    h = embedder.model
+    crops = torch.from_numpy(W.synthetic_crops(4, seed=W.CROP_SEED_GALLERY)).cuda()
+    try:
+        for n, max_n in ((1, 1), (4, 4)):
+            assert L.frt_set_small_conv(h.h, max_n) == 0
+            assert L.frt_set_small_conv_pre_epilogue(h.h, 0) == 0
+            ref = embedder.embed_tensor(crops[:n]).clone()
+            assert L.frt_set_small_conv_pre_epilogue(h.h, 1) == 0
+            got = embedder.embed_tensor(crops[:n])
+            assert torch.equal(got, ref), (n, (got - ref).abs().max().item())
+        assert L.frt_set_small_conv(h.h, 1) == 0
+        assert L.frt_set_small_conv_pre_epilogue(h.h, 0) == 0
+        off = embedder.embed_tensor(crops[:1]).clone()
+        assert L.frt_set_small_conv_pre_epilogue(h.h, 1) == 0
+        h.set_graph_batch(1)
+        for _ in range(3):
+            assert torch.equal(embedder.embed_tensor(crops[:1]), off)
+    finally:
+        h.set_graph_batch(0)
+        assert L.frt_set_small_conv_pre_epilogue(h.h, 1) == 0
+        assert L.frt_set_small_conv(h.h, 1) == 0
+
+
 def test_small_batches_match_oracle(embedder):
     """Serving batch sizes take the split-K F(4x4) path and small stream-K grids: every
     embedding stays within the pipeline's 1e-5 bar of the CPU oracle."""

@@ -2,6 +2,7 @@
 against the F(4x4) split-K path, per batch size (embed + match, IR-101, G = 1000, top-3).
 
     python tools/serve_small_ab.py [--ns 1,2,4,8,16]
+    python tools/serve_small_ab.py --pre-epilogue [--ns 1]   (conv1 pre-BN in conv2's epilogue on / off)
 """
 import argparse
 import os
@@ -31,6 +32,7 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", default="1,2,4,8,16")
+    ap.add_argument("--pre-epilogue", action="store_true")
     args = ap.parse_args()
     emb = FaceEmbedder(architecture="ir_101", model_path="synthetic", max_batch=64, graph_batch=0)
     h = emb.model
@@ -43,6 +45,17 @@ def main():
         rgb = probes[:n].contiguous()
         idx = torch.empty((n, 3), dtype=torch.int32, device="cuda")
         sc = torch.empty((n, 3), dtype=torch.float32, device="cuda")
+        if args.pre_epilogue:
+            assert L.frt_set_small_conv(h.h, n) == 0
+            t = {0: [], 1: []}
+            for rep in range(4):
+                for on in (1, 0):
+                    assert L.frt_set_small_conv_pre_epilogue(h.h, on) == 0
+                    t[on].append(timed(lambda: h.embed_match(rgb, 3, idx, sc), 100))
+            assert L.frt_set_small_conv_pre_epilogue(h.h, 1) == 0
+            print(f"n={n:3d} embed+match: pre-BN per tap {min(t[0]):.3f} ms (runs {' '.join(f'{x:.3f}' for x in t[0])}), "
+                  f"in conv2's epilogue {min(t[1]):.3f} ms (runs {' '.join(f'{x:.3f}' for x in t[1])})", flush=True)
+            continue
         row = []
         for mode in (0, n):
             assert L.frt_set_small_conv(h.h, mode) == 0
