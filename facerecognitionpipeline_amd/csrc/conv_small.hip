@@ -17,6 +17,9 @@
 //     one workgroup per CU; `tools/convs_bench.py`.)
 //   * XCD-aware order: the workgroups of one 16-channel output block (which read the same
 //     weights) sit on one XCD, so each weight is fetched from HBM once per layer, not once per XCD.
+//   * filters in fragment order (launch_convs_weights): a wave's weight load is one contiguous
+//     KiB, not 16 rows x 64 B (16 filter rows 9 Cin * 4 B apart); measured on this GPU
+//     (tools/l2_stride_bench.hip, 208 workgroups x 4 waves x 36 loads, 12 in flight): 2.5 vs 5.2 us.
 //   * pre-BN (conv1): the previous conv2's launch writes BN(y) beside y (ConvParams::y2, the same
 //     fma the per-tap form does, so bitwise the same operand) and conv1 runs without PRE on it;
 //     where that is not set up (PRE), the per-channel scale / shift are staged in LDS and applied
@@ -78,13 +81,12 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
   const bool mval = m < p.M;
   const int mm = mval ? m : 0;
   const int b = mm / (Ho * Wo), r0 = mm - b * (Ho * Wo), oy = r0 / Wo, ox = r0 - oy * Wo;
-  const int co = cb * 16 + (lane & 15);
   const int KR = 9 * Cin + Cin2;  // weight row length
   const __amdgpu_buffer_rsrc_t xr = rsrc(p.x, (long long)p.B * H * W * Cin * 4);
   const __amdgpu_buffer_rsrc_t x2r = rsrc(p.x2 ? p.x2 : p.x, p.x2 ? (long long)p.B * H * W * Cin2 * 4 : 0);
   const __amdgpu_buffer_rsrc_t wr = rsrc(p.w, (long long)Cout * KR * 4);
   const int CC = Cin >> 4;           // 16-channel chunks per tap
-  const int wrow = (co * KR + 4 * q) * 4;
+  const int wl = (cb * (KR >> 4) * 64 + lane) * 16;  // this lane's 16 B of chunk 0 of block cb
   // This wave's conv chunks: (tap, channel chunk cc) for cc = w, w + NWV, ... < CC, taps in
   // order, walked incrementally with wave-uniform (scalar) state and no branches: per chunk a few
   // scalar and ~10 vector ops (the first version's divisions, branches and per-chunk buffer
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
     const int iy = oys + ky, ix = oxs + kx;
     const bool live = it_i < nI;
     const bool in = live && mval && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-    woff = live ? wrow + (it_tap * Cin + c0) * 4 : BIGOFF;
+    woff = live ? wl + (it_tap * CC + (c0 >> 4)) * 1024 : BIGOFF;
     xoff = in ? xbase + (iy * W + ix) * (Cin * 4) + c0 * 4 : BIGOFF;
     meta = (c0 + 4 * q) | (in ? 1 << 16 : 0);
     ++it_i;
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
   for (int k = 0; k < SCMAX; ++k) {
     const int c0 = (w + NWV * k) * 16;
     const bool live = c0 < Cin2;
-    swa[k] = ld4(wr, live ? wrow + (9 * Cin + c0) * 4 : BIGOFF);
+    swa[k] = ld4(wr, live ? wl + (9 * CC + (c0 >> 4)) * 1024 : BIGOFF);
     sxa[k] = ld4(x2r, live && mval ? ((b * H + oy * S) * W + ox * S) * (Cin2 * 4) + (c0 + 4 * q) * 4 : BIGOFF);
   }
   f4 wa[CH], xa[CH];
@@ -206,7 +208,26 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
   if (p.y2) *reinterpret_cast<f4*>(p.y2 + (long long)mm * Cout + c4) = __builtin_elementwise_fma(v, e_s2, e_t2);
 }
 
+__global__ __launch_bounds__(256) void convs_weights_kernel(const float* __restrict__ w, float* __restrict__ wf,
+                                                          int Cout, int KR) {
+  const int NK = KR >> 4;
+  const long long i = blockIdx.x * 256ll + threadIdx.x;  // one 16-byte fragment per thread
+  if (i >= (long long)(Cout >> 4) * NK * 64) return;
+  const int l = (int)(i & 63);
+  const long long t = i >> 6;
+  const int kc = (int)(t % NK), cb = (int)(t / NK);
+  *reinterpret_cast<f4*>(wf + i * 4) =
+      *reinterpret_cast<const f4*>(w + (long long)(cb * 16 + (l & 15)) * KR + kc * 16 + 4 * (l >> 4));
+}
+
 }  // namespace
+
+hipError_t launch_convs_weights(const float* w, float* wf, int Cout, int KR, hipStream_t s) {
+  if (!w || !wf || Cout <= 0 || KR <= 0 || Cout % 16 || KR % 16) return hipErrorInvalidValue;
+  const long long n = (long long)Cout * KR / 4;
+  hipLaunchKernelGGL(convs_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, wf, Cout, KR);
+  return hipGetLastError();
+}
 
 bool convs_supported(const ConvParams& p, bool pre, Epi epi) {
   const bool epi_ok = epi == EPI_AFFINE_PRELU ||

@@ -175,10 +175,15 @@ hipError_t launch_wino4_chain(const W4Link* links, int nl, int grid, int* sync, 
 // Serving-batch 3x3 convs (conv_small.hip): pad 1, stride 1 or 2, optional fused shortcut
 // (Cin2 / x2, weight rows 9*Cin + Cin2), one workgroup per 16 pixels x 16 couts with the whole K
 // reduction inside it (no split-K, no fixup).  pre: pre-BN + EPI_AFFINE_PRELU (conv1); else
-// EPI_AFFINE / EPI_AFFINE_RES / EPI_AFFINE_RES_SUB.  Reads p.x, w, y, pre_*, post_*, prelu, res,
-// res_H/W, B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, M, x2, Cin2.
+// EPI_AFFINE / EPI_AFFINE_PRELU / EPI_AFFINE_RES / EPI_AFFINE_RES_SUB.  Reads p.x, w, y, pre_*,
+// post_*, prelu, res, res_H/W, B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, M, x2, Cin2, y2*.
+// p.w is in fragment order (launch_convs_weights), not [Cout][9 Cin + Cin2].
 bool convs_supported(const ConvParams& p, bool pre, Epi epi);
 hipError_t launch_convs(const ConvParams& p, bool pre, Epi epi, hipStream_t s);
+// w [Cout][KR] (KR = 9 Cin + Cin2, both % 16 == 0) -> wf, Cout * KR floats in fragment order:
+// per 16-cout block cb and 16-wide K chunk kc, the 1 KiB one load instruction of a wave reads
+// (lane l: couts cb * 16 + (l & 15), K kc * 16 + 4 (l >> 4) .. + 3).
+hipError_t launch_convs_weights(const float* w, float* wf, int Cout, int KR, hipStream_t s);
 
 // Stride-2 3x3 conv, 64 -> 64 channels, + BN + MaxPool2d(1,2) shortcut (conv_s2.hip): the first
 // block of the AdaFace stage 1.  y[b][oy][ox] = conv(x)*scale + shift + res[b][2oy][2ox], NHWC f32;

@@ -411,8 +411,9 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // 16x16 tile (conv_small.hip); f32 parity path only
   // (layers of at most 1024 output pixels: stage 1's 56x56 and 112x112 maps, 196 / 784 pixel
   // blocks x 4 cout blocks, stay on F(4x4) split-K, which is faster there: 54 vs ~20 us at @112)
-  if (B <= h->convs_max_n && p.M <= 1024 && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.kh == 3 &&
+  if (B <= h->convs_max_n && p.M <= 1024 && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.w_frag &&
       convs_supported(p, cw.pre_scale != nullptr, epi)) {
+    p.w = cw.w_frag;
     if (int rc = chain_flush(h, s)) return rc;
     if (h->convs_y2 && epi != EPI_AFFINE_PRELU) {
       p.y2 = h->convs_y2;
@@ -1416,6 +1417,32 @@ static void drop_wino4(fr_handle* h) {
   }
 }
 
+// The serving conv kernel's filters (fragment order) for every body 3x3 conv it can run: conv1,
+// conv2 and the fused conv2 + shortcut of each block (embedding models only).
+static int ensure_convs_weights(fr_handle* h) {
+  if (h->convs_arena || h->detector) return FR_OK;
+  std::vector<ConvW*> cs;
+  size_t floats = 0;
+  for (auto& b : h->blocks)
+    for (ConvW* c : {&b.conv1, &b.conv2, &b.conv2_sc}) {
+      c->w_frag = nullptr;
+      if (c->w && c->kh == 3 && c->kw == 3 && c->cin % 16 == 0 && c->cout % 16 == 0 && c->cin2 % 16 == 0) {
+        cs.push_back(c);
+        floats += (size_t)c->cout * (9 * c->cin + c->cin2);
+      }
+    }
+  if (!floats) return FR_OK;
+  FR_HIP(h, hipMalloc((void**)&h->convs_arena, floats * sizeof(float)));
+  size_t off = 0;
+  for (ConvW* c : cs) {
+    c->w_frag = h->convs_arena + off;
+    off += (size_t)c->cout * (9 * c->cin + c->cin2);
+    FR_HIP(h, launch_convs_weights(c->w, c->w_frag, c->cout, 9 * c->cin + c->cin2, nullptr));
+  }
+  FR_HIP(h, hipDeviceSynchronize());
+  return FR_OK;
+}
+
 static int ensure_winograd(fr_handle* h) {
   if (!h->winograd) return FR_OK;
   if (h->wino_m == 2) return ensure_wino2(h);
@@ -1557,6 +1584,8 @@ int fr_finalize(fr_handle* h) {
   if (h->wino_arena) FR_HIP(h, hipFree(h->wino_arena));
   h->wino_arena = nullptr;
   drop_wino4(h);
+  if (h->convs_arena) FR_HIP(h, hipFree(h->convs_arena));
+  h->convs_arena = nullptr;
   for (auto& b : h->blocks) {
     b.conv1.wino = nullptr;
     b.conv2.wino = nullptr;
@@ -1586,6 +1615,10 @@ int fr_finalize(fr_handle* h) {
       h->finalized = false;
       return rc;
     }
+  }
+  if (const int rc = ensure_convs_weights(h)) {
+    h->finalized = false;
+    return rc;
   }
   return FR_OK;
 }
@@ -2194,7 +2227,22 @@ int frt_conv2d_small(const float* x, const float* x2, const float* w, float* y, 
   p.res_H = H;
   p.res_W = W;
   p.M = B * p.Ho * p.Wo;
-  const hipError_t e = launch_convs(p, pre_scale != nullptr, (Epi)epi, (hipStream_t)stream);
+  if (!w || cout % 16 || cin % 16 || cin2 % 16)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_small: bad arguments");
+  // the kernel reads its filters in fragment order: a temporary copy (test entry point)
+  float* wf = nullptr;
+  const size_t wbytes = (size_t)cout * (9 * cin + cin2) * sizeof(float);
+  hipError_t e = hipMalloc((void**)&wf, wbytes);
+  if (e == hipSuccess) e = launch_convs_weights(w, wf, cout, 9 * cin + cin2, (hipStream_t)stream);
+  if (e == hipSuccess) {
+    p.w = wf;
+    e = launch_convs(p, pre_scale != nullptr, (Epi)epi, (hipStream_t)stream);
+  }
+  if (wf) {
+    const hipError_t e2 = hipStreamSynchronize((hipStream_t)stream);
+    (void)hipFree(wf);
+    if (e == hipSuccess) e = e2;
+  }
   if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_conv2d_small: ") + hipGetErrorString(e));
   return FR_OK;
 }

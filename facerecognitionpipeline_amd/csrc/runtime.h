@@ -29,6 +29,7 @@ struct ConvW {
   float* wino = nullptr;  // Winograd-transformed filters (stride-1 3x3 only), or null
   float* wino4 = nullptr; // F(4x4,3x3) transformed filters G (g * pre_scale) G^T (built on demand), or null
   float* wino4_t = nullptr;  // F(4x4) folded pre-BN: pre_shift / pre_scale per input channel
+  float* w_frag = nullptr;   // the serving conv kernel's copy of w in fragment order (launch_convs_weights), or null
   int cin = 0, cout = 0, kh = 0, kw = 0, stride = 1, pad = 0;
   int cin2 = 0;  // fused 1x1 shortcut input channels (w rows KH*KW*cin + cin2 long), else 0
 };
@@ -153,6 +154,7 @@ struct fr_handle {
   int wino_m = 4;                // output tile of the Winograd algorithm: 4 = F(4x4,3x3) (default), 2 = F(2x2,3x3)
   float* wino_arena = nullptr;   // F(2x2) filters, built when that algorithm is selected
   float* wino4_arena = nullptr;  // F(4x4) filters, likewise
+  float* convs_arena = nullptr;  // the serving conv kernel's filters (ConvW::w_frag), built at fr_finalize
   float* w4part = nullptr;         // F(4x4) split-K partial outputs (small batches), W4PART_FLOATS
   static constexpr long long W4PART_FLOATS = 16ll << 20;
   static constexpr long long W4CNT_INTS = 1 << 16;  // its last 256 KB: F(4x4) stream-K tail tickets
@@ -253,6 +255,7 @@ struct fr_handle {
     (void)hipFree(arena);
     (void)hipFree(wino_arena);
     (void)hipFree(wino4_arena);
+    (void)hipFree(convs_arena);
     (void)hipFree(w4part);
     for (auto p : act) (void)hipFree(p);
     (void)hipFree(sc_buf);
