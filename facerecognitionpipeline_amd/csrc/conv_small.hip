@@ -20,6 +20,11 @@
 //   * filters in fragment order (launch_convs_weights): a wave's weight load is one contiguous
 //     KiB, not 16 rows x 64 B (16 filter rows 9 Cin * 4 B apart); measured on this GPU
 //     (tools/l2_stride_bench.hip, 208 workgroups x 4 waves x 36 loads, 12 in flight): 2.5 vs 5.2 us.
+//   * activations between two such layers channel-blocked (p.blk): [B][C/16][H][W][16], so a
+//     wave's input load (16 consecutive pixels x 16 channels) is one contiguous KiB too, and so is
+//     its output store; NHWC where the producer or a consumer is another kernel.
+//   * outputs stored write-through (sc1): the next launch reads them from other XCDs anyway, and
+//     what a launch leaves dirty in L2 is written back at the kernel boundary.
 //   * pre-BN (conv1): the previous conv2's launch writes BN(y) beside y (ConvParams::y2, the same
 //     fma the per-tap form does, so bitwise the same operand) and conv1 runs without PRE on it;
 //     where that is not set up (PRE), the per-channel scale / shift are staged in LDS and applied
@@ -43,10 +48,14 @@ constexpr int CH = 12;  // chunks in flight per wave
 constexpr int SCMAX = 4;   // fused-shortcut chunks per wave (Cin2 <= 16 * NWV * SCMAX)
 constexpr int BIGOFF = 0x7F000000;
 constexpr int MAXC = 512;  // pre-BN channels staged in LDS
+constexpr int CPOL_SC1 = 16;  // buffer-store cache policy bit sc1 (write-through)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* ptr, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, (int)std::min(bytes, 0x7fffffffll),
                                            0x00020000);
+}
+__device__ __forceinline__ u32x4 bits4(f4 v) {
+  return u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
 }
 __device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, int off) {
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
@@ -86,6 +95,10 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
   const __amdgpu_buffer_rsrc_t x2r = rsrc(p.x2 ? p.x2 : p.x, p.x2 ? (long long)p.B * H * W * Cin2 * 4 : 0);
   const __amdgpu_buffer_rsrc_t wr = rsrc(p.w, (long long)Cout * KR * 4);
   const int CC = Cin >> 4;           // 16-channel chunks per tap
+  // activation layouts: bytes per pixel and per 16-channel chunk (NHWC or channel-blocked)
+  const bool xbk = p.blk & CONVS_BLK_X, x2bk = p.blk & CONVS_BLK_X2, rbk = p.blk & CONVS_BLK_RES,
+             ybk = p.blk & CONVS_BLK_Y;
+  const int xpx = xbk ? 64 : Cin * 4, xcc = xbk ? H * W * 64 : 64;
   const int wl = (cb * (KR >> 4) * 64 + lane) * 16;  // this lane's 16 B of chunk 0 of block cb
   // This wave's conv chunks: (tap, channel chunk cc) for cc = w, w + NWV, ... < CC, taps in
   // order, walked incrementally with wave-uniform (scalar) state and no branches: per chunk a few
@@ -105,7 +118,7 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
     const bool live = it_i < nI;
     const bool in = live && mval && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
     woff = live ? wl + (it_tap * CC + (c0 >> 4)) * 1024 : BIGOFF;
-    xoff = in ? xbase + (iy * W + ix) * (Cin * 4) + c0 * 4 : BIGOFF;
+    xoff = in ? xbase + (iy * W + ix) * xpx + (c0 >> 4) * xcc : BIGOFF;
     meta = (c0 + 4 * q) | (in ? 1 << 16 : 0);
     ++it_i;
     const bool wrap = ++it_k == ncc;
@@ -119,7 +132,9 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
     const int c0 = (w + NWV * k) * 16;
     const bool live = c0 < Cin2;
     swa[k] = ld4(wr, live ? wl + (9 * CC + (c0 >> 4)) * 1024 : BIGOFF);
-    sxa[k] = ld4(x2r, live && mval ? ((b * H + oy * S) * W + ox * S) * (Cin2 * 4) + (c0 + 4 * q) * 4 : BIGOFF);
+    sxa[k] = ld4(x2r, live && mval ? b * H * W * Cin2 * 4 + (oy * S * W + ox * S) * (x2bk ? 64 : Cin2 * 4) +
+                                         (c0 >> 4) * (x2bk ? H * W * 64 : 64) + 16 * q
+                                   : BIGOFF);
   }
   f4 wa[CH], xa[CH];
   int mt[CH];
@@ -133,6 +148,8 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
   }
   // the epilogue's operands, loaded now so their latency overlaps the K loop (wave 0 uses them)
   const int c4 = cb * 16 + 4 * q;
+  // output element (floats) of this lane's 4 couts: b, pixel r0 of Ho x Wo, block cb, 4 q
+  const int yoff = b * Ho * Wo * Cout + r0 * (ybk ? 16 : Cout) + cb * (ybk ? Ho * Wo * 16 : 16) + 4 * q;
   f4 e_sc = {0.f, 0.f, 0.f, 0.f}, e_sh = e_sc, e_al = e_sc, e_res = e_sc, e_s2 = e_sc, e_t2 = e_sc;
   if (w == 0) {
     if (p.y2) {
@@ -143,9 +160,14 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
     e_sh = *reinterpret_cast<const f4*>(p.post_shift + c4);
     if constexpr (EPI == EPI_AFFINE_PRELU) e_al = *reinterpret_cast<const f4*>(p.prelu + c4);
     if constexpr (EPI == EPI_AFFINE_RES)
-      if (mval) e_res = *reinterpret_cast<const f4*>(p.res + (long long)mm * Cout + c4);
+      if (mval)
+        e_res = *reinterpret_cast<const f4*>(p.res + b * Ho * Wo * Cout + r0 * (rbk ? 16 : Cout) +
+                                             cb * (rbk ? Ho * Wo * 16 : 16) + 4 * q);
     if constexpr (EPI == EPI_AFFINE_RES_SUB)  // res[b, S oy, S ox] (MaxPool2d(1, 2) of the block input)
-      if (mval) e_res = *reinterpret_cast<const f4*>(p.res + ((long long)(b * p.res_H + oy * S) * p.res_W + ox * S) * Cout + c4);
+      if (mval)
+        e_res = *reinterpret_cast<const f4*>(p.res + b * p.res_H * p.res_W * Cout +
+                                             (oy * S * p.res_W + ox * S) * (rbk ? 16 : Cout) +
+                                             cb * (rbk ? p.res_H * p.res_W * 16 : 16) + 4 * q);
   }
   // pre-BN scale / shift into LDS while the first fragments are in flight
   if constexpr (PRE) {
@@ -204,8 +226,11 @@ __global__ __launch_bounds__(64 * NWV) void convs_kernel(ConvParams p) {
     for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : v[k] * e_al[k];
   }
   if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_SUB) v += e_res;
-  *reinterpret_cast<f4*>(p.y + (long long)mm * Cout + c4) = v;
-  if (p.y2) *reinterpret_cast<f4*>(p.y2 + (long long)mm * Cout + c4) = __builtin_elementwise_fma(v, e_s2, e_t2);
+  const long long ybytes = (long long)p.M * Cout * 4;
+  __builtin_amdgcn_raw_buffer_store_b128(bits4(v), rsrc(p.y, ybytes), yoff * 4, 0, CPOL_SC1);
+  if (p.y2)
+    __builtin_amdgcn_raw_buffer_store_b128(bits4(__builtin_elementwise_fma(v, e_s2, e_t2)), rsrc(p.y2, ybytes), yoff * 4,
+                                           0, CPOL_SC1);
 }
 
 __global__ __launch_bounds__(256) void convs_weights_kernel(const float* __restrict__ w, float* __restrict__ wf,

@@ -55,7 +55,11 @@ struct ConvParams {
   float* y2;
   const float* y2_scale;
   const float* y2_shift;
+  // serving conv kernel only: which activations are channel-blocked [B][C/16][H][W][16] instead
+  // of NHWC (CONVS_BLK_* bits; y2 follows y)
+  int blk;
 };
+constexpr int CONVS_BLK_X = 1, CONVS_BLK_X2 = 2, CONVS_BLK_RES = 4, CONVS_BLK_Y = 8;
 
 // Tile family of a conv launch.
 enum ConvTile : int {

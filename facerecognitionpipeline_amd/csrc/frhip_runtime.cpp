@@ -415,6 +415,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
       convs_supported(p, cw.pre_scale != nullptr, epi)) {
     p.w = cw.w_frag;
     if (int rc = chain_flush(h, s)) return rc;
+    p.blk = h->convs_blk;
     if (h->convs_y2 && epi != EPI_AFFINE_PRELU) {
       p.y2 = h->convs_y2;
       p.y2_scale = h->convs_y2_scale;
@@ -426,6 +427,8 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     if (p.y2) h->convs_y2_done = true;
     return FR_OK;
   }
+  if (h->convs_blk)  // forward_lanes only sets it for layers the branch above takes
+    return fail(h, FR_ERR_HIP, "internal: channel-blocked activations outside the serving conv kernel");
   // Tile per layer shape, from tools/conv_sweep.py on MI355X at B=256 with the stream-K
   // schedule (profiles/r01/sweep.txt): 8-wave 128x64 for the 64-channel
   // stage and the 128-channel residual convs, 8-wave 128x128 for the 1x1 shortcuts,
@@ -677,13 +680,38 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
   int cur = 0, HW = 112;
   struct Y2Scope {
     fr_handle* h;
-    ~Y2Scope() { h->convs_y2 = nullptr; }
+    ~Y2Scope() {
+      h->convs_y2 = nullptr;
+      h->convs_blk = 0;
+    }
   } y2_scope{h};
   bool pre_done = false;  // the previous conv2 wrote this block's pre-BN input into L[0].sc_buf
+  // Which activations are channel-blocked: in a one-lane serving forward, those passed between
+  // two layers that run_conv puts on the serving conv kernel (same rule as its branch).
+  const size_t nb = h->blocks.size();
+  std::vector<char> all_convs(nb, 0), out_blk(nb, 0);
+  {
+    const bool serving = nl == 1 && h->convs_blocked && cnt[0] <= h->convs_max_n && !h->detector &&
+                         h->prec == PREC_F32;
+    auto on_convs = [&](const ConvW& c, int hw) { return serving && c.w_frag && (long long)cnt[0] * hw * hw <= 1024; };
+    std::vector<char> conv2_convs(nb, 0);
+    int hw = 112;
+    for (size_t bi = 0; bi < nb; ++bi) {
+      const BlockW& b = h->blocks[bi];
+      const bool fused = b.has_sc_conv && h->fuse_shortcut && b.conv2_sc.w;
+      const int ho = hw / b.spec.stride;
+      conv2_convs[bi] = (fused || !b.has_sc_conv) && on_convs(fused ? b.conv2_sc : b.conv2, ho);
+      all_convs[bi] = conv2_convs[bi] && on_convs(b.conv1, hw);
+      hw = ho;
+    }
+    for (size_t bi = 0; bi + 1 < nb; ++bi) out_blk[bi] = conv2_convs[bi] && all_convs[bi + 1];
+  }
   for (size_t bi = 0; bi < h->blocks.size(); ++bi) {
     const BlockW& b = h->blocks[bi];
     const int nxt = cur == 0 ? 1 : 0;
     const int Ho = HW / b.spec.stride;
+    const bool in_blk = bi > 0 && out_blk[bi - 1], r_blk = all_convs[bi];
+    h->convs_blk = (in_blk ? CONVS_BLK_X : 0) | (r_blk ? CONVS_BLK_Y : 0);
     for (int l = 0; l < nl; ++l) {
       int rc;
       if (pre_done) {
@@ -705,6 +733,7 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
     const bool fused = b.has_sc_conv && h->fuse_shortcut && b.conv2_sc.w;
     h->convs_y2 = nullptr;
     h->convs_y2_done = false;
+    h->convs_blk = (r_blk ? CONVS_BLK_X : 0) | (in_blk ? CONVS_BLK_X2 | CONVS_BLK_RES : 0) | (out_blk[bi] ? CONVS_BLK_Y : 0);
     if (nl == 1 && h->convs_pre_epilogue && bi + 1 < h->blocks.size() && (fused || !b.has_sc_conv) &&
         h->blocks[bi + 1].conv1.pre_scale && (size_t)Ho * Ho * b.spec.depth <= (size_t)56 * 56 * 64) {
       h->convs_y2 = L[0].sc_buf;
@@ -733,6 +762,7 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
     pre_done = h->convs_y2_done;
     h->convs_y2 = nullptr;
     h->convs_y2_done = false;
+    h->convs_blk = 0;
     cur = nxt;
     HW = Ho;
   }
@@ -2259,6 +2289,14 @@ int frt_set_small_conv_pre_epilogue(fr_handle* h, int on) {
   std::lock_guard<std::mutex> lk(h->mu);
   DeviceGuard dg(h->device);
   h->convs_pre_epilogue = on != 0;
+  clear_graphs(h);
+  return FR_OK;
+}
+int frt_set_small_conv_blocked(fr_handle* h, int on) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  DeviceGuard dg(h->device);
+  h->convs_blocked = on != 0;
   clear_graphs(h);
   return FR_OK;
 }

@@ -204,6 +204,10 @@ struct fr_handle {
   const float *convs_y2_scale = nullptr, *convs_y2_shift = nullptr;
   bool convs_y2_done = false;
   bool convs_pre_epilogue = true;
+  // activations passed between two serving-kernel layers of a one-lane forward are channel-blocked
+  // (ConvParams::blk; forward_lanes sets convs_blk per launch); frt_set_small_conv_blocked: A/B
+  int convs_blk = 0;
+  bool convs_blocked = true;
   bool chain_collect = false;
   int chain_seq = 0;  // index of the next run in the current forward
   std::vector<frhip::W4Link> chain_pending;

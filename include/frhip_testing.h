@@ -72,6 +72,9 @@ int frt_set_small_conv(fr_handle* h, int max_n);
 /* A/B switch (default on): in a one-lane forward, a body conv2 on the serving kernel also writes
  * BN(y) for the next block's conv1 (its pre-activation BN), which then runs without pre-BN. */
 int frt_set_small_conv_pre_epilogue(fr_handle* h, int on);
+/* A/B switch (default on): in a one-lane forward, activations passed between two layers on the
+ * serving kernel are stored channel-blocked ([n][C/16][H][W][16]) instead of NHWC. */
+int frt_set_small_conv_blocked(fr_handle* h, int on);
 /* The serving-batch kernel alone: y = epi(conv3x3 pad 1 stride s (x) [+ conv1x1 stride s (x2)
  * against weight columns 9*cin .. + cin2]), w [cout][9*cin + cin2]; pre-BN only with epi 1;
  * epi 0, 1, 2 (res shaped like y) or 3 (res [B][H][W][cout], read at (s oy, s ox)).

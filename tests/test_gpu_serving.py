@@ -208,6 +208,42 @@ def test_pre_bn_in_previous_epilogue_is_bitwise_the_per_tap_form(embedder):
         assert L.frt_set_small_conv(h.h, 1) == 0
 
 
+def test_channel_blocked_activations_are_bitwise_nhwc(embedder):
+    """Between two layers on the serving conv kernel, activations are stored channel-blocked
+    ([n][C/16][H][W][16], frt_set_small_conv_blocked, default on); layers on other kernels (stage
+    1's F(4x4), the head) keep NHWC.  Only addresses change, so the embeddings are bitwise those of
+    the all-NHWC forward: n = 1 and 4 (serving path up to 4 crops), with and without the pre-BN
+    epilogue, eager and graph-replayed."""
+    from tests import _frt
+
+    L = _frt.lib()
+    h = embedder.model
+    crops = torch.from_numpy(W.synthetic_crops(4, seed=W.CROP_SEED_GALLERY)).cuda()
+    try:
+        for pre in (1, 0):
+            assert L.frt_set_small_conv_pre_epilogue(h.h, pre) == 0
+            for n, max_n in ((1, 1), (4, 4)):
+                assert L.frt_set_small_conv(h.h, max_n) == 0
+                assert L.frt_set_small_conv_blocked(h.h, 0) == 0
+                ref = embedder.embed_tensor(crops[:n]).clone()
+                assert L.frt_set_small_conv_blocked(h.h, 1) == 0
+                got = embedder.embed_tensor(crops[:n])
+                assert torch.equal(got, ref), (pre, n, (got - ref).abs().max().item())
+        assert L.frt_set_small_conv(h.h, 1) == 0
+        assert L.frt_set_small_conv_pre_epilogue(h.h, 1) == 0
+        assert L.frt_set_small_conv_blocked(h.h, 0) == 0
+        nhwc = embedder.embed_tensor(crops[:1]).clone()
+        assert L.frt_set_small_conv_blocked(h.h, 1) == 0
+        h.set_graph_batch(1)
+        for _ in range(3):  # eager + capture, then replays
+            assert torch.equal(embedder.embed_tensor(crops[:1]), nhwc)
+    finally:
+        h.set_graph_batch(0)
+        assert L.frt_set_small_conv_blocked(h.h, 1) == 0
+        assert L.frt_set_small_conv_pre_epilogue(h.h, 1) == 0
+        assert L.frt_set_small_conv(h.h, 1) == 0
+
+
 def test_small_batches_match_oracle(embedder):
     """Serving batch sizes take the split-K F(4x4) path and small stream-K grids: every
     embedding stays within the pipeline's 1e-5 bar of the CPU oracle."""

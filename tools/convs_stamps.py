@@ -50,10 +50,10 @@ def build(spread=False):
         ("  if (w != 0) return;\n",
          "  if (w != 0) return;\n  T4 = __builtin_amdgcn_s_memrealtime();\n"),
         ("  if (!mval) return;\n", ""),
-        ("  *reinterpret_cast<f4*>(p.y + (long long)mm * Cout + c4) = v;\n",
-         "  if (mval) *reinterpret_cast<f4*>(p.y + (long long)mm * Cout + c4) = v;\n"),
-        ("  if (p.y2) *reinterpret_cast<f4*>(p.y2 + (long long)mm * Cout + c4) = __builtin_elementwise_fma(v, e_s2, e_t2);\n}",
-         "  if (p.y2 && mval) *reinterpret_cast<f4*>(p.y2 + (long long)mm * Cout + c4) = __builtin_elementwise_fma(v, e_s2, e_t2);\n"
+        ("  __builtin_amdgcn_raw_buffer_store_b128(bits4(v), rsrc(p.y, ybytes), yoff * 4, 0, CPOL_SC1);\n  if (p.y2)\n",
+         "  if (mval) __builtin_amdgcn_raw_buffer_store_b128(bits4(v), rsrc(p.y, ybytes), yoff * 4, 0, CPOL_SC1);\n  if (p.y2 && mval)\n"),
+        ("                                           0, CPOL_SC1);\n}",
+         "                                           0, CPOL_SC1);\n"
          "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
          "  if (lane == 0) {\n"
          "    const unsigned long long T5 = __builtin_amdgcn_s_memrealtime();\n"
