@@ -64,7 +64,7 @@ int frt_set_s2_band(int on);
  * Asynchronous on stream. */
 int frt_conv2d_s2band(const float* x, const float* w, float* y, int B, int H, int W, const float* post_scale,
                       const float* post_shift, const float* res, void* stream);
-/* Handle h runs every body 3x3 conv of forwards of n <= max_n crops (default 1; 0 = never) on the
+/* Handle h runs every body 3x3 conv of forwards of n <= max_n crops (default 2; 0 = never) on the
  * serving-batch kernel (conv_small.hip: one launch per layer, 16 pixels x 16 couts per workgroup
  * with the whole K reduction inside it) instead of F(4x4) split-K + fixup and the split-K direct
  * convs.  Drops captured graphs. */

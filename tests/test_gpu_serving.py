@@ -145,12 +145,12 @@ def test_chained_layers_bit_identical_to_per_layer_launches(embedder):
     finally:
         h.set_graph_batch(0)
         assert L.frt_set_wino4_chain(h.h, 0) == 0
-        assert L.frt_set_small_conv(h.h, 1) == 0
+        assert L.frt_set_small_conv(h.h, 2) == 0  # the default
 
 
 def test_serving_conv_path_vs_winograd_path(embedder):
     """Batch 1 runs every body 3x3 conv on conv_small.hip's kernel (frt_set_small_conv, default
-    n <= 1); with it off the same forward takes the F(4x4) split-K + fixup and split-K direct
+    n <= 2); with it off the same forward takes the F(4x4) split-K + fixup and split-K direct
     path.  Both are f32 with exact products: embeddings agree within the pipeline's 1e-5 bar, and
     each path is run-to-run deterministic (also under graph replay)."""
     from tests import _frt
@@ -173,7 +173,7 @@ def test_serving_conv_path_vs_winograd_path(embedder):
             assert torch.equal(embedder.embed_tensor(crops[:1]), one)
     finally:
         h.set_graph_batch(0)
-        assert L.frt_set_small_conv(h.h, 1) == 0
+        assert L.frt_set_small_conv(h.h, 2) == 0  # the default
 
 
 def test_pre_bn_in_previous_epilogue_is_bitwise_the_per_tap_form(embedder):
@@ -205,7 +205,7 @@ def test_pre_bn_in_previous_epilogue_is_bitwise_the_per_tap_form(embedder):
     finally:
         h.set_graph_batch(0)
         assert L.frt_set_small_conv_pre_epilogue(h.h, 1) == 0
-        assert L.frt_set_small_conv(h.h, 1) == 0
+        assert L.frt_set_small_conv(h.h, 2) == 0  # the default
 
 
 def test_channel_blocked_activations_are_bitwise_nhwc(embedder):
@@ -241,7 +241,7 @@ def test_channel_blocked_activations_are_bitwise_nhwc(embedder):
         h.set_graph_batch(0)
         assert L.frt_set_small_conv_blocked(h.h, 1) == 0
         assert L.frt_set_small_conv_pre_epilogue(h.h, 1) == 0
-        assert L.frt_set_small_conv(h.h, 1) == 0
+        assert L.frt_set_small_conv(h.h, 2) == 0  # the default
 
 
 def test_small_batches_match_oracle(embedder):
