@@ -354,6 +354,12 @@ int chain_flush(fr_handle* h, hipStream_t s) {
   return FR_OK;
 }
 
+// serving conv kernel: layers of at most this many output pixels (n * Ho * Wo).  Batch 1 also
+// takes stage 1's 56x56 layers (1.045 vs 1.064-1.077 ms per embed + match); at batch 2 their
+// 6,272 pixels, and stage 2's 1,568, are faster on F(4x4) split-K (1.50 vs 1.52-1.54 ms with
+// 4,096; profiles/r04/serving/pixel_threshold_ab.txt)
+static inline long long convs_max_m(int n) { return n == 1 ? 4096 : 1024; }
+
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
              const LaneWs* L, const float* x2) {
@@ -409,9 +415,9 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   const double flop = 2.0 * p.M * (double)p.Cout * (cw.kh * cw.kw * cw.cin + cw.cin2);
   // serving batches (n <= convs_max_n): every body 3x3 conv as one launch with the whole K per
   // 16x16 tile (conv_small.hip); f32 parity path only
-  // (layers of at most 1024 output pixels: stage 1's 56x56 and 112x112 maps, 196 / 784 pixel
-  // blocks x 4 cout blocks, stay on F(4x4) split-K, which is faster there: 54 vs ~20 us at @112)
-  if (B <= h->convs_max_n && p.M <= 1024 && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.w_frag &&
+  // (layers of at most convs_max_m(B) output pixels: stage 1's 112x112 conv1, 784 pixel blocks
+  // x 4 cout blocks, stays on F(4x4) split-K, which is faster there: 54 vs ~20 us)
+  if (B <= h->convs_max_n && p.M <= convs_max_m(B) && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.w_frag &&
       convs_supported(p, cw.pre_scale != nullptr, epi)) {
     p.w = cw.w_frag;
     if (int rc = chain_flush(h, s)) return rc;
@@ -693,7 +699,7 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
   {
     const bool serving = nl == 1 && h->convs_blocked && cnt[0] <= h->convs_max_n && !h->detector &&
                          h->prec == PREC_F32;
-    auto on_convs = [&](const ConvW& c, int hw) { return serving && c.w_frag && (long long)cnt[0] * hw * hw <= 1024; };
+    auto on_convs = [&](const ConvW& c, int hw) { return serving && c.w_frag && (long long)cnt[0] * hw * hw <= convs_max_m(cnt[0]); };
     std::vector<char> conv2_convs(nb, 0);
     int hw = 112;
     for (size_t bi = 0; bi < nb; ++bi) {
