@@ -354,11 +354,11 @@ int chain_flush(fr_handle* h, hipStream_t s) {
   return FR_OK;
 }
 
-// serving conv kernel: layers of at most this many output pixels (n * Ho * Wo).  4,096 at batch 1
-// (stage 1's 56x56 layers too) measured 1.045 vs 1.064-1.077 ms per embed + match, at batch 2
-// 1.52-1.54 vs 1.50 (profiles/r04/serving/pixel_threshold_ab.txt); not switched on yet: the
-// full GPU suite (single-image vs batch bars of 1e-6) has not run on it
-static inline long long convs_max_m(int) { return 1024; }
+// serving conv kernel: layers of at most this many output pixels (n * Ho * Wo).  Batch 1 also
+// takes stage 1's 56x56 layers (1.045 vs 1.064-1.077 ms per embed + match); at batch 2 their
+// 6,272 pixels, and stage 2's 1,568, are faster on F(4x4) split-K (1.50 vs 1.52-1.54 ms with
+// 4,096; profiles/r04/serving/pixel_threshold_ab.txt)
+static inline long long convs_max_m(int n) { return n == 1 ? 4096 : 1024; }
 
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
