@@ -6,8 +6,8 @@ match of a batch of 256 synthetic 112x112 crops per GPU against a 1k-row
 gallery.  One "step" = one ``fr_embed_match`` over the rank's batch, inputs
 already resident in HBM.  For N>1 there is one rank per GPU: ``--gpus N`` starts
 the N rank processes itself (fresh children, before this process touches the
-GPU), or runs as one of them under ``torchrun`` (WORLD_SIZE set, which must
-equal N).  Rank 0 embeds the gallery and broadcasts it over RCCL (the path's
+GPU), or runs as one of them under ``torchrun`` (WORLD_SIZE set; ``--gpus``
+may then be omitted, and must equal WORLD_SIZE when given).  Rank 0 embeds the gallery and broadcasts it over RCCL (the path's
 only exchange step); each rank then processes its own probes independently
 (weak scaling: N x batch faces per step).
 
@@ -19,6 +19,9 @@ Also reported:
                 The events are recorded in a second timed pass of the same K steps
                 (ms_per_step_profiled_pass): an event pair around every launch adds
                 ~0.8 ms per IR-101 step, so the throughput pass runs without them.
+  gallery_exchange (N > 1)  the broadcast's bytes, ms (first, and median of
+                --exchange-reps repeats) and GB/s, max over ranks; plus the fastest and
+                slowest rank's ms/step (rank_ms_per_step_min/max)
   cpu_baseline  the oracle (PyTorch-CPU IR-101 + reference-style per-probe
                 search) on rank 0's host cores, on a bounded sample.
 """
@@ -46,8 +49,9 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1,
-                    help="ranks, one per GPU: started here as child processes unless torchrun already did")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default 1, or WORLD_SIZE under torchrun): started here as child "
+                         "processes unless torchrun already did")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
     ap.add_argument("--same-gpu", action="store_true",
@@ -77,6 +81,8 @@ def parse():
                     help="a forward of n >= 2x this many crops runs as two concurrent halves (0: one lane; default: library's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--exchange-reps", type=int, default=3,
+                    help="N > 1: timed repeats of the gallery broadcast after the real one (steady-state rate)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per conv launch (tools/prof_summary.py --json); "
                          "default: the newest profiles/r*/layers_pmc.json")
@@ -216,22 +222,79 @@ def c4_inputs(n_faces, per_frame, dev, seed=7):
     return frames, lms
 
 
+def count_gpus():
+    """GPUs this process may use, counted WITHOUT initialising HIP (the launcher must not touch the
+    GPU before it starts the rank processes): the KFD topology's GPU nodes (gpu_id != 0) whose DRM
+    render node is openable here (a container exposes a subset), else amdsmi; capped by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.  None if neither source
+    works (the caller refuses to launch rather than fall back to a HIP-initialising count)."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = None
+    if os.path.isdir(base):
+        n = 0
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "gpu_id")) as f:
+                    if int(f.read().strip() or 0) == 0:
+                        continue  # a CPU node
+                minor = None
+                with open(os.path.join(base, node, "properties")) as f:
+                    for line in f:
+                        if line.startswith("drm_render_minor"):
+                            minor = int(line.split()[1])
+            except (OSError, ValueError, IndexError):
+                continue
+            if minor is not None and minor > 0 and not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+                continue
+            n += 1
+    else:
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            try:
+                n = len(amdsmi.amdsmi_get_processor_handles())
+            finally:
+                amdsmi.amdsmi_shut_down()
+        except Exception:  # noqa: BLE001 -- no library / no driver: the count is unknown
+            n = None
+    if n is None:
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
+def resolve_world(gpus, env) -> int:
+    """Ranks this run has: WORLD_SIZE under torchrun (``--gpus``, when given, must agree), else
+    ``--gpus`` (default 1).  Exits non-zero on a disagreement."""
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if gpus is not None and gpus != world:
+            sys.exit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}")
+        return world
+    return 1 if gpus is None else gpus
+
+
 def launch_ranks(args) -> int:
     """``--gpus N`` without torchrun: start N fresh rank processes (RANK / LOCAL_RANK / WORLD_SIZE /
     MASTER_* in their environment, the same argv) and return the first non-zero exit code, else 0.
 
-    Runs before anything here touches the GPU: ``torch.cuda.device_count()`` counts devices without
-    initialising HIP on this image, and the children are started as new processes (never exec'd
-    from this one).  Rank 0's stdout is this process's stdout, so the one JSON line comes through.
+    Runs before anything here touches the GPU: ``count_gpus`` reads the KFD topology (or amdsmi),
+    never HIP, and the children are started as new processes (never exec'd from this one).  Rank
+    0's stdout is this process's stdout, so the one JSON line comes through.
     """
     import signal
     import socket
     import subprocess
     n = args.gpus
-    visible = torch.cuda.device_count()
+    if args.same_gpu and args.dist_backend != "gloo":
+        sys.exit("bench.py: --same-gpu needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
+    visible = count_gpus()
+    if visible is None:
+        sys.exit("bench.py: cannot count the visible GPUs (no KFD topology, no amdsmi); refusing to launch ranks")
     if args.same_gpu:
-        if args.dist_backend != "gloo":
-            sys.exit("bench.py: --same-gpu needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
         if visible < 1:
             sys.exit("bench.py: --same-gpu needs one visible GPU, found none")
     elif n > visible:
@@ -286,13 +349,12 @@ def main():
     arch0, gal0 = PRESETS[args.config]
     args.arch = args.arch or arch0
     args.gallery = gal0 if args.gallery is None else args.gallery
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    world = resolve_world(args.gpus, os.environ)
+    if "WORLD_SIZE" not in os.environ and world > 1:
+        args.gpus = world
         sys.exit(launch_ranks(args))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.same_gpu and args.dist_backend != "gloo":
         sys.exit("bench.py: --same-gpu needs --dist-backend gloo")
     if args.same_gpu:
@@ -320,9 +382,34 @@ def main():
         gallery = emb.embed_tensor(torch.from_numpy(gal_crops).to(dev))
         if G > G0:
             gallery = torch.from_numpy(W.expand_gallery(gallery.cpu().numpy(), G)).to(dev)
+    exchange = None
     if world > 1 and G > 0:
         from facerecognitionpipeline_amd.distributed import broadcast_gallery
-        gallery = broadcast_gallery(gallery, G, dev, src=0)
+        red_dev = dev if args.dist_backend == "nccl" else "cpu"
+
+        def timed_broadcast(src_tensor):
+            # every rank enters together (the barrier also brings up the communicator, so its setup
+            # is not in the time); host clock around the collective + device syncs, max over ranks
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = broadcast_gallery(src_tensor, G, dev, src=0)
+            torch.cuda.synchronize()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return out, t.item()
+
+        gallery, t_first = timed_broadcast(gallery)
+        reps = [timed_broadcast(gallery if rank == 0 else None)[1] for _ in range(max(0, args.exchange_reps))]
+        nbytes = G * 512 * 4
+        t_ss = float(np.median(reps)) if reps else t_first
+        exchange = {"collective": "broadcast", "backend": "rccl" if args.dist_backend == "nccl" else "gloo",
+                    "bytes": nbytes, "ms": round(t_first * 1e3, 3),
+                    "ms_steady": round(t_ss * 1e3, 3), "reps": len(reps),
+                    # bytes delivered to the N-1 receiving ranks per second, and per receiving rank
+                    # (= per xGMI link for a fan-out from rank 0; a ring's bus bandwidth likewise)
+                    "GBps_aggregate": round(nbytes * (world - 1) / t_ss / 1e9, 3),
+                    "GBps_per_receiver": round(nbytes / t_ss / 1e9, 3)}
     if G > 0:
         emb.model.gallery_set(gallery)
 
@@ -400,14 +487,19 @@ def main():
             dist.barrier()
         t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
                          device=dev if args.dist_backend == "nccl" else "cpu")
+        tmin = t.clone()
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
+        rank_spread[:] = [tmin.item(), t.item()]
         return t.item()
 
     # throughput: the K steps with nothing else on the queue; then the same K steps again with a
     # HIP event pair around every launch (fr_profile_*) for the per-kernel roofline -- the event
     # records add ~0.8 ms per IR-101 step, so they stay out of the throughput pass
+    rank_spread = [0.0, 0.0]
     tmax = timed_steps()
+    rank_ms = [round(x / args.steps * 1e3, 3) for x in rank_spread]
     emb.model.profile_enable(True)
     emb.model.profile_read()
     tprof = timed_steps()
@@ -539,6 +631,14 @@ def main():
             "top1_self_match": top1_ok,
             "roofline": roofline,
         }
+        if world > 1:
+            # the fastest and the slowest rank's timed region (value uses the slowest)
+            out["rank_ms_per_step_min"], out["rank_ms_per_step_max"] = rank_ms
+            # the path's only collective, outside the timed region: the G x 512 gallery broadcast
+            out["gallery_exchange"] = exchange
+            if exchange is not None:
+                out["gallery_exchange_ms"] = exchange["ms"]
+                out["gallery_exchange_GBps"] = exchange["GBps_aggregate"]
         if world == 1 and not args.no_cpu_baseline and args.model_type == "adaface":
             gnp = gallery.cpu().numpy() if G > 0 else np.zeros((0, 512), np.float32)
             if args.config == "c4":

@@ -17,15 +17,26 @@ full re-upload; ``pending_delta`` gives the same delta to ship to other GPUs
 once on the GPU (``fr_build_templates``: quality filter + mean / median /
 weighted_mean + L2, ``:104-122``, ``:297-317``).
 
-Persistence uses JSON + ``.npz`` (no pickle); ``load_backup`` reads the
-reference's ``export_for_backup`` JSON (``:246-270``).
+Persistence: ``save`` writes one ``.npz`` (every array and, as a JSON string,
+every record's fields: a single atomic file) plus the reference's own
+informational ``.json`` sidecar (same keys as ``:211-229``; nothing reads it
+back).  ``load`` reads that ``.npz`` or the REFERENCE's gallery pickle
+(``pickle.dump(self.students)``, ``:207-210,234-244``) through a restricted
+unpickler that resolves only numpy's array reconstruction and the reference's
+``StudentRecord`` (mapped onto this module's dataclass) and executes nothing
+else from the file; an unreadable or foreign pickle raises, it never turns into
+an empty gallery.  ``load_backup`` reads the reference's ``export_for_backup``
+JSON (``:246-270``).
 """
 from __future__ import annotations
 
 import copy
+import importlib
 import json
 import os
+import pickle
 import shutil
+import tempfile
 import threading
 import uuid
 from dataclasses import dataclass, field
@@ -65,6 +76,88 @@ class StudentRecord:
                    template_embedding=np.array(d["template_embedding"]), num_samples=d["num_samples"],
                    enrollment_date=d["enrollment_date"], last_updated=d["last_updated"],
                    metadata=d.get("metadata", {}) or {})
+
+
+# -- the reference's gallery pickle (gallery_manager.py:207-210 dump, :234-244 load) ----------
+class _PickledRecord:
+    """Receives the attributes of a pickled reference ``StudentRecord``; no code of the file runs
+    (pickle's NEWOBJ + BUILD only create the instance and fill its ``__dict__``)."""
+
+
+# globals a reference gallery pickle may name: numpy's array / dtype / scalar reconstruction
+# (numpy 1.x ``numpy.core`` and 2.x ``numpy._core`` spellings) and the reference's record class
+# (``gallery_manager.StudentRecord``, or ``__main__.StudentRecord`` when the reference module ran
+# as a script, gallery_manager.py:333-362)
+_NUMPY_GLOBALS = {
+    ("numpy", "ndarray"), ("numpy", "dtype"),
+    ("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+    ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+    ("numpy.core.numeric", "_frombuffer"), ("numpy._core.numeric", "_frombuffer"),
+}
+_RECORD_GLOBALS = {("gallery_manager", "StudentRecord"), ("__main__", "StudentRecord")}
+
+
+class _GalleryUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        if (module, name) in _RECORD_GLOBALS:
+            return _PickledRecord
+        if (module, name) in _NUMPY_GLOBALS:
+            if module == "numpy":
+                return getattr(np, name)
+            tail = module.split(".", 2)[2]  # multiarray / numeric, under whichever core this numpy has
+            for core in ("numpy._core", "numpy.core"):
+                try:
+                    return getattr(importlib.import_module(f"{core}.{tail}"), name)
+                except (ImportError, AttributeError):
+                    continue
+        raise pickle.UnpicklingError(f"gallery pickle names a global outside the whitelist: {module}.{name}")
+
+
+def _float_array(v, what: str) -> np.ndarray:
+    if not isinstance(v, np.ndarray) or v.dtype.kind != "f":
+        raise ValueError(f"gallery pickle: {what} is not a float array")
+    return v
+
+
+def load_reference_pickle(path: str) -> Dict[str, "StudentRecord"]:
+    """The ``Dict[str, StudentRecord]`` the reference's ``save`` pickled, as this module's records.
+    Raises ``pickle.UnpicklingError`` for a global outside the whitelist and ``ValueError`` for
+    anything that is not such a dict of records."""
+    with open(path, "rb") as f:
+        obj = _GalleryUnpickler(f).load()
+    if not isinstance(obj, dict):
+        raise ValueError(f"gallery pickle {path}: top level is {type(obj).__name__}, not a dict of StudentRecord")
+    out: Dict[str, StudentRecord] = {}
+    for sid, r in obj.items():
+        if not isinstance(r, _PickledRecord):
+            raise ValueError(f"gallery pickle {path}: entry {sid!r} is {type(r).__name__}, not a StudentRecord")
+        d = r.__dict__
+        try:
+            emb = _float_array(d["embeddings"], f"{sid} embeddings")
+            tpl = _float_array(d["template_embedding"], f"{sid} template_embedding")
+            rec = StudentRecord(str(d["student_id"]), str(d["name"]), emb, tpl, int(d["num_samples"]),
+                                str(d["enrollment_date"]), str(d["last_updated"]), d.get("metadata") or {})
+        except KeyError as e:
+            raise ValueError(f"gallery pickle {path}: record {sid!r} lacks field {e}") from None
+        if not isinstance(rec.metadata, dict):
+            raise ValueError(f"gallery pickle {path}: record {sid!r} metadata is not a dict")
+        out[sid] = rec
+    return out
+
+
+def _atomic_write(path: str, write) -> None:
+    """``write(fileobj)`` into a uniquely named temporary in ``path``'s directory, then rename it
+    over ``path``: readers see the old file or the new one, and concurrent savers (other managers,
+    other processes) never share a temporary."""
+    fd, tmp = tempfile.mkstemp(prefix=os.path.basename(path) + ".", suffix=".tmp", dir=os.path.dirname(path) or ".")
+    try:
+        with os.fdopen(fd, "wb") as f:
+            write(f)
+        os.replace(tmp, path)
+    except BaseException:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+        raise
 
 
 def _slice_len(n: int, top_k: int) -> int:
@@ -152,7 +245,7 @@ class GalleryManager:
     def __init__(self, gallery_path: Optional[str] = None, aggregation_method: str = "mean", device=None,
                  verbose: bool = True):
         if gallery_path is None:
-            gallery_path = str(SCRIPT_DIR / "gallery" / "students.npz")
+            gallery_path = str(SCRIPT_DIR / "gallery" / "students.pkl")  # the reference's default name (:57-58)
         self.gallery_path = gallery_path
         self.aggregation_method = aggregation_method
         self.students: Dict[str, StudentRecord] = {}
@@ -170,8 +263,8 @@ class GalleryManager:
         self._lock = threading.RLock()
         self._save_lock = threading.Lock()  # one save() at a time: snapshot + both files, in order
         os.makedirs(os.path.dirname(gallery_path) or ".", exist_ok=True)
-        if os.path.exists(self._arrays_path(gallery_path)):
-            self.load()
+        if self._source(gallery_path) is not None:
+            self.load()  # raises on a file it cannot read: never an empty gallery in its place
             self._log(f"Loaded gallery with {len(self.students)} students")
         else:
             self._log("Initialized empty gallery")
@@ -386,11 +479,35 @@ class GalleryManager:
         root, _ext = os.path.splitext(path)
         return root + ".npz"
 
+    @staticmethod
+    def _pickle_path(path: str) -> str:
+        root, _ext = os.path.splitext(path)
+        return root + ".pkl"
+
+    @classmethod
+    def _source(cls, path: str) -> Optional[Tuple[str, str]]:
+        """What ``load(path)`` reads: ("npz", file) -- this module's save -- or ("pkl", file) -- the
+        reference's ``pickle.dump(self.students)`` (gallery_manager.py:207-210), or None.  When both
+        exist (a reference gallery saved here since), the more recently written one."""
+        npz, pkl = cls._arrays_path(path), cls._pickle_path(path)
+        have_npz, have_pkl = os.path.exists(npz), os.path.exists(pkl)
+        if have_npz and have_pkl:
+            return ("pkl", pkl) if os.path.getmtime(pkl) > os.path.getmtime(npz) else ("npz", npz)
+        if have_npz:
+            return "npz", npz
+        if have_pkl:
+            return "pkl", pkl
+        return None
+
     def save(self, path: Optional[str] = None) -> None:
+        """Write ``<stem>.npz`` (templates, samples and every record field: the whole gallery in
+        one file, replaced atomically) and the reference's informational ``<stem>.json`` sidecar in
+        the reference's own format (gallery_manager.py:211-229).  A reference ``.pkl`` at the path
+        is left untouched; ``load`` then prefers the newer ``.npz``."""
         path = path or self.gallery_path
-        # _save_lock orders whole saves (the later snapshot lands last, and no save interleaves its
-        # .npz with another's .json); the snapshot itself is taken under the gallery lock, so
-        # enrollment is blocked only while it is copied, not while the files are written
+        # _save_lock orders whole saves of this manager (the later snapshot lands last); unique
+        # temporaries keep saves of other managers / processes from mixing; the snapshot itself is
+        # taken under the gallery lock, so enrollment is blocked only while it is copied
         with self._save_lock:
             with self._lock:
                 ids = list(self.students.keys())
@@ -398,36 +515,44 @@ class GalleryManager:
                 for i, s in enumerate(ids):
                     arrays[f"e{i}"] = np.array(self.students[s].embeddings)
                     arrays[f"t{i}"] = np.array(self.students[s].template_embedding)
-                meta = {"num_students": len(ids), "last_saved": datetime.now().isoformat(), "order": ids,
-                        "students": {s: {"student_id": r.student_id, "name": r.name, "num_samples": r.num_samples,
-                                         "enrollment_date": r.enrollment_date, "last_updated": r.last_updated,
-                                         "metadata": copy.deepcopy(r.metadata)} for s, r in self.students.items()}}
-            # both files written to temporaries first and then renamed, so a reader never sees a
-            # half-written file (a crash between the two renames can still pair a new .npz with the
-            # previous .json; load() then fails on the missing e{i}/t{i} or ids)
-            npz, js = self._arrays_path(path), os.path.splitext(path)[0] + ".json"
-            with open(npz + ".tmp", "wb") as f:
-                np.savez(f, **arrays)
-            with open(js + ".tmp", "w") as f:
-                json.dump(meta, f, indent=2)
-            os.replace(npz + ".tmp", npz)
-            os.replace(js + ".tmp", js)
+                now = datetime.now().isoformat()
+                fields = {s: {"student_id": r.student_id, "name": r.name, "num_samples": r.num_samples,
+                              "enrollment_date": r.enrollment_date, "last_updated": r.last_updated,
+                              "metadata": copy.deepcopy(r.metadata)} for s, r in self.students.items()}
+            meta = {"format": "frhip-gallery-1", "order": ids, "students": fields}
+            os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+            arrays["meta"] = np.array(json.dumps(meta))
+            _atomic_write(self._arrays_path(path), lambda f: np.savez(f, **arrays))
+            sidecar = {"num_students": len(ids), "last_saved": now, "students": fields}
+            _atomic_write(os.path.splitext(path)[0] + ".json",
+                          lambda f: f.write(json.dumps(sidecar, indent=2).encode()))
 
     def load(self, path: Optional[str] = None) -> None:
+        """Load ``<stem>.npz`` or the reference's ``<stem>.pkl`` (``_source``); a path with neither
+        logs and keeps the current records, as the reference does (gallery_manager.py:237-239)."""
         with self._lock:
             path = path or self.gallery_path
-            arr_path = self._arrays_path(path)
-            if not os.path.exists(arr_path):
-                self._log(f"Gallery file not found: {arr_path}")
+            src = self._source(path)
+            if src is None:
+                self._log(f"Gallery file not found: {path}")
                 return
-            with open(os.path.splitext(path)[0] + ".json") as f:
-                meta = json.load(f)
-            arrays = np.load(arr_path)
-            self.students = {}
-            for i, s in enumerate(meta["order"]):
-                m = meta["students"][s]
-                self.students[s] = StudentRecord(s, m["name"], arrays[f"e{i}"], arrays[f"t{i}"], m["num_samples"],
-                                                 m["enrollment_date"], m["last_updated"], m.get("metadata", {}))
+            kind, fpath = src
+            if kind == "pkl":
+                self.students = load_reference_pickle(fpath)
+            else:
+                with np.load(fpath) as arrays:
+                    if "meta" in arrays.files:
+                        meta = json.loads(str(arrays["meta"]))
+                    else:  # a round-4 save: fields in the .json beside it
+                        with open(os.path.splitext(fpath)[0] + ".json") as f:
+                            meta = json.load(f)
+                    students = {}
+                    for i, s in enumerate(meta["order"]):
+                        m = meta["students"][s]
+                        students[s] = StudentRecord(s, m["name"], arrays[f"e{i}"], arrays[f"t{i}"],
+                                                    m["num_samples"], m["enrollment_date"], m["last_updated"],
+                                                    m.get("metadata", {}) or {})
+                self.students = students
             self._touch()
 
     def load_backup(self, json_path: str) -> None:

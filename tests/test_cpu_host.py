@@ -78,7 +78,7 @@ def test_gallery_records_and_templates(tmp_path, golden_dir):
     assert gm.delete_student(sid) and not gm.delete_student(sid)
     st = gm.get_statistics()
     assert st["num_students"] == 4
-    # save/load round trip (JSON + npz, no pickle)
+    # save/load round trip (one npz with every field)
     gm.save()
     gm2 = _gm(tmp_path)
     assert list(gm2.students) == list(gm.students)
@@ -104,6 +104,81 @@ def test_reference_backup_json_loads(tmp_path, golden_dir):
     gm.load_backup(str(p))
     E, _ = gm.get_gallery_embeddings()
     assert np.array_equal(E.astype(np.float32), f["stored_template"])
+
+
+def test_reference_gallery_pickle_loads(tmp_path, golden_dir):
+    """The reference's own gallery file (pickle.dump(self.students), gallery_manager.py:207-210),
+    written by the reference GalleryManager (tools/make_golden.py refpkl), loads through the
+    restricted unpickler: every record field, templates equal to the reference's own."""
+    import json
+    import shutil
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    f = np.load(os.path.join(golden_dir, "backup_adaface_ir_101.npz"))
+    d = tmp_path / "gallery"
+    d.mkdir()
+    shutil.copyfile(os.path.join(golden_dir, "ref_students.pkl"), d / "students.pkl")
+    shutil.copyfile(os.path.join(golden_dir, "ref_students.json"), d / "students.json")
+    ref_json = (d / "students.json").read_text()
+    gm = GalleryManager(gallery_path=str(d / "students.pkl"), verbose=False)
+    E, ids = gm.get_gallery_embeddings()
+    assert ids == [str(s) for s in f["student_ids"]]
+    assert np.array_equal(E, f["ref_template"])
+    meta = json.loads(ref_json)["students"]
+    for sid, r in gm.students.items():
+        assert r.name == meta[sid]["name"] and r.num_samples == meta[sid]["num_samples"] == 8
+        assert r.enrollment_date == meta[sid]["enrollment_date"] and r.metadata == meta[sid]["metadata"]
+        assert r.embeddings.shape == (8, 512)
+    # a save writes this module's .npz and the reference-format sidecar; the .pkl is never touched,
+    # and the next load takes the newer .npz
+    pkl_bytes = (d / "students.pkl").read_bytes()
+    assert gm.delete_student(ids[0])
+    gm.save()
+    assert (d / "students.pkl").read_bytes() == pkl_bytes
+    side = json.loads((d / "students.json").read_text())
+    assert set(side) == set(json.loads(ref_json)) and list(side["students"]) == ids[1:]
+    assert set(side["students"][ids[1]]) == set(meta[ids[1]])
+    gm2 = GalleryManager(gallery_path=str(d / "students.pkl"), verbose=False)
+    assert list(gm2.students) == ids[1:]
+    assert np.array_equal(gm2.get_gallery_embeddings()[0], f["ref_template"][1:])
+    assert not [p for p in os.listdir(d) if p.endswith(".tmp")]
+
+
+def test_gallery_pickle_with_foreign_globals_raises(tmp_path):
+    """A pickle naming anything outside numpy's array reconstruction and the reference's
+    StudentRecord raises before it is resolved; an unreadable gallery never loads as empty."""
+    import pickle
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    d = tmp_path / "g"
+    d.mkdir()
+    bad = [b"cos\nsystem\n(S'echo pwned > /dev/null'\ntR.",           # protocol 0 GLOBAL os.system
+           b"\x80\x04cbuiltins\neval\n(S'1+1'\ntR.",                 # builtins.eval
+           pickle.dumps({"S1": 3}),                                  # not a StudentRecord
+           pickle.dumps([1, 2]),                                     # not a dict
+           b"not a pickle at all"]
+    for i, blob in enumerate(bad):
+        (d / "students.pkl").write_bytes(blob)
+        with pytest.raises((pickle.UnpicklingError, ValueError, EOFError)):
+            GalleryManager(gallery_path=str(d / "students.pkl"), verbose=False)
+
+
+def test_save_uses_unique_temporaries_and_one_file(tmp_path):
+    """Two managers saving the same path concurrently each land a complete, loadable file."""
+    import threading
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    p = str(tmp_path / "s" / "students.npz")
+    rng = np.random.default_rng(3)
+    mgrs = []
+    for m in range(2):
+        gm = GalleryManager(gallery_path=str(tmp_path / f"src{m}" / "x.npz"), verbose=False)
+        for i in range(6 + m):
+            gm.add_student(f"S{m}{i}", f"N{i}", rng.standard_normal((2, 512)).astype(np.float32))
+        mgrs.append(gm)
+    ts = [threading.Thread(target=lambda g=g: [g.save(p) for _ in range(5)]) for g in mgrs]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    out = GalleryManager(gallery_path=p, verbose=False)
+    assert list(out.students) in ([f"S0{i}" for i in range(6)], [f"S1{i}" for i in range(7)])
+    assert not [q for q in os.listdir(tmp_path / "s") if q.endswith(".tmp")]
 
 
 def test_slice_semantics_of_top_k():

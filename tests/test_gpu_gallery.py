@@ -37,6 +37,29 @@ def test_build_templates_backup_kat(handle, name, golden_dir):
     assert np.abs(tpl - f["stored_template"]).max() <= 1e-7     # the committed templates
 
 
+def test_search_on_reference_gallery_pickle(tmp_path, golden_dir):
+    """The reference's own gallery file (tests/golden/ref_students.pkl, written by the reference
+    GalleryManager.save, gallery_manager.py:207-210) loaded through the restricted unpickler and
+    searched on the GPU: every stored sample's top-5 equals the reference search of the same
+    templates (backup_adaface_ir_101.npz, gallery_manager.py:189-205), scores within 1e-6."""
+    import shutil
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    f = np.load(os.path.join(golden_dir, "backup_adaface_ir_101.npz"))
+    shutil.copyfile(os.path.join(golden_dir, "ref_students.pkl"), tmp_path / "students.pkl")
+    gm = GalleryManager(gallery_path=str(tmp_path / "students.pkl"), device="cuda:0", verbose=False)
+    q = f["embeddings"].reshape(-1, 512)
+    res = gm.search_batch(q, top_k=5)
+    ids = [str(s) for s in f["student_ids"]]
+    got_idx = np.array([[ids.index(sid) for sid, _n, _s in r] for r in res])
+    got_sc = np.array([[sc for _sid, _n, sc in r] for r in res], dtype=np.float32)
+    assert np.array_equal(got_idx, f["search_idx"])
+    assert np.abs(got_sc - f["search_score"]).max() <= 1e-6
+    assert res[0][0][1] == gm.students[res[0][0][0]].name
+    # single-query form, as FaceMatcher.match_single_face calls it
+    one = gm.search(q[9], top_k=3)
+    assert [ids.index(s) for s, _n, _sc in one] == f["search_idx"][9][:3].tolist()
+
+
 @pytest.mark.parametrize("method", ["mean", "median", "weighted_mean"])
 def test_build_templates_random_vs_oracle(handle, method):
     """Ragged students (1..40 samples), clusters loose enough that the 0.70 filter drops

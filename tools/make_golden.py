@@ -27,6 +27,11 @@ the reference's own ``face_embedder.FaceEmbedder`` and
   templates rebuilt by ``add_student`` and reference ``search`` results for
   every stored sample.  ``backups/adaface_ir_50_backup_20251202_081742.json``
   becomes ``backup_root_adaface_ir_50.npz``.
+* ``ref_students.pkl`` / ``ref_students.json`` — the reference's own gallery
+  FILES (gallery_manager.py:207-232): a reference ``GalleryManager`` built
+  with ``add_student`` (samples + metadata) from
+  ``gallery/backups/adaface_ir_101_backup_*.json`` and ``.save()``d.  Its
+  templates and search results are those of ``backup_adaface_ir_101.npz``.
 
 Two modules the reference imports are absent from this image and are supplied
 in a temporary directory that is put on ``sys.path`` for this run only:
@@ -38,8 +43,8 @@ fixture).  Weights are the seeded synthetic checkpoint of
 format.  Crops are regenerated from their seeds at test time; their SHA-256 is
 stored to pin them.
 
-Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups]`` (no
-argument: all).
+Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups] [refpkl]``
+(no argument: all).
 """
 from __future__ import annotations
 
@@ -98,7 +103,7 @@ def quiet():
 def main() -> None:
     if not os.path.isdir(REF):
         raise SystemExit("reference not present; golden files are generated in the build container only")
-    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups"}
+    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups", "refpkl"}
     os.makedirs(OUT, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="frgolden_")
     with open(os.path.join(tmp, "cv2.py"), "w") as f:
@@ -218,6 +223,22 @@ def main() -> None:
                 student_ids=np.array(sids), embeddings=emb, stored_template=tmpl, avg_similarity=avg,
                 ref_template=gal.astype(np.float32), search_idx=idx, search_score=sc)
             print(name, emb.shape)
+
+    if "refpkl" in parts:
+        import shutil
+        path = sorted(glob.glob(os.path.join(REF, "gallery", "backups", "adaface_ir_101_backup_*.json")))[0]
+        with open(path) as f:
+            data = json.load(f)
+        d = os.path.join(tmp, "refpkl")
+        with quiet():
+            gm = ref_gm.GalleryManager(gallery_path=os.path.join(d, "students.pkl"), aggregation_method="mean")
+            for sid, rec in data["students"].items():
+                gm.add_student(sid, rec["name"], np.array(rec["embeddings"], dtype=np.float32),
+                               metadata=rec.get("metadata") or {})
+            gm.save()
+        shutil.copyfile(os.path.join(d, "students.pkl"), os.path.join(OUT, "ref_students.pkl"))
+        shutil.copyfile(os.path.join(d, "students.json"), os.path.join(OUT, "ref_students.json"))
+        print("refpkl", len(data["students"]), "students from", os.path.basename(path))
 
 
 if __name__ == "__main__":

@@ -517,7 +517,34 @@ def aprio2(s):
     return aprio(s).replace("if (ahead <= 1)", "if (ahead <= 2)")
 
 
+CBLK_EDITS = [
+    ("        roff[e] = rin[e] ? (rs * p.NC * H + y) * W * Cin * 4 : BIGOFF;",
+     "        roff[e] = rin[e] ? (rs * p.NC * H * W * Cin + y * W * KC) * 4 : BIGOFF;"),
+    ("        coff[e] = cin[e] ? ((cs * H * W + x) * Cin + ch) * 4 : BIGOFF;",
+     "        coff[e] = cin[e] ? (cs * H * W * Cin + x * KC + ch) * 4 : BIGOFF;"),
+    ("      const int soff = step * KC * 4;", "      const int soff = step * H * W * KC * 4;"),
+    ("          gt[e] = (y >= 0 && rs * p.NC < p.B && T < p.ntiles) ? (rs * p.NC * H + y) * W : -1;",
+     "          gt[e] = (y >= 0 && rs * p.NC < p.B && T < p.ntiles) ? rs * p.NC * H * W * Cout + y * W * 16 : -1;"),
+    ("          gt[4 + e] = (x >= 0 && cs < p.NC) ? cs * H * W + x : -1;",
+     "          gt[4 + e] = (x >= 0 && cs < p.NC) ? cs * H * W * Cout + x * 16 : -1;"),
+    ("        ro[e] = orow >= 0 && live ? (orow * Cout + cout0) * 4 : BIGOFF;",
+     "        ro[e] = orow >= 0 && live ? (orow + (cout0 >> 4) * H * W * 16 + (cout0 & 15)) * 4 : BIGOFF;"),
+    ("        co[e] = ocol >= 0 ? ocol * Cout * 4 : BIGOFF;", "        co[e] = ocol >= 0 ? ocol * 4 : BIGOFF;"),
+]
+
+
+def cblk(s):
+    """channel-blocked activations [n][C/16][H][W][16] for the patch loads, the output stores and
+    the residual loads (timing only here: the bench's data stays as it is)"""
+    for x, y in CBLK_EDITS:
+        assert x in s, x
+        s = s.replace(x, y)
+    return s
+
+
 VARIANTS = {
+    "cblk": cblk,
+    "cblk_noload": lambda s: VARIANTS["noload"](cblk(s)),
     "nbg8": nbg(8),
     "nbg16": nbg(16),
     "nbuf3": lambda s: s.replace("constexpr int NBUF = 4; ", "constexpr int NBUF = 3; "),
@@ -575,7 +602,7 @@ VARIANTS = {
     "noprio": lambda s: s.replace("    if constexpr (PRE) __builtin_amdgcn_s_setprio(1);\n", ""),
     "nomad": nomad,
     "nofixup": lambda s: s.replace("    if (MODE_ == 1) /* 64-thread blocks", "    if (false) /* 64-thread blocks"),
-    "noload": lambda s: s.replace("""          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);""",
+    "noload": lambda s: s.replace("""          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, XPOL);""",
                                   """          const u32x2 v = {(unsigned)(poff[a][b] + soff), 0u};"""),
     "nomfma": lambda s: (s.replace(MFMA8, "        acc[x][0] += a0.x * u0.x + a1.w * u1.w;\n") if MFMA8 in s else s + "#error MFMA8"),
     "nouload": nouload,
