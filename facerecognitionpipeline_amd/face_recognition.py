@@ -101,8 +101,9 @@ class FaceQualityFilter:
         self._ops = _DeviceOps(device)
 
     def compute_blur_score(self, face_image) -> float:
-        return float(self.compute_blur_scores(face_image[None] if isinstance(face_image, np.ndarray)
-                                              else face_image.unsqueeze(0))[0])
+        # np.float64, like ndarray.var() in the reference (face_recognition.py:99)
+        return np.float64(self.compute_blur_scores(face_image[None] if isinstance(face_image, np.ndarray)
+                                                   else face_image.unsqueeze(0))[0])
 
     def compute_blur_scores(self, crops) -> np.ndarray:
         """uint8 [n,S,S,3] RGB crops (host array or device tensor) -> float64 [n]."""
@@ -134,7 +135,7 @@ class FaceQualityFilter:
         if abs(pose["yaw"]) > self.max_yaw or abs(pose["pitch"]) > self.max_pitch or abs(pose["roll"]) > self.max_roll:
             return False, m
         if self.check_blur and (face_image is not None or blur_score is not None):
-            m["blur_score"] = blur_score if blur_score is not None else self.compute_blur_score(face_image)
+            m["blur_score"] = np.float64(blur_score) if blur_score is not None else self.compute_blur_score(face_image)
             if m["blur_score"] < self.blur_threshold:
                 return False, m
         return True, m

@@ -1,0 +1,42 @@
+"""CPU: FaceQualityFilter's pose arithmetic and gate order vs the REFERENCE module itself.
+
+tests/golden/gate.npz holds what the reference ``FaceQualityFilter.compute_pose_angles`` /
+``is_valid`` (face_recognition.py:101-158) returned on the fixed detections of
+tests/_gate_inputs.py (tools/make_golden.py gate: the reference module imported with insightface
+stubbed and cv2 delegated to oracle/align_ref.py).  Here the gate runs with the reference's own
+blur values handed in, so everything but the device blur kernel is checked without a GPU:
+metric values bitwise, their numpy types, the early exits.  tests/test_gpu_gate.py runs the whole
+GPU FaceProcessor on the same inputs.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests._gate_inputs import QUALITY_CONFIGS, detections
+
+
+@pytest.fixture(scope="module")
+def records(golden_dir):
+    return json.loads(str(np.load(os.path.join(golden_dir, "gate.npz"))["records"]))
+
+
+def _same(got: dict, want: dict):
+    assert list(got) == list(want)  # same keys in the same (insertion) order: the same early exit
+    for k, w in want.items():
+        assert type(got[k]).__name__ == w["t"], (k, type(got[k]), w["t"])
+        assert float(got[k]) == w["v"], (k, float(got[k]), w["v"])
+
+
+def test_pose_angles_and_gate_match_reference(records):
+    from facerecognitionpipeline_amd.face_recognition import FaceQualityFilter
+    dets = detections()
+    for rec in records:
+        qf = FaceQualityFilter(**QUALITY_CONFIGS[rec["config"]])
+        for d, want in zip(dets, rec["per_face"]):
+            _same(qf.compute_pose_angles(d["landmarks"]), want["pose"])
+            blur = want["metrics"].get("blur_score")
+            ok, m = qf.is_valid(d, None, None if blur is None else blur["v"])
+            assert ok == want["is_valid"]
+            _same(m, want["metrics"])

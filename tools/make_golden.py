@@ -27,6 +27,17 @@ the reference's own ``face_embedder.FaceEmbedder`` and
   templates rebuilt by ``add_student`` and reference ``search`` results for
   every stored sample.  ``backups/adaface_ir_50_backup_20251202_081742.json``
   becomes ``backup_root_adaface_ir_50.npz``.
+* ``gate.npz`` — the reference ``FaceQualityFilter.compute_pose_angles`` /
+  ``is_valid`` and ``FaceProcessor.process_numpy`` (face_recognition.py:101-216)
+  on the seeded frame and fixed detections of ``tests/_gate_inputs.py``, for
+  three quality configurations, RGB and grayscale frames, ``return_all``
+  true and false: every result's detection index, ``is_valid``, metrics
+  (values and types) and aligned-crop SHA-256.  ``insightface`` is absent and
+  is stubbed (``FaceAnalysis`` refuses to be built; the processor gets a
+  fixed-detection detector); the cv2 calls go to the restatements in
+  ``oracle/align_ref.py``, so this file pins the reference's gate logic,
+  pose arithmetic, ordering and dict layout -- everything but cv2's own
+  numerics.
 * ``ref_students.pkl`` / ``ref_students.json`` — the reference's own gallery
   FILES (gallery_manager.py:207-232): a reference ``GalleryManager`` built
   with ``add_student`` (samples + metadata) from
@@ -43,7 +54,7 @@ fixture).  Weights are the seeded synthetic checkpoint of
 format.  Crops are regenerated from their seeds at test time; their SHA-256 is
 stored to pin them.
 
-Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups] [refpkl]``
+Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups] [refpkl] [gate]``
 (no argument: all).
 """
 from __future__ import annotations
@@ -85,6 +96,47 @@ def resize(img, dsize, interpolation=INTER_LINEAR):
     from oracle.scrfd import resize_linear_u8  # restatement of cv::resize INTER_LINEAR (uint8)
     assert interpolation == INTER_LINEAR
     return resize_linear_u8(img, int(dsize[0]), int(dsize[1]))
+
+# face_recognition.py's calls (gate fixture): delegated to the restatements in oracle/align_ref.py
+COLOR_RGB2BGR = COLOR_BGR2RGB = 4
+COLOR_RGB2GRAY = 7
+COLOR_GRAY2BGR = 8
+CV_64F = 6
+BORDER_CONSTANT = 0
+def _A():
+    sys.path.insert(0, {repo!r})
+    from oracle import align_ref
+    return align_ref
+def cvtColor(img, code):
+    import numpy as np
+    if code == COLOR_RGB2BGR:
+        return np.ascontiguousarray(img[..., ::-1])
+    if code == COLOR_GRAY2BGR:
+        return np.repeat(img[..., None], 3, axis=2)
+    if code == COLOR_RGB2GRAY:
+        return _A().rgb_to_gray(img)
+    raise NotImplementedError(code)
+def estimateAffinePartial2D(src, dst):
+    return _A().fit_similarity(src, dst), None
+def getAffineTransform(src, dst):
+    raise NotImplementedError("not on the similarity path")
+def warpAffine(img, M, dsize, flags=INTER_LINEAR, borderMode=BORDER_CONSTANT, borderValue=0):
+    assert flags == INTER_LINEAR and borderMode == BORDER_CONSTANT and borderValue == 0 and dsize[0] == dsize[1]
+    if img.ndim == 2:
+        return _A().warp_affine_linear(img[:, :, None], M, int(dsize[0]))[:, :, 0]
+    return _A().warp_affine_linear(img, M, int(dsize[0]))
+def Laplacian(gray, ddepth):
+    import numpy as np
+    assert ddepth == CV_64F
+    g = gray.astype(np.float64)
+    p = np.pad(g, 1, mode="reflect")  # BORDER_REFLECT_101, ksize 1: [0 1 0; 1 -4 1; 0 1 0]
+    return p[:-2, 1:-1] + p[2:, 1:-1] + p[1:-1, :-2] + p[1:-1, 2:] - 4.0 * g
+'''
+# insightface is absent: FaceAnalysis('buffalo_l') would download its model pack, so the stub
+# refuses to be constructed; FaceProcessor gets a fixed-detection stub detector instead
+INSIGHTFACE_APP = '''class FaceAnalysis:
+    def __init__(self, *a, **k):
+        raise RuntimeError("insightface stub: FaceAnalysis is never constructed for the golden files")
 '''
 NET_SHIM = '''import sys
 sys.path.insert(0, {repo!r})
@@ -103,13 +155,19 @@ def quiet():
 def main() -> None:
     if not os.path.isdir(REF):
         raise SystemExit("reference not present; golden files are generated in the build container only")
-    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups", "refpkl"}
+    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups", "refpkl", "gate"}
     os.makedirs(OUT, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="frgolden_")
     with open(os.path.join(tmp, "cv2.py"), "w") as f:
         f.write(CV2_STUB.format(repo=REPO))
     with open(os.path.join(tmp, "net.py"), "w") as f:
         f.write(NET_SHIM.format(repo=REPO))
+    for d in ("insightface", os.path.join("insightface", "utils")):
+        os.makedirs(os.path.join(tmp, d), exist_ok=True)
+        open(os.path.join(tmp, d, "__init__.py"), "w").close()
+    with open(os.path.join(tmp, "insightface", "app.py"), "w") as f:
+        f.write(INSIGHTFACE_APP)
+    open(os.path.join(tmp, "insightface", "utils", "face_align.py"), "w").close()
     sys.path.insert(0, tmp)
     sys.path.append(REF)
     import torch
@@ -239,6 +297,51 @@ def main() -> None:
         shutil.copyfile(os.path.join(d, "students.pkl"), os.path.join(OUT, "ref_students.pkl"))
         shutil.copyfile(os.path.join(d, "students.json"), os.path.join(OUT, "ref_students.json"))
         print("refpkl", len(data["students"]), "students from", os.path.basename(path))
+
+    if "gate" in parts:
+        import face_recognition as ref_fr  # reference module (insightface / cv2 stubbed above)
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import _gate_inputs as GI
+        frame = GI.frame()
+        dets = GI.detections()
+
+        class FixedDetector:  # the reference detector's output contract (face_recognition.py:37-48)
+            def detect(self, image):
+                return [{"bbox": d["bbox"].copy(), "landmarks": d["landmarks"].copy(), "det_score": d["det_score"],
+                         "pose": None, "age": None, "gender": None} for d in dets]
+
+        def enc(v):
+            return {"v": float(v), "t": type(v).__name__}
+
+        records = []
+        for ci, cfg in enumerate(GI.QUALITY_CONFIGS):
+            qf = ref_fr.FaceQualityFilter(**cfg)
+            al = ref_fr.FaceAligner(output_size=GI.S)
+            fp = ref_fr.FaceProcessor.__new__(ref_fr.FaceProcessor)  # __init__ would build FaceAnalysis
+            fp.detector, fp.aligner, fp.quality_filter = FixedDetector(), al, qf
+            for kind, img in (("rgb", frame), ("gray", GI.frame_gray(frame))):
+                with quiet():
+                    per_face = []
+                    for d in dets:
+                        crop = al.align(img, d["landmarks"])
+                        ok, m = qf.is_valid(d, crop)
+                        per_face.append({"is_valid": bool(ok), "metrics": {k: enc(v) for k, v in m.items()},
+                                         "pose": {k: enc(v) for k, v in qf.compute_pose_angles(d["landmarks"]).items()},
+                                         "crop_sha256": sha(crop)})
+                    runs = {}
+                    for ra in (False, True):
+                        res = fp.process_numpy(img, return_all=ra)
+                        runs[str(ra)] = [{"det": next(i for i, d in enumerate(dets)
+                                                      if np.array_equal(d["landmarks"], r["landmarks"])),
+                                          "is_valid": bool(r["is_valid"]), "det_score": r["det_score"],
+                                          "metrics": {k: enc(v) for k, v in r["quality_metrics"].items()},
+                                          "crop_sha256": sha(r["aligned_face"]), "crop_ndim": int(r["aligned_face"].ndim),
+                                          "keys": sorted(r)} for r in res]
+                records.append({"config": ci, "frame": kind, "per_face": per_face, "process_numpy": runs})
+        np.savez_compressed(os.path.join(OUT, "gate.npz"), frame_sha256=np.array(sha(frame)),
+                            records=np.array(json.dumps(records)))
+        valid = sum(f["is_valid"] for r in records for f in r["per_face"])
+        print("gate", len(records), "runs,", valid, "valid of", sum(len(r["per_face"]) for r in records))
 
 
 if __name__ == "__main__":

@@ -542,7 +542,38 @@ def cblk(s):
     return s
 
 
+NOPRE_A = "  FR_W4_CASE(true, EPI_AFFINE_PRELU)       // IR conv1: pre-BN (in the transform), BN, PReLU\n"
+NOPRE_B = "hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {\n"
+
+
+def nopre(s):
+    """conv1 without the pre-BN in the transform (as if the previous conv2's epilogue had applied it
+    to a second copy of its output): timing only"""
+    assert NOPRE_A in s and NOPRE_B in s
+    return s.replace(NOPRE_A, "").replace(NOPRE_B, NOPRE_B + "  if (pre && epi == EPI_AFFINE_PRELU) pre = false;\n")
+
+
+Y2_STORE = "    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);\n"
+
+
+def y2store(s):
+    """conv2 epilogues also write BN_next(y) = y * s + t (here the post-BN pair again) into a second
+    tensor of y's shape (the residual buffer: timing only): what the next conv1's pre-BN costs here"""
+    assert Y2_STORE in s
+    return s.replace(Y2_STORE, Y2_STORE + """    if constexpr (DRES) {
+      const f4 v2 = __builtin_elementwise_fma(v, psc, psh);
+      const u32x4 b2 = {__float_as_uint(v2.x), __float_as_uint(v2.y), __float_as_uint(v2.z), __float_as_uint(v2.w)};
+      __builtin_amdgcn_raw_buffer_store_b128(b2, y2r_d, po[i], 0, 0);
+    }
+""").replace("  const __amdgpu_buffer_rsrc_t yr_d = uniform_rsrc(p.y, p.B * H * W * Cout * 4);\n",
+             "  const __amdgpu_buffer_rsrc_t yr_d = uniform_rsrc(p.y, p.B * H * W * Cout * 4);\n"
+             "  const __amdgpu_buffer_rsrc_t y2r_d = uniform_rsrc(p.res, p.res ? p.B * H * W * Cout * 4 : 0);\n")
+
+
 VARIANTS = {
+    "nopre": nopre,
+    "y2store": y2store,
+    "cblk_nopre_y2": lambda s: y2store(nopre(cblk(s))),
     "cblk": cblk,
     "cblk_noload": lambda s: VARIANTS["noload"](cblk(s)),
     "nbg8": nbg(8),
