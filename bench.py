@@ -197,6 +197,40 @@ def cpu_baseline_c4(sd, det_sd, gallery_np, frames, lms, per_frame, budget_s):
                       f"IR-101 embed, G={gallery_np.shape[0]} per-probe search), {dt:.1f} s on {threads} host threads"}
 
 
+def build_id_of(version: str):
+    """The content hash at the end of fr_version() ("... build <id>"), or None."""
+    return version.rsplit("build ", 1)[-1].strip() if version and "build " in version else None
+
+
+def profile_figures(traffic_json, family, build, same_workload):
+    """PMC figures of the dominant kernel family from the committed profile of this workload:
+    (traffic bytes per launch, algorithmic bytes per launch, MFMA-busy fraction, source, note).
+    PMC counters need rocprofv3 passes of their own, so they come from profiles/r*/layers_pmc.json
+    (tools/gpu_profile.sh) -- and only when that profile was taken on THIS library build (its
+    build_id equals the loaded library's fr_version() hash); otherwise None with the reason."""
+    import glob
+    tj = traffic_json
+    if tj is None:
+        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "layers_pmc.json")))
+        tj = cands[-1] if cands else None
+    if not same_workload:
+        return None, None, None, None, "no PMC profile of this workload (the committed one is C3 fp32 F(4x4))"
+    if not tj or not os.path.exists(tj):
+        return None, None, None, None, "no PMC profile found"
+    with open(tj) as f:
+        pj = json.load(f)
+    rel = os.path.relpath(tj, REPO)
+    want = build_id_of(build)
+    if pj.get("build_id") is None or pj.get("build_id") != want:
+        return None, None, None, None, (f"{rel} was collected on build {pj.get('build_id')}, the loaded library is "
+                                        f"build {want}: its PMC figures are not attached")
+    kj = pj.get("kernels", {}).get(family, {})
+    traffic = kj.get("hbm_bytes_per_launch")
+    src = (rel + f" (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload, build {want})"
+           if traffic is not None else None)
+    return traffic, kj.get("alg_bytes_per_launch"), kj.get("mfma_busy_frac"), src, None
+
+
 PRESETS = {"c2": ("ir_50", 0), "c3": ("ir_101", 1000), "c4": ("ir_101", 1000), "c5": ("ir_101", 100_000)}
 
 
@@ -528,22 +562,13 @@ def main():
         # bf16x3 executes 3 bf16 MFMA products per algorithmic f32 product: its executed fraction is
         # taken against the dense bf16 MFMA peak
         peak, mult = (FP32_MFMA_PEAK_TFLOPS, 1.0) if args.precision == "fp32" else (BF16_MFMA_PEAK_TFLOPS, 3.0)
-        traffic, traffic_src, alg_bytes, mfma_busy = None, None, None, None
-        tj = args.traffic_json
-        if tj is None:
-            import glob
-            cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "layers_pmc.json")))
-            tj = cands[-1] if cands else None
-        if (tj and os.path.exists(tj) and args.config == "c3" and args.model_type == "adaface" and args.arch == "ir_101" and args.batch == 256
-                and G == 1000 and args.precision == "fp32"):
-            with open(tj) as f:
-                pj = json.load(f)
-            kj = pj.get("kernels", {}).get(dom, {})
-            traffic = kj.get("hbm_bytes_per_launch")
-            alg_bytes = kj.get("alg_bytes_per_launch")
-            mfma_busy = kj.get("mfma_busy_frac")
-            if traffic is not None:
-                traffic_src = os.path.relpath(tj, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same workload)"
+        from facerecognitionpipeline_amd import _lib as frlib
+        build = frlib.load().fr_version().decode()
+        same_workload = (args.config == "c3" and args.model_type == "adaface" and args.arch == "ir_101"
+                         and args.batch == 256 and G == 1000 and args.precision == "fp32"
+                         and args.conv_algorithm == "winograd4")
+        traffic, alg_bytes, mfma_busy, traffic_src, traffic_note = profile_figures(
+            args.traffic_json, dom, build, same_workload)
         kernel_name = {"winograd": ("wino4_kernel (Winograd F(4x4,3x3) f32: fused input transform, 16x16x4 "
                                     "MFMA, lane-local output transform; every stride-1 3x3 conv)"
                                     if args.conv_algorithm == "winograd4" else
@@ -560,7 +585,8 @@ def main():
                     # traffic is NOT observed in this run: PMC counters need their own rocprofv3 passes,
                     # so it is read from the committed profile of the same workload (traffic_source)
                     "traffic": traffic, "traffic_from_profile": traffic is not None,
-                    "traffic_source": traffic_src, "alg_bytes_per_launch": alg_bytes,
+                    "traffic_source": traffic_src, "traffic_note": traffic_note, "library_build": build,
+                    "alg_bytes_per_launch": alg_bytes,
                     # PMC SQ_VALU_MFMA_BUSY_CYCLES / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8) of the same kernel in
                     # the committed profile of this workload (its own rocprofv3 pass, like traffic)
                     "mfma_busy_frac_from_profile": round(mfma_busy, 4) if mfma_busy is not None else None,

@@ -56,12 +56,34 @@ def _compile(src: str) -> str:
     return obj
 
 
+def build_id() -> str:
+    """Content hash of every source, header and flag that goes into libfrhip.so.  Compiled into the
+    library (``fr_version()`` ends in ``build <id>``), so a profile stamped with it can be matched
+    to the library a later run loads (bench.py attaches PMC figures only on a match)."""
+    h = hashlib.sha256()
+    for src in SOURCES:
+        h.update(_digest(os.path.join(CSRC, src)).encode())
+    return h.hexdigest()[:16]
+
+
+def _build_id_obj(bid: str) -> str:
+    src = os.path.join(BUILD, f"build_id_{bid}.cpp")
+    obj = src + ".o"
+    if not os.path.exists(obj):
+        with open(src, "w") as f:
+            f.write(f'extern "C" const char* frhip_build_id(void) {{ return "{bid}"; }}\n')
+        subprocess.run([HIPCC, "-O2", "-fPIC", "-c", src, "-o", obj + ".tmp"], check=True)
+        os.replace(obj + ".tmp", obj)
+    return obj
+
+
 def build(verbose: bool = True) -> str:
     """Compile every HIP source for gfx950 and link libfrhip.so; return its path."""
     os.makedirs(BUILD, exist_ok=True)
     jobs = min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8")))
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(_compile, SOURCES))
+    objs.append(_build_id_obj(build_id()))
     stamp = hashlib.sha256("".join(objs).encode()).hexdigest()[:16]
     stamp_file = os.path.join(BUILD, "libfrhip.stamp")
     if os.path.exists(LIB) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:

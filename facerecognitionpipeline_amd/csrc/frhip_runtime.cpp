@@ -358,7 +358,37 @@ int chain_flush(fr_handle* h, hipStream_t s) {
 // takes stage 1's 56x56 layers (1.045 vs 1.064-1.077 ms per embed + match); at batch 2 their
 // 6,272 pixels, and stage 2's 1,568, are faster on F(4x4) split-K (1.50 vs 1.52-1.54 ms with
 // 4,096; profiles/r04/serving/pixel_threshold_ab.txt)
-static inline long long convs_max_m(int n) { return n == 1 ? 4096 : 1024; }
+static inline long long convs_max_m(const fr_handle* h, int n) { return n == 1 ? h->convs_max_m1 : 1024; }
+
+// The geometry fields of conv cw over a B x H x W input: what the kernel-selection rules read.
+static ConvParams conv_shape(const ConvW& cw, int B, int H, int W) {
+  ConvParams p{};
+  p.B = B;
+  p.H = H;
+  p.W = W;
+  p.Cin = cw.cin;
+  p.Cout = cw.cout;
+  p.KH = cw.kh;
+  p.KW = cw.kw;
+  p.stride = cw.stride;
+  p.pad = cw.pad;
+  p.Ho = (H + 2 * cw.pad - cw.kh) / cw.stride + 1;
+  p.Wo = (W + 2 * cw.pad - cw.kw) / cw.stride + 1;
+  p.M = B * p.Ho * p.Wo;
+  p.Cin2 = std::max(cw.cin2, 0);
+  return p;
+}
+
+// Whether run_conv puts this launch on the serving conv kernel (conv_small.hip).  One rule for
+// run_conv's branch and for forward_lanes' plan of which activations are channel-blocked (the
+// kernel is the only consumer / producer of that layout), so the two cannot disagree.
+// has_x2: the fused shortcut's input will be passed (cw.cin2 > 0).
+static bool convs_takes(const fr_handle* h, const ConvW& cw, ConvParams p, Epi epi, int nsplit, bool has_x2) {
+  static const float sentinel = 0.f;
+  if (has_x2 && !p.x2) p.x2 = &sentinel;  // convs_supported only checks that it is given
+  return p.B <= h->convs_max_n && p.M <= convs_max_m(h, p.B) && !h->detector && h->prec == PREC_F32 && nsplit == 1 &&
+         cw.w_frag && convs_supported(p, cw.pre_scale != nullptr, epi);
+}
 
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
@@ -417,8 +447,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // 16x16 tile (conv_small.hip); f32 parity path only
   // (layers of at most convs_max_m(B) output pixels: stage 1's 112x112 conv1, 784 pixel blocks
   // x 4 cout blocks, stays on F(4x4) split-K, which is faster there: 54 vs ~20 us)
-  if (B <= h->convs_max_n && p.M <= convs_max_m(B) && !h->detector && h->prec == PREC_F32 && nsplit == 1 && cw.w_frag &&
-      convs_supported(p, cw.pre_scale != nullptr, epi)) {
+  if (convs_takes(h, cw, p, epi, nsplit, x2 != nullptr)) {
     p.w = cw.w_frag;
     if (int rc = chain_flush(h, s)) return rc;
     p.blk = h->convs_blk;
@@ -697,17 +726,23 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
   const size_t nb = h->blocks.size();
   std::vector<char> all_convs(nb, 0), out_blk(nb, 0);
   {
-    const bool serving = nl == 1 && h->convs_blocked && cnt[0] <= h->convs_max_n && !h->detector &&
-                         h->prec == PREC_F32;
-    auto on_convs = [&](const ConvW& c, int hw) { return serving && c.w_frag && (long long)cnt[0] * hw * hw <= convs_max_m(cnt[0]); };
+    const bool serving = nl == 1 && h->convs_blocked;
+    // the launches forward_lanes makes below: conv1 (pre-BN, BN, PReLU) at the block's input size;
+    // conv2 with the fused conv shortcut (EPI_AFFINE + x2), the identity residual or the
+    // MaxPool(1,2) one (an unfused conv shortcut keeps NHWC: its own launch reads the input)
+    auto on_convs = [&](const ConvW& c, int hw, Epi epi, bool x2) {
+      return serving && convs_takes(h, c, conv_shape(c, cnt[0], hw, hw), epi, 1, x2);
+    };
     std::vector<char> conv2_convs(nb, 0);
     int hw = 112;
     for (size_t bi = 0; bi < nb; ++bi) {
       const BlockW& b = h->blocks[bi];
       const bool fused = b.has_sc_conv && h->fuse_shortcut && b.conv2_sc.w;
       const int ho = hw / b.spec.stride;
-      conv2_convs[bi] = (fused || !b.has_sc_conv) && on_convs(fused ? b.conv2_sc : b.conv2, ho);
-      all_convs[bi] = conv2_convs[bi] && on_convs(b.conv1, hw);
+      conv2_convs[bi] = fused ? on_convs(b.conv2_sc, hw, EPI_AFFINE, true)
+                              : !b.has_sc_conv && on_convs(b.conv2, hw, b.spec.stride == 1 ? EPI_AFFINE_RES
+                                                                                          : EPI_AFFINE_RES_SUB, false);
+      all_convs[bi] = conv2_convs[bi] && on_convs(b.conv1, hw, EPI_AFFINE_PRELU, false);
       hw = ho;
     }
     for (size_t bi = 0; bi + 1 < nb; ++bi) out_blk[bi] = conv2_convs[bi] && all_convs[bi + 1];
@@ -2102,7 +2137,12 @@ int fr_profile_kernel(fr_handle* h, int kind, double* ms, double* flop, double* 
 
 const char* fr_last_error(fr_handle* h) { return h ? h->err.c_str() : g_create_error.c_str(); }
 
-const char* fr_version(void) { return "frhip 0.1 gfx950 fp32-mfma"; }
+// content hash of the library's sources and flags (build.py build_id, a generated translation unit)
+extern "C" const char* frhip_build_id(void);
+const char* fr_version(void) {
+  static const std::string v = std::string("frhip 0.1 gfx950 fp32-mfma build ") + frhip_build_id();
+  return v.c_str();
+}
 
 int frt_conv2d(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout, int kh, int kw,
                int stride, int pad, const float* pre_scale, const float* pre_shift, const float* post_scale,
@@ -2295,6 +2335,14 @@ int frt_set_small_conv_pre_epilogue(fr_handle* h, int on) {
   std::lock_guard<std::mutex> lk(h->mu);
   DeviceGuard dg(h->device);
   h->convs_pre_epilogue = on != 0;
+  clear_graphs(h);
+  return FR_OK;
+}
+int frt_set_small_conv_pixels(fr_handle* h, int max_m1) {
+  if (!h || max_m1 < 0) return fail(h, FR_ERR_INVALID_ARGUMENT, "bad handle or pixel limit");
+  std::lock_guard<std::mutex> lk(h->mu);
+  DeviceGuard dg(h->device);
+  h->convs_max_m1 = max_m1;
   clear_graphs(h);
   return FR_OK;
 }

@@ -197,6 +197,8 @@ struct fr_handle {
   // launch per layer, whole K per 16x16 tile) instead of F(4x4) split-K + fixup / the split-K
   // direct convs (frt_set_small_conv)
   int convs_max_n = 2;
+  // output-pixel limit of a batch-1 layer on that kernel (frt_set_small_conv_pixels; batch 2: 1,024)
+  int convs_max_m1 = 4096;
   // a one-lane forward's conv2 on that kernel also writes the next block's pre-BN input into
   // convs_y2 (forward_lanes sets these three; run_conv sets convs_y2_done when it did), and that
   // block's conv1 then runs without pre-BN on it (frt_set_small_conv_pre_epilogue: A/B)

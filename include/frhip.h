@@ -222,7 +222,8 @@ int fr_profile_kernel(fr_handle* h, int kind, double* ms, double* flop, double* 
 
 /* Last error message of this handle (or of the last failed fr_create if h is NULL). */
 const char* fr_last_error(fr_handle* h);
-/* Library build/version string. */
+/* Library build/version string; it ends in "build <id>", the content hash of every source and
+ * flag the library was built from (build.py build_id), which profiles are stamped with. */
 const char* fr_version(void);
 
 #ifdef __cplusplus

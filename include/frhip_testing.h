@@ -69,6 +69,9 @@ int frt_conv2d_s2band(const float* x, const float* w, float* y, int B, int H, in
  * with the whole K reduction inside it) instead of F(4x4) split-K + fixup and the split-K direct
  * convs.  Drops captured graphs. */
 int frt_set_small_conv(fr_handle* h, int max_n);
+/* Output-pixel limit (n * Ho * Wo) of a batch-1 layer on the serving kernel (default 4,096:
+ * stage 1's 56x56 layers join stages 2-4; 1,024 keeps them on F(4x4) split-K).  A/B only. */
+int frt_set_small_conv_pixels(fr_handle* h, int max_m1);
 /* A/B switch (default on): in a one-lane forward, a body conv2 on the serving kernel also writes
  * BN(y) for the next block's conv1 (its pre-activation BN), which then runs without pre-BN. */
 int frt_set_small_conv_pre_epilogue(fr_handle* h, int on);
@@ -78,7 +81,8 @@ int frt_set_small_conv_blocked(fr_handle* h, int on);
 /* The serving-batch kernel alone: y = epi(conv3x3 pad 1 stride s (x) [+ conv1x1 stride s (x2)
  * against weight columns 9*cin .. + cin2]), w [cout][9*cin + cin2]; pre-BN only with epi 1;
  * epi 0, 1, 2 (res shaped like y) or 3 (res [B][H][W][cout], read at (s oy, s ox)).
- * cin, cout, cin2 % 16 == 0.  Asynchronous on stream. */
+ * cin, cout, cin2 % 16 == 0.  Synchronises the stream before it returns (it frees the
+ * temporary fragment-order copy of w it launched with). */
 int frt_conv2d_small(const float* x, const float* x2, const float* w, float* y, int B, int H, int W, int cin,
                      int cin2, int cout, int stride, const float* pre_scale, const float* pre_shift,
                      const float* post_scale, const float* post_shift, const float* prelu, const float* res, int epi,

@@ -63,3 +63,26 @@ def test_gpu_count_never_initialises_hip(monkeypatch):
     if n is not None:
         monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
         assert b.count_gpus() <= 1
+
+
+def test_pmc_figures_attach_only_to_the_profiled_build(tmp_path):
+    """bench.py's roofline.traffic / mfma_busy come from a committed PMC profile only when that
+    profile was stamped with the loaded library's build (fr_version() hash)."""
+    import json
+    b = _bench_module()
+    pj = {"build_id": "0123456789abcdef",
+          "kernels": {"winograd": {"hbm_bytes_per_launch": 4.2e8, "alg_bytes_per_launch": 2e8, "mfma_busy_frac": 0.55}}}
+    f = tmp_path / "layers_pmc.json"
+    f.write_text(json.dumps(pj))
+    t, a, m, src, note = b.profile_figures(str(f), "winograd", "frhip 0.1 gfx950 fp32-mfma build 0123456789abcdef", True)
+    assert (t, a, m) == (4.2e8, 2e8, 0.55) and "0123456789abcdef" in src and note is None
+    t, a, m, src, note = b.profile_figures(str(f), "winograd", "frhip 0.1 gfx950 fp32-mfma build ffffffffffffffff", True)
+    assert t is a is m is src is None and "not attached" in note
+    pj.pop("build_id")
+    f.write_text(json.dumps(pj))
+    assert b.profile_figures(str(f), "winograd", "x build 0123456789abcdef", True)[0] is None
+    assert b.profile_figures(str(f), "winograd", "x build 0123456789abcdef", False)[0] is None
+    # the library carries its content hash (tests/test_gpu_bench_launch.py checks it is this tree's)
+    import re
+    from facerecognitionpipeline_amd import _lib
+    assert re.fullmatch(r"[0-9a-f]{16}", b.build_id_of(_lib.load().fr_version().decode()))

@@ -67,6 +67,10 @@ def test_torchrun_form_without_gpus_flag():
 
 def test_bench_gpus1_line_unchanged_shape():
     out = _run()
+    # the library that ran is this tree's build, and the line says which one it is
+    from facerecognitionpipeline_amd.build import build_id
+    assert out["roofline"]["library_build"].endswith("build " + build_id())
+    assert (out["roofline"]["traffic"] is None) == (out["roofline"]["traffic_source"] is None)
     assert out["n_gpus"] == 1 and out["config"]["global_batch"] == 256
     assert out["config"]["gallery_exchange"] == "none" and "ranks_share_gpu" not in out["config"]
     assert "gallery_exchange_ms" not in out and "rank_ms_per_step_min" not in out

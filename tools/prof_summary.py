@@ -6,6 +6,13 @@ head_reduce) with the IR layer list, then prints per-layer-class average
 duration, achieved TFLOP/s, and (with PMC csvs) HBM bytes per launch.
 
 usage: prof_summary.py TRACE_DIR [--arch ir_101] [--batch 256] [--pmc DIR ...] [--json OUT]
+                       [--build "fr_version() string"]
+
+Also prints every kernel of the PMC passes by name (dispatches, average duration, HBM bytes,
+MFMA busy), whether or not it aligns with a forward -- e.g. the serving kernel of a batch-1 run,
+whose split-K layers do not align one dispatch per layer.  --build stamps the JSON with the
+library build the profile was taken on (fr_version(): "... build <id>"); bench.py attaches the
+PMC figures only to a run of the same build.
 """
 import argparse
 import collections
@@ -80,6 +87,48 @@ def read_csv(path):
         return list(csv.DictReader(f))
 
 
+def kernel_short(n):
+    """'void frhip::(anonymous namespace)::wino4_kernel<true, 1, 0, false>(frhip::Wino4Params)' ->
+    'wino4_kernel<true, 1, 0, false>'"""
+    return n.replace("(anonymous namespace)", "anon").split("(")[0].replace("void ", "").split("::")[-1][:48]
+
+
+def by_kernel(trace_dir, pmc_dirs):
+    """Per kernel name (template arguments dropped): dispatches and average duration in the trace,
+    HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE, x 1 KiB) and MFMA busy per dispatch in the PMC passes."""
+    short = kernel_short
+    dur = collections.defaultdict(list)
+    for r in read_csv(glob.glob(os.path.join(trace_dir, "*kernel_trace.csv"))[0]):
+        dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    cnt = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in pmc_dirs:
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        names = {}
+        for c in read_csv(glob.glob(os.path.join(d, "*counter_collection.csv"))[0]):
+            k = int(c["Dispatch_Id"])
+            per[k][c["Counter_Name"]] += float(c["Counter_Value"])
+            names[k] = short(c["Kernel_Name"])
+        for k, cs in per.items():
+            for cn, v in cs.items():
+                cnt[names[k]][cn].append(v)
+    out = {}
+    print(f"{'kernel':48s} {'disp':>6s} {'avg us':>8s} {'HBM MB':>8s} {'MFMAbusy':>8s}")
+    for name, ds in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
+        row = {"dispatches": len(ds), "avg_us": sum(ds) / len(ds) / 1e3}
+        c = cnt.get(name, {})
+        if c.get("FETCH_SIZE") and c.get("WRITE_SIZE"):
+            row["hbm_bytes"] = 2 * 1024 * sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"]) + 1024 * sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
+        if c.get("SQ_VALU_MFMA_BUSY_CYCLES") and c.get("GRBM_GUI_ACTIVE"):
+            busy = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"]) / len(c["SQ_VALU_MFMA_BUSY_CYCLES"])
+            clk = sum(c["GRBM_GUI_ACTIVE"]) / len(c["GRBM_GUI_ACTIVE"]) / 8.0
+            row["mfma_busy_frac"] = busy / (1024.0 * clk) if clk else 0.0
+        out[name] = row
+        print(f"{name:48s} {len(ds):6d} {row['avg_us']:8.1f} "
+              + (f"{row['hbm_bytes'] / 1e6:8.1f} " if "hbm_bytes" in row else f"{'-':>8s} ")
+              + (f"{100 * row['mfma_busy_frac']:7.1f}%" if "mfma_busy_frac" in row else f"{'-':>8s}"))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace_dir")
@@ -88,6 +137,7 @@ def main():
     ap.add_argument("--pmc", nargs="*", default=[])
     ap.add_argument("--json", default=None)
     ap.add_argument("--unfused-shortcut", action="store_true", help="traces taken with frt_set_fuse_shortcut(h, 0)")
+    ap.add_argument("--build", default=None, help="fr_version() of the library the profile was taken on")
     a = ap.parse_args()
     rows = read_csv(glob.glob(os.path.join(a.trace_dir, "*kernel_trace.csv"))[0])
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -113,7 +163,7 @@ def main():
                 for cn, v in vals.get(int(r["Dispatch_Id"]), {}).items():
                     pmc[cn][name].append(v)
     print(f"forwards aligned: {len(fwds)}")
-    hdr = f"{'layer':38s} {'n/fwd':>5s} {'avg us':>9s} {'TF/s':>7s} {'%peak':>6s} {'%time':>6s} {'alg MB':>8s}"
+    hdr = f"{'layer':38s} {'kernel':18s} {'n/fwd':>5s} {'avg us':>9s} {'TF/s':>7s} {'%peak':>6s} {'%time':>6s} {'alg MB':>8s}"
     if pmc:
         hdr += f" {'HBM MB':>8s} {'HBM/alg':>7s}"
     mf = "SQ_VALU_MFMA_BUSY_CYCLES" in pmc and "GRBM_GUI_ACTIVE" in pmc
@@ -138,7 +188,9 @@ def main():
         tot_ns += avg_ns * cnt
         tot_flop += flop * cnt
         row = {"layer": name, "per_fwd": cnt, "avg_us": avg_ns / 1e3, "tflops": tf, "alg_bytes": alg}
-        line = f"{name:38s} {cnt:5d} {avg_ns / 1e3:9.1f} {tf:7.1f} {100 * tf / PEAK:6.1f} {100 * share:6.1f} {alg / 1e6:8.1f}"
+        kshort = kernel_short(kname.get(name, "")).split("<")[0][:18]
+        line = (f"{name:38s} {kshort:18s} {cnt:5d} {avg_ns / 1e3:9.1f} {tf:7.1f} {100 * tf / PEAK:6.1f} {100 * share:6.1f}"
+                f" {alg / 1e6:8.1f}")
         is_conv = "conv" in name or "shortcut" in name or "head.fc" in name
         kn = kname.get(name, "")
         family = "winograd" if "wino" in kn else ("direct" if is_conv else "other")
@@ -227,6 +279,10 @@ def main():
               + (f", HBM {k['hbm_bytes_per_launch'] / 1e6:.1f} MB/launch vs alg {k['alg_bytes_per_launch'] / 1e6:.1f}"
                  if "hbm_bytes_per_launch" in k else ""))
     res["kernels"] = kernels
+    res["by_kernel"] = by_kernel(a.trace_dir, a.pmc)
+    if a.build:
+        res["build"] = a.build
+        res["build_id"] = a.build.rsplit("build ", 1)[-1].strip() if "build " in a.build else None
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)

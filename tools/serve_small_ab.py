@@ -3,6 +3,7 @@ against the F(4x4) split-K path, per batch size (embed + match, IR-101, G = 1000
 
     python tools/serve_small_ab.py [--ns 1,2,4,8,16]
     python tools/serve_small_ab.py --pre-epilogue [--ns 1]   (conv1 pre-BN in conv2's epilogue on / off)
+    python tools/serve_small_ab.py --pixels 1024,4096 [--reps 8]  (batch-1 pixel limit, interleaved)
 """
 import argparse
 import os
@@ -33,6 +34,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", default="1,2,4,8,16")
     ap.add_argument("--pre-epilogue", action="store_true")
+    ap.add_argument("--pixels", default=None, help="batch-1 serving-kernel pixel limits to interleave")
+    ap.add_argument("--reps", type=int, default=8)
     args = ap.parse_args()
     emb = FaceEmbedder(architecture="ir_101", model_path="synthetic", max_batch=64, graph_batch=0)
     h = emb.model
@@ -45,6 +48,21 @@ def main():
         rgb = probes[:n].contiguous()
         idx = torch.empty((n, 3), dtype=torch.int32, device="cuda")
         sc = torch.empty((n, 3), dtype=torch.float32, device="cuda")
+        if args.pixels:
+            # one process, the limits interleaved rep by rep, every run kept: the spread is the
+            # yardstick for the difference
+            lims = [int(x) for x in args.pixels.split(",")]
+            t = {m: [] for m in lims}
+            for rep in range(args.reps):
+                for m in (lims if rep % 2 == 0 else lims[::-1]):
+                    assert L.frt_set_small_conv_pixels(h.h, m) == 0
+                    t[m].append(timed(lambda: h.embed_match(rgb, 3, idx, sc), 200))
+            assert L.frt_set_small_conv_pixels(h.h, 4096) == 0
+            for m in lims:
+                v = sorted(t[m])
+                print(f"n={n} pixel limit {m}: median {v[len(v) // 2]:.4f} ms, min {v[0]:.4f}, max {v[-1]:.4f} "
+                      f"(runs {' '.join(f'{x:.4f}' for x in t[m])})", flush=True)
+            continue
         if args.pre_epilogue:
             assert L.frt_set_small_conv(h.h, n) == 0
             t = {0: [], 1: []}
