@@ -93,7 +93,10 @@ constexpr int NGEO = 8;
 // an LDS table (item, first step) so the schedule's scalars do not stay live across the K loop
 constexpr int MAXSEG = 64;
 static_assert(NGEO > NBUF + 2, "geometry table overwritten while an epilogue may still read it");
-static_assert((NBUF * VSTEP + NGEO * FT * 8 + 8 + 2 * MAXSEG) * 4 <= 160 * 1024, "LDS budget");
+// output geometry per tile: 4 rows (image-row base, y * W) and 4 columns (image base, x), so the
+// epilogue can address the output and the residual in either layout (NHWC or channel-blocked)
+constexpr int GEOW = 16;
+static_assert((NBUF * VSTEP + NGEO * FT * GEOW + 8 + 2 * MAXSEG) * 4 <= 160 * 1024, "LDS budget");
 static_assert(NXI % uring_depth<EPI_AFFINE_RES>() == 0 && NXI % uring_depth<EPI_AFFINE>() == 0,
               "U ring phase must repeat every K-step");
 
@@ -283,8 +286,12 @@ __device__ __forceinline__ Item item_of(const Wino4Params& p, int gi) {
 // The kernel body, for wino4_kernel (bid, nblk = blockIdx.x, gridDim.x) and for the layers of
 // wino4_chain_kernel (CH: the input patches are loaded device-coherent, sc1, since earlier layers
 // of the same launch wrote them from other CUs).  ring: the workgroup's LDS (W4_LDS_FLOATS).
-constexpr int W4_LDS_FLOATS = NBUF * VSTEP + NGEO * FT * 8 + 8 + 2 * MAXSEG;
-template <bool PRE, int EPI, int MODE, bool CH>
+constexpr int W4_LDS_FLOATS = NBUF * VSTEP + NGEO * FT * GEOW + 8 + 2 * MAXSEG;
+// RMIX: the residual's layout differs from the output's, in an instance of its own (its offsets are
+// computed on their own: more live registers in the epilogue): 1 = residual NHWC, output
+// channel-blocked; 2 = residual channel-blocked, output NHWC.  0: p.blk's y and res layouts are the
+// same, and the residual is addressed with the output's offsets.
+template <bool PRE, int EPI, int MODE, bool CH, int RMIX = 0>
 __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, const int bid, const int nblk) {
   constexpr bool SPLIT = MODE == 1, SK = MODE == 2;
   constexpr int XPOL = CH ? CPOL_SC1 : 0;
@@ -311,7 +318,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   const int tt_first = u_lo / KST, s_tail0 = u_lo - tt_first * KST;
   const int nseg = SK ? p.sk_dp + (u_hi > u_lo ? (u_hi - 1) / KST - tt_first + 1 : 0) : nloc;
   const int t_last = nseg - 1;  // last segment
-  int* const segtab = reinterpret_cast<int*>(ring + NBUF * VSTEP + NGEO * FT * 8 + 8);  // SK: [MAXSEG][item, step0]
+  int* const segtab = reinterpret_cast<int*>(ring + NBUF * VSTEP + NGEO * FT * GEOW + 8);  // SK: [MAXSEG][item, step0]
   auto seg_begin = [&](int j) {
     return SK && j <= t_last ? __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j + 1]) : 0;
   };
@@ -329,8 +336,8 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   auto steps_of = [&](const Item& it) { return SPLIT ? min(KS, KST - it.split * KS) : KST; };
   const int G = SK ? p.sk_dp * KST + (u_hi - u_lo) : nloc * KS;  // K-steps in this workgroup's stream
 
-  int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [NGEO items][16 tiles][8]
-  int* const rdy = geo + NGEO * FT * 8;                           // [4] K-steps written, per transform wave
+  int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [NGEO items][16 tiles][GEOW]
+  int* const rdy = geo + NGEO * FT * GEOW;                        // [4] K-steps written, per transform wave
   int* const fre = rdy + 4;                                       // [4] K-steps read, per MFMA wave
   if (tid < 8) rdy[tid] = 0;
   if (SK && tid < nseg) {
@@ -358,6 +365,12 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     const int half = lane >> 5, ii = (lane >> 3) & 3, pr = lane & 7;
     const int i = 4 * t + ii, ch = 2 * pr;
     const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
+    // input layout: NHWC (a pixel's Cin channels contiguous, a K-step's 16 at +16 step floats) or
+    // channel-blocked [B][Cin/16][H][W][16] (a pixel's 16 channels of block `step` contiguous, the
+    // next pixel 16 floats on: a wave load covers neighbouring pixels' lines)
+    const bool xblk = (p.blk & W4_BLK_X) != 0;
+    const int xppx = xblk ? KC : Cin;                     // floats from one pixel to the next
+    const int xstep = xblk ? H * W * KC * 4 : KC * 4;     // bytes from one K-step to the next
     const __amdgpu_buffer_rsrc_t xr_none = uniform_rsrc(p.x, 0);
     const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
     // the item's patch geometry, recomputed when the load stream enters a new item: byte
@@ -386,14 +399,14 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
         int rs;
         const int y = canvas_coord(4 * tr - 1 + e, ir0, p.Pr, H, sep_r, rs);
         rin[e] = y >= 0 && rs * p.NC < p.B && T < p.ntiles;
-        roff[e] = rin[e] ? (rs * p.NC * H + y) * W * Cin * 4 : BIGOFF;
+        roff[e] = rin[e] ? (rs * p.NC * H * W * Cin + y * W * xppx) * 4 : BIGOFF;
       }
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
         int cs;
         const int x = canvas_coord(4 * tc - 1 + 3 * half + e, ic0, p.Pc, W, sep_c, cs);
         cin[e] = x >= 0 && cs < p.NC;
-        coff[e] = cin[e] ? ((cs * H * W + x) * Cin + ch) * 4 : BIGOFF;
+        coff[e] = cin[e] ? (cs * H * W * Cin + x * xppx + ch) * 4 : BIGOFF;
       }
 #pragma unroll
       for (int a = 0; a < 6; ++a)
@@ -408,14 +421,19 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       // output geometry of the item's tiles, for the MFMA waves' epilogue (not for the
       // stream's overrun past the last item)
       if (half == 0 && pr == 0 && j <= t_last) {
-        int* gt = geo + ((j % NGEO) * FT + i) * 8;
+        // rows: [e] image-row base (floats of the images before the row's), [4 + e] y * W (or -1);
+        // columns: [8 + e] image base within the row, [12 + e] x (or -1)
+        int* gt = geo + ((j % NGEO) * FT + i) * GEOW;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           int rs, cs;
           const int y = canvas_coord(4 * tr + e, ir0, p.Pr, H, sep_r, rs);
           const int x = canvas_coord(4 * tc + e, ic0, p.Pc, W, sep_c, cs);
-          gt[e] = (y >= 0 && rs * p.NC < p.B && T < p.ntiles) ? (rs * p.NC * H + y) * W : -1;
-          gt[4 + e] = (x >= 0 && cs < p.NC) ? cs * H * W + x : -1;
+          const bool rok = y >= 0 && rs * p.NC < p.B && T < p.ntiles, cok = x >= 0 && cs < p.NC;
+          gt[e] = rok ? rs * p.NC * H * W * Cout : 0;
+          gt[4 + e] = rok ? y * W : -1;
+          gt[8 + e] = cok ? cs * H * W * Cout : 0;
+          gt[12 + e] = cok ? x : -1;
         }
       }
     };
@@ -444,7 +462,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       const bool live = !SPLIT || __builtin_amdgcn_readfirstlane(ls < ks_real ? 1 : 0);
       const __amdgpu_buffer_rsrc_t r = live ? xr : xr_none;
       const int step = __builtin_amdgcn_readfirstlane(step0 + min(ls, ks_real - 1));
-      const int soff = step * KC * 4;
+      const int soff = step * xstep;
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
@@ -712,21 +730,29 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     // Padding rows / columns and an idle quarter get BIGOFF, so every sum with them lies past the
     // buffer's range (unsigned) and the store / residual load is dropped by the range check,
     // which also drops the pixels of absent images in a partial last canvas row (>= B*H*W).
-    const int* gt = geo + ((j % NGEO) * FT + n) * 8;
-    int oo[4][4];
-    {
-      int ro[4], co[4];
+    const int* gt = geo + ((j % NGEO) * FT + n) * GEOW;
+    // byte offsets of the tile's 16 pixels (4 couts each) in a tensor of the output's shape, NHWC
+    // (ppx = Cout floats per pixel, couts at cout0) or channel-blocked (ppx = 16, cout0's block)
+    auto row_col_offsets = [&](bool blk, int (&ro)[4], int (&co)[4]) {
+      const int ppx = blk ? 16 : Cout;
+      const int cb = blk ? (cout0 >> 4) * H * W * 16 + (cout0 & 15) : cout0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int orow = gt[e], ocol = gt[4 + e];
-        ro[e] = orow >= 0 && live ? (orow * Cout + cout0) * 4 : BIGOFF;
-        co[e] = ocol >= 0 ? ocol * Cout * 4 : BIGOFF;
+        ro[e] = gt[4 + e] >= 0 && live ? (gt[e] + gt[4 + e] * ppx + cb) * 4 : BIGOFF;
+        co[e] = gt[12 + e] >= 0 ? (gt[8 + e] + gt[12 + e] * ppx) * 4 : BIGOFF;
       }
+    };
+    auto tile_offsets = [&](bool blk, int (&oo)[4][4]) {
+      int ro[4], co[4];
+      row_col_offsets(blk, ro, co);
 #pragma unroll
       for (int y = 0; y < 4; ++y)
 #pragma unroll
         for (int x = 0; x < 4; ++x) oo[y][x] = (int)((unsigned)ro[y] + (unsigned)co[x]);
-    }
+    };
+    const bool yblk = RMIX ? RMIX == 1 : (p.blk & W4_BLK_Y) != 0, rblk = RMIX ? RMIX == 2 : (p.blk & W4_BLK_RES) != 0;
+    int oo[4][4];
+    tile_offsets(yblk, oo);
     if constexpr (DEFER) {
       // part A: rows of A^T M A on all 4 couts (each frees 8 accumulator registers), the residual
       // of output rows 0-1 in flight during the column pass, then rows 2-3
@@ -737,9 +763,15 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
           const f4 m6[6] = {acc[6 * a], acc[6 * a + 1], acc[6 * a + 2], acc[6 * a + 3], acc[6 * a + 4], acc[6 * a + 5]};
           at6q(m6, z[a]);
         }
-        if constexpr (DRES)
+        if constexpr (DRES && RMIX) {
+          int rro[4], rco[4];
+          row_col_offsets(rblk, rro, rco);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) pres[i] = ld4(rr, (int)((unsigned)rro[i >> 2] + (unsigned)rco[i & 3]));
+        } else if constexpr (DRES) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) pres[i] = ld4(rr, oo[i >> 2][i & 3]);
+        }
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
           const f4 c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
@@ -750,9 +782,15 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
         }
       };
       auto set_pending = [&]() {
-        if constexpr (DRES)
+        if constexpr (DRES && RMIX) {
+          int rro[4], rco[4];
+          row_col_offsets(rblk, rro, rco);
+#pragma unroll
+          for (int i = 8; i < 16; ++i) pres[i] = ld4(rr, (int)((unsigned)rro[i >> 2] + (unsigned)rco[i & 3]));
+        } else if constexpr (DRES) {
 #pragma unroll
           for (int i = 8; i < 16; ++i) pres[i] = ld4(rr, oo[i >> 2][i & 3]);
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) po[i] = oo[i >> 2][i & 3];
         psc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
@@ -836,13 +874,15 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
           };
           // half the item's 16 pixels at a time, up to three parts' loads in flight per round (the
           // sums stay in part order: deterministic), the half's residual issued with them
+          int troff[4][4];
+          if constexpr (DRES) tile_offsets(RMIX ? rblk : yblk, troff);
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             f4 sm[8], rv[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
               sm[k] = f4{0.f, 0.f, 0.f, 0.f};
-              if constexpr (DRES) rv[k] = ld4(rr, oo[(8 * h + k) >> 2][(8 * h + k) & 3]);
+              if constexpr (DRES) rv[k] = ld4(rr, troff[(8 * h + k) >> 2][(8 * h + k) & 3]);
             }
             // the parts' workgroups in order, three at a time (empty ranges skipped)
             int c = first;
@@ -932,10 +972,10 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   w4_report_handoff(rseen, p.err);
 }
 
-template <bool PRE, int EPI, int MODE>
+template <bool PRE, int EPI, int MODE, int RMIX = 0>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
-  wino4_body<PRE, EPI, MODE, false>(p, ring, blockIdx.x, gridDim.x);
+  wino4_body<PRE, EPI, MODE, false, RMIX>(p, ring, blockIdx.x, gridDim.x);
 }
 
 // Split-K finish of one output element group: y = epilogue(sum of an item's raw partial outputs,
@@ -989,19 +1029,25 @@ __device__ __forceinline__ void w4_fixup_elem(const Wino4Params& p, int li, int 
         v[3] += a[u].w;
       }
   }
-  const long long yo = pix * p.Cout + cout0;
+  // float offset of (pix, cout0) in NHWC or in the channel-blocked layout [B][Cout/16][H][W][16]
+  auto at = [&](bool blk) {
+    if (!blk) return pix * p.Cout + cout0;
+    const long long hw = (long long)H * W, img = pix / hw;
+    return img * hw * p.Cout + (long long)(cout0 >> 4) * hw * 16 + (pix - img * hw) * 16 + (cout0 & 15);
+  };
+  const long long yo = at((p.blk & W4_BLK_Y) != 0), ro = at((p.blk & W4_BLK_RES) != 0);
   float rv[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) {
     if constexpr (CH) {
       const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, p.B * H * W * p.Cout * 4);
-      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(yo * 4), 0, CPOL_SC1);
+      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(ro * 4), 0, CPOL_SC1);
       rv[0] = __uint_as_float(w.x);
       rv[1] = __uint_as_float(w.y);
       rv[2] = __uint_as_float(w.z);
       rv[3] = __uint_as_float(w.w);
     } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) rv[r] = p.res[yo + r];
+      for (int r = 0; r < 4; ++r) rv[r] = p.res[ro + r];
     }
   }
 #pragma unroll
@@ -1301,6 +1347,28 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
     if (MODE_ == 1) /* 64-thread blocks: a serving grid's few items still spread over the CUs */          \
       hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_>), dim3(FT * 16 * FN / 4 / 64, pw.nitem),     \
                          dim3(64), 0, s, pw, KST, cus);                                                     \
+  }
+  // a residual whose layout differs from y's (p.blk: the seams between NHWC and channel-blocked
+  // activations): whole-item launches run an instance of their own (RMIX); a split-K launch's fixup
+  // and the stream-K tail address the residual on their own anyway, so split-K is the usual one
+  // and the tail is not used
+  const bool rmix = (((p.blk & W4_BLK_RES) != 0) != ((p.blk & W4_BLK_Y) != 0)) &&
+                    (epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU);
+  if (rmix) {
+    if (pre || epi != EPI_AFFINE_RES) return hipErrorInvalidValue;
+    int ks_per = KST;
+    const int S = can_split && nT <= cus / 2 ? split_of(nT, ks_per) : 1;
+    if (S > 1) {
+      splitk(0, nT, S, ks_per);
+      FR_W4_LAUNCH(false, EPI_AFFINE_RES, 1)
+      return hipGetLastError();
+    }
+    whole(0, nT);
+    if (p.blk & W4_BLK_Y)
+      hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 1>), dim3(std::min(nT, cus)), dim3(512), 0, s, pw);
+    else
+      hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 2>), dim3(std::min(nT, cus)), dim3(512), 0, s, pw);
+    return hipGetLastError();
   }
 #define FR_W4_CASE(PRE_, EPI_)                                                                              \
   if (pre == PRE_ && epi == EPI_) {                                                                         \

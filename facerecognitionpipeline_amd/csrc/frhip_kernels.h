@@ -156,7 +156,11 @@ struct Wino4Params {
   // poll_max 0 means the default (WINO4_POLL_DEFAULT), < 0 no polls at all (tests).
   int* err;
   int poll_max;
+  // layouts (W4_BLK_* bits): which of x, res, y are channel-blocked [B][C/16][H][W][16] instead of
+  // NHWC (the same per-element arithmetic either way: outputs are bitwise the NHWC launch's)
+  int blk;
 };
+constexpr int W4_BLK_X = 1, W4_BLK_RES = 2, W4_BLK_Y = 4;
 constexpr int WINO4_POLL_DEFAULT = 1 << 16;
 constexpr int FR_DEVERR_W4_HANDOFF = 1;
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16

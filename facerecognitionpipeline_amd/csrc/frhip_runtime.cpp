@@ -390,6 +390,18 @@ static bool convs_takes(const fr_handle* h, const ConvW& cw, ConvParams p, Epi e
          cw.w_frag && convs_supported(p, cw.pre_scale != nullptr, epi);
 }
 
+// Whether run_conv puts this conv on the F(4x4) kernel (the branch below; the plan of channel-
+// blocked activations in forward_lanes reads the same rule).  Ho / Wo: the conv's output size.
+static bool w4_takes(const fr_handle* h, const ConvW& cw, Epi epi, int res_H, int res_W, int Ho, int Wo) {
+  const bool wino_epi = (epi == EPI_AFFINE_PRELU && cw.pre_scale) || (epi == EPI_AFFINE_RES && !cw.pre_scale && res_H == Ho);
+  // F(4x4) also takes the detector's epilogues (no pre-BN; residual of the output's shape)
+  const bool wino4_epi = wino_epi || (!cw.pre_scale && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE ||
+                                                        ((epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU) &&
+                                                         (res_H == 0 || res_H == Ho) && (res_W == 0 || res_W == Wo))));
+  return h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 && wino4_epi &&
+         wino4_supported(cw.cin, cw.cout, cw.kh, cw.kw, cw.stride, cw.pad);
+}
+
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
              const LaneWs* L, const float* x2) {
@@ -468,14 +480,8 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // schedule (profiles/r01/sweep.txt): 8-wave 128x64 for the 64-channel
   // stage and the 128-channel residual convs, 8-wave 128x128 for the 1x1 shortcuts,
   // 8-wave 256x128 for every other 3x3 conv and the FC.
-  const bool wino_epi = (epi == EPI_AFFINE_PRELU && cw.pre_scale) || (epi == EPI_AFFINE_RES && !cw.pre_scale && res_H == p.Ho);
-  // F(4x4) also takes the detector's epilogues (no pre-BN; residual of the output's shape)
-  const bool wino4_epi = wino_epi || (!cw.pre_scale && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE ||
-                                                        ((epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU) &&
-                                                         (res_H == 0 || res_H == p.Ho) && (res_W == 0 || res_W == p.Wo))));
   // Winograd F(4x4,3x3) for the stride-1 3x3 convs (f32 parity path only)
-  if (h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 && wino4_epi &&
-      wino4_supported(cw.cin, cw.cout, cw.kh, cw.kw, cw.stride, cw.pad)) {
+  if (w4_takes(h, cw, epi, res_H, res_W, p.Ho, p.Wo)) {
     Wino4Params wp{};
     wp.x = x;
     wp.u = cw.wino4;
@@ -499,6 +505,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.max_split = g_wino4_max_split;
     wp.err = h->dev_err;
     wp.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
+    wp.blk = h->w4_blk;  // forward_lanes' plan of channel-blocked activations
     // a serving forward's conv1 / conv2: collected into the current chain when it plans as a
     // one-round split-K launch (the chain launches at the next layer that cannot join it)
     if (h->chain_collect && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE_RES)) {
@@ -517,6 +524,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     }
     if (int rc = chain_flush(h, s)) return rc;
     Wino4Params cv = wp;
+    cv.blk = 0;
     wino4_canvas(cv);
     // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
     const double exec = 2.0 * 36.0 * cv.ntiles * (double)cw.cin * cw.cout;
@@ -526,6 +534,8 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     return FR_OK;
   }
   if (int rc = chain_flush(h, s)) return rc;
+  if (h->w4_blk)  // forward_lanes only sets it for layers the F(4x4) branch above takes
+    return fail(h, FR_ERR_HIP, "internal: channel-blocked activations outside the F(4x4) kernel");
   // Winograd F(2x2,3x3) for the stride-1 3x3 convs (f32 parity path only)
   if (h->winograd && h->prec == PREC_F32 && cw.wino &&
       ((epi == EPI_AFFINE_PRELU && cw.pre_scale) || (epi == EPI_AFFINE_RES && !cw.pre_scale && res_H == p.Ho))) {
@@ -747,12 +757,40 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
     }
     for (size_t bi = 0; bi + 1 < nb; ++bi) out_blk[bi] = conv2_convs[bi] && all_convs[bi + 1];
   }
+  // Channel-blocked activations between F(4x4) layers (batches the serving kernel does not take):
+  // a block's conv1 output when both convs of the block run on F(4x4); a block's output when its
+  // conv2 and the next block's conv1 and conv2 (identity residual) do.  Every other tensor -- the
+  // stem's, the stride-2 / shortcut / FC kernels' inputs and outputs -- stays NHWC.  The layouts
+  // change nothing in the arithmetic: embeddings are bitwise the NHWC forward's (tested).
+  std::vector<char> w4r_blk(nb, 0), w4y_blk(nb, 0);
+  if (h->w4_blocked && cnt[0] > h->convs_max_n && !h->chain_collect && !h->detector) {
+    std::vector<char> c1(nb, 0), c2(nb, 0);
+    int hw = 112;
+    for (size_t bi = 0; bi < nb; ++bi) {
+      const BlockW& b = h->blocks[bi];
+      const int ho = hw / b.spec.stride;
+      c1[bi] = w4_takes(h, b.conv1, EPI_AFFINE_PRELU, 0, 0, hw, hw);
+      // (a conv shortcut or a stride-2 conv2 runs on another kernel)
+      c2[bi] = !b.has_sc_conv && b.spec.stride == 1 && w4_takes(h, b.conv2, EPI_AFFINE_RES, hw, hw, hw, hw);
+      hw = ho;
+    }
+    for (size_t bi = 0; bi < nb; ++bi) {
+      w4r_blk[bi] = c1[bi] && c2[bi];
+      w4y_blk[bi] = c2[bi] && bi + 1 < nb && c1[bi + 1] && c2[bi + 1];
+    }
+  }
+  struct W4Scope {
+    fr_handle* h;
+    ~W4Scope() { h->w4_blk = 0; }
+  } w4_scope{h};
   for (size_t bi = 0; bi < h->blocks.size(); ++bi) {
     const BlockW& b = h->blocks[bi];
     const int nxt = cur == 0 ? 1 : 0;
     const int Ho = HW / b.spec.stride;
     const bool in_blk = bi > 0 && out_blk[bi - 1], r_blk = all_convs[bi];
     h->convs_blk = (in_blk ? CONVS_BLK_X : 0) | (r_blk ? CONVS_BLK_Y : 0);
+    const bool w4_in = bi > 0 && w4y_blk[bi - 1];
+    h->w4_blk = (w4_in ? W4_BLK_X : 0) | (w4r_blk[bi] ? W4_BLK_Y : 0);
     for (int l = 0; l < nl; ++l) {
       int rc;
       if (pre_done) {
@@ -775,6 +813,7 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
     h->convs_y2 = nullptr;
     h->convs_y2_done = false;
     h->convs_blk = (r_blk ? CONVS_BLK_X : 0) | (in_blk ? CONVS_BLK_X2 | CONVS_BLK_RES : 0) | (out_blk[bi] ? CONVS_BLK_Y : 0);
+    h->w4_blk = (w4r_blk[bi] ? W4_BLK_X : 0) | (w4_in ? W4_BLK_RES : 0) | (w4y_blk[bi] ? W4_BLK_Y : 0);
     if (nl == 1 && h->convs_pre_epilogue && bi + 1 < h->blocks.size() && (fused || !b.has_sc_conv) &&
         h->blocks[bi + 1].conv1.pre_scale && (size_t)Ho * Ho * b.spec.depth <= (size_t)56 * 56 * 64) {
       h->convs_y2 = L[0].sc_buf;
@@ -804,6 +843,7 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
     h->convs_y2 = nullptr;
     h->convs_y2_done = false;
     h->convs_blk = 0;
+    h->w4_blk = 0;
     cur = nxt;
     HW = Ho;
   }
@@ -2343,6 +2383,14 @@ int frt_set_small_conv_pixels(fr_handle* h, int max_m1) {
   std::lock_guard<std::mutex> lk(h->mu);
   DeviceGuard dg(h->device);
   h->convs_max_m1 = max_m1;
+  clear_graphs(h);
+  return FR_OK;
+}
+int frt_set_wino4_blocked(fr_handle* h, int on) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  DeviceGuard dg(h->device);
+  h->w4_blocked = on != 0;
   clear_graphs(h);
   return FR_OK;
 }

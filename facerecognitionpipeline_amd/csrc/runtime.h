@@ -210,6 +210,10 @@ struct fr_handle {
   // (ConvParams::blk; forward_lanes sets convs_blk per launch); frt_set_small_conv_blocked: A/B
   int convs_blk = 0;
   bool convs_blocked = true;
+  // channel-blocked activations between F(4x4) layers of larger forwards (forward_lanes sets w4_blk,
+  // the Wino4Params::blk of the next launch); frt_set_wino4_blocked: A/B
+  int w4_blk = 0;
+  bool w4_blocked = true;
   bool chain_collect = false;
   int chain_seq = 0;  // index of the next run in the current forward
   std::vector<frhip::W4Link> chain_pending;

@@ -75,6 +75,10 @@ int frt_set_small_conv_pixels(fr_handle* h, int max_m1);
 /* A/B switch (default on): in a one-lane forward, a body conv2 on the serving kernel also writes
  * BN(y) for the next block's conv1 (its pre-activation BN), which then runs without pre-BN. */
 int frt_set_small_conv_pre_epilogue(fr_handle* h, int on);
+/* A/B switch (default on): in a forward the serving kernel does not take (n > 2 crops),
+ * activations passed between two F(4x4) layers are stored channel-blocked ([n][C/16][H][W][16])
+ * instead of NHWC (bitwise the same embeddings). */
+int frt_set_wino4_blocked(fr_handle* h, int on);
 /* A/B switch (default on): in a one-lane forward, activations passed between two layers on the
  * serving kernel are stored channel-blocked ([n][C/16][H][W][16]) instead of NHWC. */
 int frt_set_small_conv_blocked(fr_handle* h, int on);

@@ -42,6 +42,8 @@ def lib():
         L.frt_set_small_conv_blocked.argtypes = [_P, _I]
         L.frt_set_small_conv_pixels.restype = _I
         L.frt_set_small_conv_pixels.argtypes = [_P, _I]
+        L.frt_set_wino4_blocked.restype = _I
+        L.frt_set_wino4_blocked.argtypes = [_P, _I]
         L.frt_conv2d_small.restype = _I
         L.frt_conv2d_small.argtypes = [_P, _P, _P, _P] + [_I] * 7 + [_P] * 6 + [_I, _P]
         L.frt_stem.restype = _I

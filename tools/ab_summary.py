@@ -6,7 +6,7 @@ import sys
 
 d = collections.defaultdict(lambda: collections.defaultdict(list))
 for line in open(sys.argv[1]):
-    m = re.match(r"(\S+) \| B=(\d+) H=(\d+) (\d+)->(\d+) epi=(\d).*?: ([\d.]+) us", line)
+    m = re.match(r"(\S+) \| B=(\d+) H=(\d+) (\d+)->(\d+) epi=(\d)[^:]*: ([\d.]+) us", line)
     if m:
         d[f"B{m[2]} {m[4]}->{m[5]}@{m[3]} epi{m[6]}"][m[1]].append(float(m[7]))
 for shape, v in d.items():

@@ -3,6 +3,7 @@
 # Every shape runs every variant in turn, REPS times, alternating, so clock drift hits all alike.
 #   VARIANTS="base cblk" SHAPES="256 14 256 256 1;256 14 256 256 2" REPS=3 tools/gpu_w4_ab.sh
 # A shape is "B H Cin Cout epi" (epi 1: pre-BN + BN + PReLU = conv1, 2: BN + residual = conv2).
+# A variant name may carry a layout suffix "name:blk" (W4_BLK_* bits of Wino4Params.blk).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 VARIANTS=${VARIANTS:-"base"}
@@ -12,10 +13,11 @@ ITERS=${ITERS:-30}
 IFS=';' read -ra SH <<< "$SHAPES"
 for shp in "${SH[@]}"; do
   for rep in $(seq $REPS); do
-    for v in $VARIANTS; do
-      # argv: shape, iterations, sk_mode 0 (whole items: the runtime's default), no_split 1
-      out=$(timeout -k 5 60 tools/wv/w4g_$v $shp $ITERS 0 1) || { echo "$v $shp failed rc=$?"; exit 3; }
-      echo "$v | $out"
+    for vb in $VARIANTS; do
+      v=${vb%%:*}; blk=0; [ "$vb" != "$v" ] && blk=${vb#*:}
+      # argv: shape, iterations, sk_mode 0 (whole items: the runtime's default), no_split 1, lanes 1, layouts
+      out=$(timeout -k 5 60 tools/wv/w4g_$v $shp $ITERS 0 1 1 $blk) || { echo "$vb $shp failed rc=$?"; exit 3; }
+      echo "$vb | $out"
     done
   done
 done

@@ -84,6 +84,9 @@ int main(int argc, char** argv) {
   p.no_split = argc > 8 ? atoi(argv[8]) : 0;  // 1: whole items only (no tail split-K)
   // argv[9] lanes: 1 one stream; 2 two streams of B/2 each, launches interleaved (fr_set_lanes)
   const int nl = argc > 9 ? atoi(argv[9]) : 1;
+  // argv[10] layouts (W4_BLK_* bits: 1 x, 2 res, 4 y channel-blocked); timing only, the data is not
+  // rearranged, and the check below compares with a launch of the same layouts
+  p.blk = argc > 10 ? atoi(argv[10]) : 0;
   p.B = B;
   p.H = H;
   p.W = H;
@@ -156,8 +159,8 @@ int main(int argc, char** argv) {
     mx = std::max(mx, (double)std::fabs(h2[i]));
     ndiff += h1[i] != h2[i];
   }
-  printf("B=%d H=%d %d->%d epi=%d lanes=%d sk=%d: %.1f us (%.1f TF executed) | vs whole items: max|d| %.3g (max|y| %.3g), %zu differ\n",
-         B, H, Cin, Cout, epi, nl, p.sk_mode, 1e3 * t / iters, exec / (1e-3 * t / iters) / 1e12, md, mx, ndiff);
+  printf("B=%d H=%d %d->%d epi=%d lanes=%d sk=%d blk=%d: %.1f us (%.1f TF executed) | vs whole items: max|d| %.3g (max|y| %.3g), %zu differ\n",
+         B, H, Cin, Cout, epi, nl, p.sk_mode, p.blk, 1e3 * t / iters, exec / (1e-3 * t / iters) / 1e12, md, mx, ndiff);
   if (w4g_after_run) w4g_after_run();  // instrumented variants (w4g_variants.py "stamps") report here
   return 0;
 }
