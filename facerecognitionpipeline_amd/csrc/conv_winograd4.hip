@@ -1349,9 +1349,8 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
                          dim3(64), 0, s, pw, KST, cus);                                                     \
   }
   // a residual whose layout differs from y's (p.blk: the seams between NHWC and channel-blocked
-  // activations): whole-item launches run an instance of their own (RMIX); a split-K launch's fixup
-  // and the stream-K tail address the residual on their own anyway, so split-K is the usual one
-  // and the tail is not used
+  // activations): whole-item and stream-K launches run instances of their own (RMIX); a split-K
+  // launch's fixup addresses the residual on its own anyway, so split-K is the usual one
   const bool rmix = (((p.blk & W4_BLK_RES) != 0) != ((p.blk & W4_BLK_Y) != 0)) &&
                     (epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU);
   if (rmix) {
@@ -1364,10 +1363,18 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
       return hipGetLastError();
     }
     whole(0, nT);
-    if (p.blk & W4_BLK_Y)
-      hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 1>), dim3(std::min(nT, cus)), dim3(512), 0, s, pw);
-    else
-      hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 2>), dim3(std::min(nT, cus)), dim3(512), 0, s, pw);
+    const dim3 grid(sk ? cus : std::min(nT, cus));
+    if (p.blk & W4_BLK_Y) {
+      if (sk)
+        hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 2, 1>), grid, dim3(512), 0, s, pw);
+      else
+        hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 1>), grid, dim3(512), 0, s, pw);
+    } else {
+      if (sk)
+        hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 2, 2>), grid, dim3(512), 0, s, pw);
+      else
+        hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 2>), grid, dim3(512), 0, s, pw);
+    }
     return hipGetLastError();
   }
 #define FR_W4_CASE(PRE_, EPI_)                                                                              \
