@@ -570,7 +570,62 @@ def y2store(s):
              "  const __amdgpu_buffer_rsrc_t y2r_d = uniform_rsrc(p.res, p.res ? p.B * H * W * Cout * 4 : 0);\n")
 
 
+FINISH = """  auto finish = [&](int i) {  // part B of pending pixel i
+    f4 v = __builtin_elementwise_fma(pv[i], psc, psh);
+    if constexpr (EPI == EPI_AFFINE_PRELU) v = prelu_q(v, pal, pcl);
+    if constexpr (DRES) {
+      v += pres[i];
+      if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = prelu_q(v, pal, pcl);
+    }
+    const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);
+  };
+"""
+PAIRSTORE = """  // part B in pixel pairs (x, x + 1) of a tile row: lanes of tiles n, n ^ 1 (lane ^ 1, same couts)
+  // swap one value each (DPP quad_perm [1,0,3,2]) so that each store instruction writes whole
+  // 128-B lines of the channel-blocked output (pixels 2k, 2k + 1 of one tile)
+  f4 pend = {0.f, 0.f, 0.f, 0.f};
+  int pend_off = BIGOFF;
+  auto epi_px = [&](int i) {
+    f4 v = __builtin_elementwise_fma(pv[i], psc, psh);
+    if constexpr (EPI == EPI_AFFINE_PRELU) v = prelu_q(v, pal, pcl);
+    if constexpr (DRES) {
+      v += pres[i];
+      if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = prelu_q(v, pal, pcl);
+    }
+    return v;
+  };
+  auto swp = [](float f) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(f), 0xB1, 0xF, 0xF, false));
+  };
+  auto st = [&](f4 v, int off) {
+    const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, off, 0, 0);
+  };
+  auto finish = [&](int i) {
+    if ((i & 1) == 0) {
+      const bool odd = (threadIdx.x & 1) != 0;
+      const f4 v0 = epi_px(i), v1 = epi_px(i + 1);
+      const f4 t = odd ? v0 : v1;
+      const f4 sw = {swp(t.x), swp(t.y), swp(t.z), swp(t.w)};
+      const int so = __builtin_amdgcn_update_dpp(0, odd ? po[i] : po[i + 1], 0xB1, 0xF, 0xF, false);
+      st(odd ? sw : v0, odd ? so : po[i]);
+      pend = odd ? v1 : sw;
+      pend_off = odd ? po[i + 1] : so;
+    } else {
+      st(pend, pend_off);
+    }
+  };
+"""
+
+
+def pairstore(s):
+    assert FINISH in s
+    return s.replace(FINISH, PAIRSTORE)
+
+
 VARIANTS = {
+    "pairstore": pairstore,
     "nopre": nopre,
     "y2store": y2store,
     "cblk_nopre_y2": lambda s: y2store(nopre(cblk(s))),
