@@ -355,9 +355,10 @@ int chain_flush(fr_handle* h, hipStream_t s) {
 }
 
 // serving conv kernel: layers of at most this many output pixels (n * Ho * Wo).  Batch 1 also
-// takes stage 1's 56x56 layers (1.045 vs 1.064-1.077 ms per embed + match); at batch 2 their
-// 6,272 pixels, and stage 2's 1,568, are faster on F(4x4) split-K (1.50 vs 1.52-1.54 ms with
-// 4,096; profiles/r04/serving/pixel_threshold_ab.txt)
+// takes stage 1's 56x56 layers: 1.0626 vs 1.0740 ms per embed + match, medians of 8 runs each
+// interleaved in one process, spreads 0.0003 / 0.0007 ms (profiles/r05/serving_pixel_limit_ab.txt,
+// tools/serve_small_ab.py --pixels); at batch 2 their 6,272 pixels, and stage 2's 1,568, are
+// faster on F(4x4) split-K (1.50 vs 1.52-1.54 ms with 4,096; profiles/r04/serving/pixel_threshold_ab.txt)
 static inline long long convs_max_m(const fr_handle* h, int n) { return n == 1 ? h->convs_max_m1 : 1024; }
 
 // The geometry fields of conv cw over a B x H x W input: what the kernel-selection rules read.
