@@ -42,7 +42,10 @@ def _digest(path: str) -> str:
               os.path.join(REPO, "include", "frhip.h"), os.path.join(REPO, "include", "frhip_testing.h")]:
         with open(p, "rb") as f:
             h.update(f.read())
-    h.update(" ".join(CFLAGS + EXTRA.get(os.path.basename(path), [])).encode())
+    # the flags without this checkout's absolute include paths: the digest (and the build id baked
+    # into the library) must be the same wherever the tree is, e.g. on the GPU box's scratch copy
+    flags = [f.replace(REPO, "<repo>") for f in CFLAGS + EXTRA.get(os.path.basename(path), [])]
+    h.update(" ".join(flags).encode())
     return h.hexdigest()[:16]
 
 
