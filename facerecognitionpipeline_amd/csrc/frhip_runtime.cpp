@@ -779,6 +779,13 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
       w4r_blk[bi] = c1[bi] && c2[bi];
       w4y_blk[bi] = c2[bi] && bi + 1 < nb && c1[bi + 1] && c2[bi + 1];
     }
+    // a lone blocked block output makes both conv2s around it seams (residual and output in
+    // different layouts: the RMIX instances, ~1% slower than NHWC, profiles/r05/w4ab_layouts_table.txt)
+    // and no conv2 of the run gains: IR stages 1 and 4 (two F(4x4) blocks each) stay NHWC
+    std::vector<char> keep(nb, 0);
+    for (size_t bi = 0; bi < nb; ++bi)
+      keep[bi] = w4y_blk[bi] && ((bi > 0 && w4y_blk[bi - 1]) || (bi + 1 < nb && w4y_blk[bi + 1]));
+    w4y_blk = keep;
   }
   struct W4Scope {
     fr_handle* h;
