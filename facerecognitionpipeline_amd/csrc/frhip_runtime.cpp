@@ -286,6 +286,8 @@ struct ProfScope {
 // default: measured neutral on the IR-101 layers where its policy applies (stage 2, B=256:
 // 241-246 vs 239-243 us whole items), DESIGN.md §4.
 static int g_wino4_streamk = 0;
+// A/B (frt_set_conv2sc_tile): the tile of the fused stride-2 conv2 + conv-shortcut launches, -1 = the rule
+static int g_conv2sc_tile = -1;
 // cap on the F(4x4) split-K parts of small grids (frt_set_wino4_max_split: serving sweeps); 0 = none
 static int g_wino4_max_split = 0;
 // the stage-1 stride-2 conv2 on its band kernel (frt_set_s2_band: tests compare it with the
@@ -597,6 +599,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // embedding serving batches (M = B*Ho*Wo <= 4096: the stride-2 / 1x1 convs at batch <= ~20):
   // the 64x128 tile gives stream-K more, smaller tiles (batch 1: 2.28 -> 2.15 ms per forward).
   // The detector's tile set (conv_det.hip) has no 64x128 instance.
+  if (cw.cin2 > 0 && g_conv2sc_tile >= 0 && nsplit == 1) tile = (ConvTile)g_conv2sc_tile;
   if (!h->detector && p.M <= 4096 && nsplit == 1) tile = TILE_64x128;
   // the head FC (split-K) of a serving batch (M = n <= 64 rows) or of <= 256 crops (tools/fc_sweep.py,
   // 32 splits: --batch 128 43.0 us on 128x64/W8 vs 106 on 256x128/W8; --batch 256 69.3 vs 111.8).
@@ -2285,6 +2288,11 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 }
 
 static int g_frt_wino4_split = 1;
+int frt_set_conv2sc_tile(int tile) {
+  if (tile < -1 || tile >= TILE_COUNT) return FR_ERR_INVALID_ARGUMENT;
+  g_conv2sc_tile = tile;
+  return FR_OK;
+}
 int frt_set_wino4_streamk(int on) {
   g_wino4_streamk = on < 0 ? 0 : (on > 2 ? 2 : on);
   return FR_OK;

@@ -45,6 +45,9 @@ int frt_set_wino4_split(int on);
  * by their last-arriving wave); 2 = every item-step in equal ranges (experiments).
  * Applies to launches issued after the call (captured graphs keep theirs). */
 int frt_set_wino4_streamk(int on);
+/* A/B (process-wide): the ConvTile of the fused stride-2 conv2 + conv-shortcut launches of
+ * non-serving batches (-1: the built-in rule).  Forwards already captured in graphs keep theirs. */
+int frt_set_conv2sc_tile(int tile);
 /* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
  * before the call keep their schedule). */
 int frt_set_wino4_max_split(int s);
