@@ -1244,6 +1244,7 @@ bool w4_setup(Wino4Params& p, bool pre) {
   // instead of all of it, for patches read twice (stage 4: 238 -> 232 us, PMC-modelled traffic
   // 677 -> 453 MB per launch)
   p.nbg = std::max(1, std::min(p.mblocks, std::max(32 / p.nblocks, 8)));
+  if (p.nbg_override > 0) p.nbg = std::max(1, std::min(p.mblocks, p.nbg_override));
   return true;
 }
 

@@ -159,6 +159,7 @@ struct Wino4Params {
   // layouts (W4_BLK_* bits): which of x, res, y are channel-blocked [B][C/16][H][W][16] instead of
   // NHWC (the same per-element arithmetic either way: outputs are bitwise the NHWC launch's)
   int blk;
+  int nbg_override;  // > 0: tile blocks per XCD item group instead of the rule (A/B only)
 };
 constexpr int W4_BLK_X = 1, W4_BLK_RES = 2, W4_BLK_Y = 4;
 constexpr int WINO4_POLL_DEFAULT = 1 << 16;

@@ -288,6 +288,8 @@ struct ProfScope {
 static int g_wino4_streamk = 0;
 // A/B (frt_set_conv2sc_tile): the tile of the fused stride-2 conv2 + conv-shortcut launches, -1 = the rule
 static int g_conv2sc_tile = -1;
+// A/B (frt_set_wino4_nbg): tile blocks per XCD item group of the F(4x4) launches, 0 = the rule
+static int g_wino4_nbg = 0;
 // cap on the F(4x4) split-K parts of small grids (frt_set_wino4_max_split: serving sweeps); 0 = none
 static int g_wino4_max_split = 0;
 // the stage-1 stride-2 conv2 on its band kernel (frt_set_s2_band: tests compare it with the
@@ -509,6 +511,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.err = h->dev_err;
     wp.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     wp.blk = h->w4_blk;  // forward_lanes' plan of channel-blocked activations
+    wp.nbg_override = g_wino4_nbg;
     // a serving forward's conv1 / conv2: collected into the current chain when it plans as a
     // one-round split-K launch (the chain launches at the next layer that cannot join it)
     if (h->chain_collect && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE_RES)) {
@@ -2288,6 +2291,11 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 }
 
 static int g_frt_wino4_split = 1;
+int frt_set_wino4_nbg(int nbg) {
+  if (nbg < 0) return FR_ERR_INVALID_ARGUMENT;
+  g_wino4_nbg = nbg;
+  return FR_OK;
+}
 int frt_set_conv2sc_tile(int tile) {
   if (tile < -1 || tile >= TILE_COUNT) return FR_ERR_INVALID_ARGUMENT;
   g_conv2sc_tile = tile;

@@ -48,6 +48,9 @@ int frt_set_wino4_streamk(int on);
 /* A/B (process-wide): the ConvTile of the fused stride-2 conv2 + conv-shortcut launches of
  * non-serving batches (-1: the built-in rule).  Forwards already captured in graphs keep theirs. */
 int frt_set_conv2sc_tile(int tile);
+/* A/B (process-wide): tile blocks per XCD item group of the F(4x4) launches (0: the built-in rule,
+ * 32 items per group; 8 x 8 at 512 channels).  Forwards already captured in graphs keep theirs. */
+int frt_set_wino4_nbg(int nbg);
 /* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
  * before the call keep their schedule). */
 int frt_set_wino4_max_split(int s);
