@@ -162,6 +162,12 @@ struct Wino4Params {
   int nbg_override;  // > 0: tile blocks per XCD item group instead of the rule (A/B only)
 };
 constexpr int W4_BLK_X = 1, W4_BLK_RES = 2, W4_BLK_Y = 4;
+// The symmetric-wave F(4x4) kernel (conv_winograd4s.hip) for launches of whole items: same U
+// (launch_wino4_weights), same results up to rounding.  Reads x, u, y, pre_t, post_*, prelu, res, B,
+// H, W, Cin, Cout, blk and sk_mode of p.  Takes pre-BN + BN + PReLU, BN + residual and BN + PReLU
+// launches with Cout % 64 == 0 whose grid has at least `cus` items (sk_mode 2 stays on wino4).
+bool wino4s_takes(const Wino4Params& p, bool pre, Epi epi, int cus);
+hipError_t launch_wino4s(const Wino4Params& p, bool pre, Epi epi, hipStream_t s);
 constexpr int WINO4_POLL_DEFAULT = 1 << 16;
 constexpr int FR_DEVERR_W4_HANDOFF = 1;
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16

@@ -290,6 +290,11 @@ static int g_wino4_streamk = 0;
 static int g_conv2sc_tile = -1;
 // A/B (frt_set_wino4_nbg): tile blocks per XCD item group of the F(4x4) launches, 0 = the rule
 static int g_wino4_nbg = 0;
+// F(4x4) launches of whole items (at least one item per CU) on the symmetric-wave kernel
+// (conv_winograd4s.hip) instead of wino4_kernel (frt_set_wino4s: A/B and tests).  Off by default:
+// 5-8% faster per launch in isolation (two lanes, cold caches), 11% slower in the C3 forward
+// 
+static int g_wino4s = 0;
 // cap on the F(4x4) split-K parts of small grids (frt_set_wino4_max_split: serving sweeps); 0 = none
 static int g_wino4_max_split = 0;
 // the stage-1 stride-2 conv2 on its band kernel (frt_set_s2_band: tests compare it with the
@@ -532,10 +537,12 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     Wino4Params cv = wp;
     cv.blk = 0;
     wino4_canvas(cv);
-    // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair
+    // executed: 36 products per (canvas) 4x4 tile and (cin, cout) pair (the same canvas either kernel)
     const double exec = 2.0 * 36.0 * cv.ntiles * (double)cw.cin * cw.cout;
     ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
-    hipError_t e = launch_wino4(wp, cw.pre_scale != nullptr, epi, s);
+    const bool pre = cw.pre_scale != nullptr;
+    hipError_t e = g_wino4s && wino4s_takes(wp, pre, epi, h->cus) ? launch_wino4s(wp, pre, epi, s)
+                                                                   : launch_wino4(wp, pre, epi, s);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
     return FR_OK;
   }
@@ -2291,6 +2298,11 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 }
 
 static int g_frt_wino4_split = 1;
+int frt_set_wino4s(int on) {
+  if (on != 0 && on != 1) return FR_ERR_INVALID_ARGUMENT;
+  g_wino4s = on;
+  return FR_OK;
+}
 int frt_set_wino4_nbg(int nbg) {
   if (nbg < 0) return FR_ERR_INVALID_ARGUMENT;
   g_wino4_nbg = nbg;
@@ -2501,7 +2513,13 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
       }
       p.part = part;
     }
-    if (e == hipSuccess) e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s);
+    if (e == hipSuccess) {
+      int cus = 256, dev = 0;
+      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const bool pre = pre_scale != nullptr;
+      e = g_wino4s && wino4s_takes(p, pre, (Epi)epi, cus) ? launch_wino4s(p, pre, (Epi)epi, s)
+                                                          : launch_wino4(p, pre, (Epi)epi, s);
+    }
   }
   const hipError_t se = hipStreamSynchronize(s);
   (void)hipFree(u);

@@ -51,6 +51,11 @@ int frt_set_conv2sc_tile(int tile);
 /* A/B (process-wide): tile blocks per XCD item group of the F(4x4) launches (0: the built-in rule,
  * 32 items per group; 8 x 8 at 512 channels).  Forwards already captured in graphs keep theirs. */
 int frt_set_wino4_nbg(int nbg);
+/* F(4x4) launches of whole items (grids of at least one 16-tile x 64-cout item per CU: the batch-256
+ * forward, frt_conv2d_winograd4 at such sizes) on the symmetric-wave kernel (conv_winograd4s.hip,
+ * on = 1) or on wino4_kernel (0, default), process-wide; graphs captured before the call keep
+ * theirs. */
+int frt_set_wino4s(int on);
 /* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
  * before the call keep their schedule). */
 int frt_set_wino4_max_split(int s);

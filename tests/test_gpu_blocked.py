@@ -54,3 +54,24 @@ def test_blocked_forward_is_bitwise_nhwc(arch, model_type):
     finally:
         assert L.frt_set_wino4_streamk(0) == 0
         assert L.frt_set_wino4_blocked(emb.model.h, 1) == 0
+
+
+def test_blocked_forward_is_bitwise_nhwc_symmetric_waves():
+    """The same with the whole-item F(4x4) launches on the symmetric-wave kernel (frt_set_wino4s):
+    its layout bits move addresses only too."""
+    from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
+    from tests import _frt
+    L = _frt.lib()
+    sd = W.synthetic_state_dict("ir_101")
+    emb = FaceEmbedder(architecture="ir_101", state_dict=sd, device="cuda:0", max_batch=256)
+    crops = torch.from_numpy(W.synthetic_crops(256, seed=W.CROP_SEED_GALLERY)).cuda()
+    try:
+        assert L.frt_set_wino4s(1) == 0
+        got, ref = _both(emb, crops, L)
+        assert torch.equal(got, ref), (got - ref).abs().max().item()
+        assert L.frt_set_wino4s(0) == 0
+        w4 = emb.embed_tensor(crops).clone()
+        assert (got - w4).abs().max().item() <= 1e-5  # the two F(4x4) kernels round differently
+    finally:
+        L.frt_set_wino4s(0)  # the library default
+        assert L.frt_set_wino4_blocked(emb.model.h, 1) == 0

@@ -72,9 +72,45 @@ def test_winograd_non_square_map(m):
     (96, 14, 256, 256),  # 344 workgroups > CUs: a full round plus a partial one
     (32, 112, 64, 64),   # 1568 workgroups, Cin = 64 (4 K-steps)
 ])
-def test_winograd4_multi_round(B, H, cin, cout):
-    got, ref = _wino_case(B, H, cin, cout, 2, seed=500 + H, m=4)
+@pytest.mark.parametrize("w4s", [1, 0])
+def test_winograd4_multi_round(B, H, cin, cout, w4s):
+    L = _frt.lib()
+    try:
+        assert L.frt_set_wino4s(w4s) == 0
+        got, ref = _wino_case(B, H, cin, cout, 2, seed=500 + H, m=4)
+    finally:
+        L.frt_set_wino4s(0)  # the library default
     _close(got, ref, rel=REL[4])
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout", [
+    (256, 14, 14, 256, 256),  # IR-101 stage 3 at B = 256: 900 items
+    (128, 28, 28, 128, 128),  # stage 2, one lane of the headline batch
+    (64, 56, 56, 64, 64),     # stage 1 at 56 (4 K-steps per item)
+    (256, 7, 7, 512, 512),    # stage 4: 8 cout blocks, 4x4 tiles of a 7x7 map
+    (300, 15, 15, 32, 64),    # Cin = 32 (2 K-steps), even period 16, one cout block
+    (400, 9, 9, 64, 128),     # odd map, separator rows and columns, part-filled last canvas row
+    (1023, 8, 14, 32, 64),    # pre-BN: 4 | H but not W, a partial last canvas row (separator row added)
+])
+@pytest.mark.parametrize("epi", [1, 2])
+def test_winograd4_symmetric_waves(B, H, W, cin, cout, epi):
+    """Launches of whole items (at least one per CU) run on the symmetric-wave kernel
+    (conv_winograd4s.hip): matches the CPU conv, the shipping wino4_kernel to the same bar, and is
+    deterministic run to run."""
+    L = _frt.lib()
+    outs = {}
+    try:
+        for on in (1, 0):
+            assert L.frt_set_wino4s(on) == 0
+            got, ref = _wino_case(B, H, cin, cout, epi, seed=1500 + H + cin + epi, W=W, m=4)
+            _close(got, ref, rel=REL[4])
+            outs[on] = got
+        assert L.frt_set_wino4s(1) == 0
+        again, _ = _wino_case(B, H, cin, cout, epi, seed=1500 + H + cin + epi, W=W, m=4)
+        assert torch.equal(again, outs[1]), "symmetric-wave F(4x4) is not run-to-run deterministic"
+    finally:
+        L.frt_set_wino4s(0)  # the library default
+    _close(outs[1], outs[0], rel=REL[4])
 
 
 @pytest.mark.parametrize("B,H,cin,cout", [
@@ -132,6 +168,7 @@ def test_winograd4_stream_k(B, H, cin, cout, epi):
     L = _frt.lib()
     outs = {}
     try:
+        assert L.frt_set_wino4s(0) == 0  # wino4_kernel's schedules (the symmetric kernel takes whole items only)
         for mode in (1, 2, 0):
             L.frt_set_wino4_streamk(mode)
             got, ref = _wino_case(B, H, cin, cout, epi, seed=1300 + H + cin + epi, m=4)
@@ -143,6 +180,7 @@ def test_winograd4_stream_k(B, H, cin, cout, epi):
             assert torch.equal(again, outs[mode]), f"stream-K mode {mode} is not run-to-run deterministic"
     finally:
         L.frt_set_wino4_streamk(0)
+        L.frt_set_wino4s(0)  # the library default
     _close(outs[1], outs[0], rel=REL[4])
     _close(outs[2], outs[0], rel=REL[4])
 

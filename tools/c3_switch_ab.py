@@ -41,6 +41,7 @@ def main():
     sc = torch.empty((256, 5), dtype=torch.float32, device="cuda")
     t = {v: [] for v in vals}
     fam = {v: [] for v in vals}  # ms per one-lane forward of the direct-conv family (HIP events)
+    famw = {v: [] for v in vals}  # ... and of the Winograd family
     setv = (lambda v: fn(v)) if args.glob else (lambda v: fn(h.h, v))
     for rep in range(args.reps):
         for on in vals[rep % len(vals):] + vals[:rep % len(vals)]:
@@ -62,12 +63,14 @@ def main():
             pr = h.profile_read()
             h.profile_enable(False)
             fam[on].append(pr["direct"]["ms"] / 3)
+            famw[on].append(pr["winograd"]["ms"] / 3)
     assert setv(vals[0] if args.glob else 1) == 0
     for on in vals:
         v = sorted(t[on])
         print(f"{args.switch}({on}): median {v[len(v) // 2]:.3f} ms/step = {256 / v[len(v) // 2] * 1e3:.0f} faces/s, "
               f"min {v[0]:.3f}, max {v[-1]:.3f} (runs {' '.join(f'{x:.3f}' for x in t[on])}); direct-conv family "
-              f"{sorted(fam[on])[len(fam[on]) // 2]:.3f} ms per one-lane forward", flush=True)
+              f"{sorted(fam[on])[len(fam[on]) // 2]:.3f} ms, Winograd family {sorted(famw[on])[len(famw[on]) // 2]:.3f} ms "
+              f"per one-lane forward", flush=True)
 
 
 if __name__ == "__main__":
