@@ -58,7 +58,7 @@ constexpr int VSTEP_S = NXI_S * FT_S * KC_S;  // 9,216 floats
 constexpr int XCH_S = 8 * 64 * 32;            // partial-output exchange: 8 waves x 64 lanes x 32 floats
 constexpr int BIGOFF_S = 0x7F000000;
 #ifndef W4S_UR
-#define W4S_UR 9
+#define W4S_UR 6
 #endif
 constexpr int UR_S = W4S_UR;  // xi of U in flight per wave (18 % UR_S == 0)
 static_assert(18 % UR_S == 0, "U ring phase must repeat every K-step");

@@ -1,12 +1,13 @@
 // Stand-alone check and timing of the symmetric-wave F(4x4) kernel
 // (csrc/conv_winograd4s.hip) against the shipping F(4x4) one on the same
 // layer (same U), and both against a float64 direct convolution of the first images.
-// usage: w4s_bench B H Cin Cout epi iters [nimg_check] [lanes] [copies] [blk]   (epi 1 = pre-BN + BN + PReLU, 2 = BN + residual,
+// usage: w4s_bench B H Cin Cout epi iters [nimg_check] [lanes] [copies] [blk] [sk]   (epi 1 = pre-BN + BN + PReLU, 2 = BN + residual,
 //        3 = BN + PReLU without pre-BN; W6_ZERO_SHIFT=1: pre-BN shift 0; lanes 2: timing as two
 //        streams of B/2 each, launches interleaved, as the network's two lanes run; copies N: the
 //        timed launches cycle through N copies of x, U and res, so that with N >= 8 the working set
 //        exceeds the 256 MB MALL as the network's layer sequence does); blk: W4_BLK_* layout bits
-//        for the timed launches of both kernels (the data is not rearranged: timing only)
+//        for the timed launches of both kernels (the data is not rearranged: timing only); sk: the
+//        shipping kernel's sk_mode (default 1; the network runs 0)
 // build: SRC=w4s tools/w6_build.sh (hipcc, gfx950)
 #include <hip/hip_runtime.h>
 
@@ -199,6 +200,7 @@ int main(int argc, char** argv) {
   };
   const int nl = argc > 8 ? atoi(argv[8]) : 1;
   p4.blk = p6.blk = argc > 10 ? atoi(argv[10]) : 0;
+  p4.sk_mode = argc > 11 ? atoi(argv[11]) : 1;
   hipStream_t st[2] = {nullptr, nullptr};
   Wino4Params p4l[2] = {p4, p4};
   Wino4Params p6l[2] = {p6, p6};
