@@ -83,63 +83,41 @@ hipError_t launch_warp_affine_by_value(const uint8_t* frame, int H, int W, const
 // with both sums in that order; fp contraction is off in this file, so every operation rounds
 // as numpy's does and the result is bitwise numpy's (tests/test_align.py).
 constexpr int NP_BUFSIZE = 8192, NP_PW_BLOCK = 128;
-
-// calls f(leaf index, start, length) for the pairwise_sum leaves of [0, n), left to right
-template <typename F>
-__device__ void np_sum_leaves(int n, F&& f) {
-  int li = 0;
-  for (int c0 = 0; c0 < n; c0 += NP_BUFSIZE) {
-    int st[24], ln[24], sp = 1;
-    st[0] = c0;
-    ln[0] = min(NP_BUFSIZE, n - c0);
-    while (sp) {
-      --sp;
-      const int s = st[sp], m = ln[sp];
-      if (m <= NP_PW_BLOCK) {
-        f(li++, s, m);
-        continue;
-      }
-      int m2 = m / 2;
-      m2 -= m2 % 8;
-      st[sp] = s + m2;  // right half below the left, so the left pops first
-      ln[sp] = m - m2;
-      st[sp + 1] = s;
-      ln[sp + 1] = m2;
-      sp += 2;
-    }
-  }
-}
-
-// pw(m) over the leaf values part[li ..] (consumed in order); a chunk of <= 8192 is <= 7 levels deep
-template <int D>
-__device__ __noinline__ double np_pw_eval(int m, const double* part, int& li) {
-  if (m <= NP_PW_BLOCK) return part[li++];
-  if constexpr (D > 0) {
-    int m2 = m / 2;
-    m2 -= m2 % 8;
-    const double a = np_pw_eval<D - 1>(m2, part, li);
-    const double b = np_pw_eval<D - 1>(m - m2, part, li);
-    return a + b;
-  } else {
-    __builtin_trap();
-  }
-}
+// The pairwise tree of a chunk of <= 8192 elements is at most 7 splits deep (each split leaves
+// parts of at most half + 8 elements; checked for every chunk length): 128 leaf-level slots and
+// 255 tree nodes per chunk.
+constexpr int NP_DEPTH = 7, NP_SLOTS = 1 << NP_DEPTH, NP_NODES = 2 * NP_SLOTS - 1;
 
 // One block per crop: gray into LDS, 4-neighbour Laplacian with reflect-101 borders (integers,
 // exact in double), sum(L) exactly in int64 (so its float64 value does not depend on the order),
-// then the squared deviations summed in numpy's order: each thread sums whole pairwise leaves,
-// thread 0 combines them in the tree's order.
+// then the squared deviations summed in numpy's order, the tree evaluated level by level in
+// parallel.  Node k of level l of chunk c lives at c * 255 + 2^l - 1 + k; its children are nodes
+// 2k and 2k + 1 of level l + 1 (a leaf is carried down to 2k alone), so every level keeps the
+// left-to-right order.  Top-down the node ranges are split as pairwise_sum splits them; at the
+// last level each thread sums one leaf exactly as pairwise_sum's leaf loop does; bottom-up a split
+// node's value is left + right (a carried leaf passes its value up unchanged); thread 0 adds the
+// chunks' values to a running 0.  Every addition is numpy's, in numpy's order: bitwise
+// ndarray.var (tests/test_align.py).  (The first form walked the tree per thread and combined it
+// in one thread through recursive calls: 1.23 ms for 256 crops, on the C4 step's critical path.)
 __global__ __launch_bounds__(256) void blur_kernel(const uint8_t* __restrict__ crops, int S, double* __restrict__ var) {
   extern __shared__ __align__(8) uint8_t s_dyn[];
-  double* part = reinterpret_cast<double*>(s_dyn);               // [leaves]
   const int n = S * S;
-  uint8_t* s_gray = s_dyn + 8 * (n / 64 + 2 * ((n + NP_BUFSIZE - 1) / NP_BUFSIZE));
+  const int nch = (n + NP_BUFSIZE - 1) / NP_BUFSIZE;
+  double* val = reinterpret_cast<double*>(s_dyn);   // [2][nch * 128]: two adjacent levels' values
+  int* lo = reinterpret_cast<int*>(val + 2 * nch * NP_SLOTS);  // [nch * 255]: node starts
+  int* len = lo + nch * NP_NODES;                               // [nch * 255]: node lengths
+  uint8_t* s_gray = reinterpret_cast<uint8_t*>(len + nch * NP_NODES);
   __shared__ long long red[4];
   __shared__ double s_mean;
+  const int tid = threadIdx.x;
   const uint8_t* img = crops + (long long)blockIdx.x * n * 3;
-  for (int i = threadIdx.x; i < n; i += 256) {
+  for (int i = tid; i < n; i += 256) {
     const int r = img[i * 3], g = img[i * 3 + 1], b = img[i * 3 + 2];
     s_gray[i] = (uint8_t)((r * 4899 + g * 9617 + b * 1868 + (1 << 13)) >> 14);
+  }
+  for (int c = tid; c < nch; c += 256) {  // level 0: the chunks
+    lo[c * NP_NODES] = c * NP_BUFSIZE;
+    len[c * NP_NODES] = min(NP_BUFSIZE, n - c * NP_BUFSIZE);
   }
   __syncthreads();
   auto lap = [&](int i) {
@@ -149,56 +127,86 @@ __global__ __launch_bounds__(256) void blur_kernel(const uint8_t* __restrict__ c
     return s_gray[ym * S + x] + s_gray[yp * S + x] + s_gray[y * S + xm] + s_gray[y * S + xp] - 4 * s_gray[i];
   };
   long long s1 = 0;
-  for (int i = threadIdx.x; i < n; i += 256) s1 += lap(i);
+  for (int i = tid; i < n; i += 256) s1 += lap(i);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s1;
+  if ((tid & 63) == 0) red[tid >> 6] = s1;
+  // top-down: split every node of level l into its two children on level l + 1
+  for (int l = 0; l < NP_DEPTH; ++l) {
+    for (int j = tid; j < (nch << l); j += 256) {
+      const int c = j >> l, k = j & ((1 << l) - 1);
+      const int src = c * NP_NODES + (1 << l) - 1 + k;
+      const int dst = c * NP_NODES + (2 << l) - 1 + 2 * k;
+      const int s0 = lo[src], m = len[src];
+      int m2 = m;  // a leaf (or nothing) is carried down alone
+      if (m > NP_PW_BLOCK) {
+        m2 = m / 2;
+        m2 -= m2 % 8;
+      }
+      lo[dst] = s0;
+      len[dst] = m2;
+      lo[dst + 1] = s0 + m2;
+      len[dst + 1] = m - m2;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) s_mean = (double)(red[0] + red[1] + red[2] + red[3]) / (double)n;
   __syncthreads();
-  if (threadIdx.x == 0) s_mean = (double)(red[0] + red[1] + red[2] + red[3]) / (double)n;
-  __syncthreads();
-  const double m = s_mean;
+  const double mean = s_mean;
   auto dev2 = [&](int i) {
-    const double d = (double)lap(i) - m;
+    const double d = (double)lap(i) - mean;
     return d * d;
   };
-  np_sum_leaves(n, [&](int li, int s, int len) {
-    if (li % 256 != (int)threadIdx.x) return;
-    double res;
-    if (len < 8) {
-      res = 0.0;
-      for (int i = 0; i < len; ++i) res = res + dev2(s + i);
+  // leaves (pairwise_sum's n <= 128 branch), one per thread; level NP_DEPTH's values in val[1]
+  for (int j = tid; j < nch * NP_SLOTS; j += 256) {
+    const int c = j / NP_SLOTS, k = j % NP_SLOTS;
+    const int nd = c * NP_NODES + NP_SLOTS - 1 + k;
+    const int s = lo[nd], m = len[nd];
+    double res = 0.0;
+    if (m < 8) {
+      for (int i = 0; i < m; ++i) res = res + dev2(s + i);
     } else {
       double r[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = dev2(s + j);
+      for (int q = 0; q < 8; ++q) r[q] = dev2(s + q);
       int i = 8;
-      for (; i < len - (len % 8); i += 8)
+      for (; i < m - (m % 8); i += 8)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = r[j] + dev2(s + i + j);
+        for (int q = 0; q < 8; ++q) r[q] = r[q] + dev2(s + i + q);
       res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-      for (; i < len; ++i) res = res + dev2(s + i);
+      for (; i < m; ++i) res = res + dev2(s + i);
     }
-    part[li] = res;
-  });
+    val[(NP_DEPTH & 1) * nch * NP_SLOTS + j] = res;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  // bottom-up: a split node = left + right, a carried leaf passes its value up
+  for (int l = NP_DEPTH - 1; l >= 0; --l) {
+    const double* vc = val + ((l + 1) & 1) * nch * NP_SLOTS;
+    double* vp = val + (l & 1) * nch * NP_SLOTS;
+    for (int j = tid; j < (nch << l); j += 256) {
+      const int c = j >> l, k = j & ((1 << l) - 1);
+      const int ch = c * NP_SLOTS + 2 * k;
+      vp[c * NP_SLOTS + k] = len[c * NP_NODES + (1 << l) - 1 + k] > NP_PW_BLOCK ? vc[ch] + vc[ch + 1] : vc[ch];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
     double acc = 0.0;
-    int li = 0;
-    for (int c0 = 0; c0 < n; c0 += NP_BUFSIZE) acc = acc + np_pw_eval<10>(min(NP_BUFSIZE, n - c0), part, li);
+    for (int c = 0; c < nch; ++c) acc = acc + val[c * NP_SLOTS];  // level 0 in val[0]
     var[blockIdx.x] = acc / (double)n;
   }
 }
 
-// dynamic LDS of blur_kernel: the leaf sums (<= n / 64 + 2 per chunk) + the gray crop
+// dynamic LDS of blur_kernel: two levels of values, the trees' node ranges, the gray crop
 static size_t blur_lds_bytes(int S) {
-  const size_t n = (size_t)S * S;
-  return 8 * (n / 64 + 2 * ((n + NP_BUFSIZE - 1) / NP_BUFSIZE)) + n;
+  const size_t n = (size_t)S * S, nch = (n + NP_BUFSIZE - 1) / NP_BUFSIZE;
+  return 2 * nch * NP_SLOTS * 8 + 2 * nch * NP_NODES * 4 + n;
 }
 
 hipError_t launch_blur(const uint8_t* crops, int n, int S, double* var, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const size_t lds = blur_lds_bytes(S);
-  if (S < 2 || lds > 160 * 1024) return hipErrorInvalidValue;  // crops up to 357 x 357
+  if (S < 2 || lds > 160 * 1024) return hipErrorInvalidValue;  // crops up to 320 x 320
   hipLaunchKernelGGL(blur_kernel, dim3(n), dim3(256), lds, s, crops, S, var);
   return hipGetLastError();
 }
