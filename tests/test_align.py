@@ -184,15 +184,15 @@ def test_blur_kernel_matches_restatement():
     big = rng.integers(0, 256, (2, 224, 224, 3), dtype=np.uint8)
     assert np.array_equal(qf.compute_blur_scores(big), [A.blur_score(c) for c in big])
     # smooth crops (small variances, many equal Laplacians) and odd sizes: chunk and leaf edges
-    # ... up to the largest crop whose gray image and pairwise trees fit the LDS (S = 320: 13 chunks)
-    for S in (7, 8, 9, 90, 91, 129, 200, 256, 320):
+    # ... up to the largest crop the C ABI takes (fr_blur_scores: S in [3, 256], 8 chunks)
+    for S in (7, 8, 9, 90, 91, 129, 200, 256):
         yy, xx = np.mgrid[0:S, 0:S]
         sm = np.stack([(yy * 3 + xx) % 256, (xx * 2) % 256, (yy + 40) % 256], -1).astype(np.uint8)[None]
         sm = np.concatenate([sm, rng.integers(0, 256, (1, S, S, 3), dtype=np.uint8)])
         assert np.array_equal(qf.compute_blur_scores(sm), [A.blur_score(c) for c in sm]), S
     # larger crops are refused (an error, never a value computed another way)
-    with pytest.raises(Exception):
-        qf.compute_blur_scores(np.zeros((1, 330, 330, 3), np.uint8))
+    with pytest.raises(ValueError):
+        qf.compute_blur_scores(np.zeros((1, 257, 257, 3), np.uint8))
 
 
 @pytest.mark.gpu
