@@ -1,4 +1,7 @@
-// Winograd F(6x6, 3x3) convolution in f32 on gfx950 (v_mfma_f32_16x16x4_f32): EXPERIMENTAL.
+// Winograd F(6x6, 3x3) convolution in f32 on gfx950 (v_mfma_f32_16x16x4_f32): an EXPERIMENT, not
+// in the library (tools/w6_bench.cpp checks it against a float64 direct conv and times it against
+// wino4_kernel).  Measured and dropped in round 5: 0.97-1.11x F(4x4) at B = 256, 4-10x at serving
+// sizes (profiles/r05/w6_*.txt).
 //
 // Per 6x6 output tile and (cin, cout) pair the algorithm does 64 products instead of 324 (F(4x4):
 // 36 per 16 outputs).  At IR-101 stage 3 (14x14 maps, 52% of the forward) both tile sizes waste
@@ -12,17 +15,19 @@
 //   A^T = [1 1 1 1 1 1 1 0; 0 1 -1 2 -2 1/2 -1/2 0; 0 1 1 4 4 1/4 1/4 0; 0 1 -1 8 -8 1/8 -1/8 0;
 //          0 1 1 16 16 1/16 1/16 0; 0 1 -1 32 -32 1/32 -1/32 1]
 // fp32 error per layer, simulated against a float64 direct conv (256 channels, U built in double):
-// 2.8x F(4x4)'s -- far inside the path's 1e-5 / 1e-4 bars.
+// 2.8x F(4x4)'s; measured 7-16e-5 at |y| ~ 5 (F(4x4): 2-9e-5).
 //
 // Structure (not F(4x4)'s warp specialisation): 64 transform elements x 16 tiles x 16 couts of
 // accumulators are 256 registers per lane, which only a wave alone on its SIMD can hold (512
 // VGPR + AGPR), so each of the 4 waves of a workgroup does both jobs for its 16 couts: per K-step
 // (16 input channels) it transforms 4 of the item's 16 tiles into the LDS ring slot of the NEXT
 // K-step while it runs this K-step's 256 MFMAs from the current slot; one workgroup barrier per
-// K-step hands the slots over (two slots of 64 KiB).  f32 MFMA and VALU share a SIMD either way, so
-// the transform's cost is the same as with separate waves; what the single-wave form gives up is
-// the second wave's latency hiding, which the U ring (16 xi ahead) and patch loads a whole K-step
-// ahead make up for.
+// K-step hands the slots over (two slots of 64 KiB).  The transform runs as 14 pieces placed
+// between MFMA pairs (W6_PSTART / W6_PSTRIDE) or as one burst (W6_BURST); U is loaded W6_UR xi
+// ahead.  What the single-wave form cannot do is hide its own VALU and dependency bubbles behind a
+// second wave's MFMAs: a K-step costs ~14k cycles against 8.2k of MFMA issue even without global
+// loads (W6_NOLOAD / W6_NOULOAD timing variants).  The pre-BN masks are taken from the patch
+// offsets; a form with float mask registers gave wrong values on the last canvas row.
 //
 // Work item = 16 tiles x 64 couts x 64 xi; wave w owns couts 16w .. 16w+15.  Fragment layouts as in
 // conv_winograd4.hip (v_mfma_f32_16x16x4_f32: A[l&15][k=l>>4] = U, B[k=l>>4][l&15] = V; a lane's
