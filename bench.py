@@ -12,7 +12,7 @@ only exchange step); each rank then processes its own probes independently
 (weak scaling: N x batch faces per step).
 
 Also reported:
-  roofline      the dominant conv kernel family (wino4s_kernel / wino4_kernel for the stride-1 3x3 convs
+  roofline      the dominant conv kernel family (wino4_kernel for the stride-1 3x3 convs
                 under the f32 default): algorithmic (direct-conv) FLOP / summed
                 HIP-event time of its launches, vs the 157.3 TF dense fp32 MFMA
                 peak; executed_* counts the MFMA work Winograd actually performs.
@@ -576,14 +576,19 @@ def main():
         build = frlib.load().fr_version().decode()
         same_workload = (args.config == "c3" and args.model_type == "adaface" and args.arch == "ir_101"
                          and args.batch == 256 and G == 1000 and args.precision == "fp32"
-                         and args.conv_algorithm == "winograd4")
+                         and args.conv_algorithm == "winograd4" and args.wino4s != "on")
         traffic, alg_bytes, mfma_busy, traffic_src, traffic_note = profile_figures(
             args.traffic_json, dom, build, same_workload)
-        kernel_name = {"winograd": ("wino4s_kernel + wino4_kernel (Winograd F(4x4,3x3) f32, 16x16x4 MFMA, fused "
-                                    "transforms; every stride-1 3x3 conv: whole-item grids on the symmetric-wave "
-                                    "wino4s_kernel, split-K grids on wino4_kernel)"
-                                    if args.conv_algorithm == "winograd4" else
-                                    "wino_kernel (Winograd F(2x2,3x3) f32, every stride-1 3x3 conv)"),
+        if args.conv_algorithm != "winograd4":
+            wino_name = "wino_kernel (Winograd F(2x2,3x3) f32, every stride-1 3x3 conv)"
+        elif args.wino4s == "on":
+            wino_name = ("wino4s_kernel + wino4_kernel (Winograd F(4x4,3x3) f32, 16x16x4 MFMA, fused transforms; "
+                         "every stride-1 3x3 conv: whole-item grids on the symmetric-wave wino4s_kernel, split-K "
+                         "grids on wino4_kernel)")
+        else:
+            wino_name = ("wino4_kernel (Winograd F(4x4,3x3) f32: fused input transform, 16x16x4 MFMA, lane-local "
+                         "output transform; every stride-1 3x3 conv)")
+        kernel_name = {"winograd": wino_name,
                        "direct": "conv_mfma_kernel (implicit-GEMM; every conv/FC launch in this mode)"}[dom]
         # achieved = the FLOPs the kernel's algorithm performs per launch / its average launch time:
         # direct conv 2*M*N*K; Winograd F(m x m, 3x3) 2 * (m+2)^2 products per m x m output tile
