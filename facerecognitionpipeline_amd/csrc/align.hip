@@ -206,7 +206,7 @@ static size_t blur_lds_bytes(int S) {
 hipError_t launch_blur(const uint8_t* crops, int n, int S, double* var, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const size_t lds = blur_lds_bytes(S);
-  if (S < 2 || lds > 160 * 1024) return hipErrorInvalidValue;  // crops up to 320 x 320
+  if (S < 2 || lds > 160 * 1024) return hipErrorInvalidValue;  // up to 320 x 320 (fr_blur_scores takes <= 256)
   hipLaunchKernelGGL(blur_kernel, dim3(n), dim3(256), lds, s, crops, S, var);
   return hipGetLastError();
 }

@@ -143,8 +143,9 @@ int fr_align_faces(fr_handle* h, const uint8_t* frame, int height, int width, co
 int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, const double* tforms, int n,
                    int out_size, uint8_t* out, void* stream);
 /* FaceQualityFilter.compute_blur_score for n crops (face_recognition.py:94-99):
- * cv2.Laplacian(cvtColor(RGB2GRAY), CV_64F).var().  crops: device uint8 [n][size][size][3];
- * scores: host double [n].  Synchronises. */
+ * cv2.Laplacian(cvtColor(RGB2GRAY), CV_64F).var(), the variance summed in numpy's order (bitwise
+ * ndarray.var).  crops: device uint8 [n][size][size][3], size in [3, 256]; scores: host double [n].
+ * Synchronises. */
 int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* scores);
 
 /* FaceDetector.detect (face_recognition.py:31-48: insightface SCRFD det_10g at det_size
