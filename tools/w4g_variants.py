@@ -345,6 +345,18 @@ def early_res(s):
 NBG = "  p.nbg = std::max(1, std::min(p.mblocks, std::max(32 / p.nblocks, 8)));"
 
 
+GRID = "dim3(MODE_ == 2 ? cus : std::min(nit, cus))"
+
+
+def grid(n):
+    # whole-item launches (MODE 0) on a persistent grid of n workgroups instead of one per CU: two
+    # concurrent lanes on disjoint parts of the chip instead of queueing behind each other
+    def f(s):
+        assert GRID in s
+        return s.replace(GRID, f"dim3(MODE_ == 2 ? cus : std::min(nit, MODE_ == 0 ? {n} : cus))")
+    return f
+
+
 def nbg(minimum):
     # at least `minimum` tile blocks per XCD item group (Cout = 512: 4 -> 8, U streamed per XCD
     # round halves, patches read twice)
@@ -631,6 +643,8 @@ VARIANTS = {
     "cblk_nopre_y2": lambda s: y2store(nopre(cblk(s))),
     "cblk": cblk,
     "cblk_noload": lambda s: VARIANTS["noload"](cblk(s)),
+    "grid128": grid(128),
+    "grid192": grid(192),
     "nbg8": nbg(8),
     "nbg16": nbg(16),
     "nbuf3": lambda s: s.replace("constexpr int NBUF = 4; ", "constexpr int NBUF = 3; "),
