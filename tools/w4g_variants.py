@@ -643,6 +643,10 @@ VARIANTS = {
     "cblk_nopre_y2": lambda s: y2store(nopre(cblk(s))),
     "cblk": cblk,
     "cblk_noload": lambda s: VARIANTS["noload"](cblk(s)),
+    "uring18pre": lambda s: s.replace("  return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 9 : 12;",
+                                      "  return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 9 : 18;"),
+    "uring6res": lambda s: s.replace("  return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 9 : 12;",
+                                     "  return (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) ? 6 : 12;"),
     "grid128": grid(128),
     "grid192": grid(192),
     "nbg8": nbg(8),
