@@ -253,8 +253,14 @@ struct WarpMaps {
 hipError_t launch_warp_affine_by_value(const uint8_t* frame, int H, int W, const double* host_minv, int n, int S,
                                        uint8_t* out, hipStream_t s);
 
-// Laplacian variance of the gray image of n uint8 RGB crops [n][S][S][3] -> var[n] (double).
-hipError_t launch_blur(const uint8_t* crops, int n, int S, double* var, hipStream_t s);
+// Laplacian variance (numpy's summation order) of the gray image of n uint8 images [n][H][W][C]
+// (C = 3 / 4: RGB(A) -> gray; C = 1: gray) -> var[n] (double).  Images whose gray copy and
+// summation trees fit BLUR_LDS_MAX bytes of LDS take one block each; larger ones take three
+// launches over (chunk, image) blocks and blur_workspace_bytes(n, H, W) of device workspace ws.
+constexpr size_t BLUR_LDS_MAX = 160 * 1024;
+size_t blur_lds_bytes(int H, int W);
+size_t blur_workspace_bytes(int n, int H, int W);
+hipError_t launch_blur(const uint8_t* crops, int n, int H, int W, int C, double* var, void* ws, hipStream_t s);
 
 // Gallery templates (GalleryManager._aggregate_embeddings) for n_students CSR slices of
 // emb [total][512]; offsets: device [n_students + 1]; out: [n_students][512]; kept: [n] or NULL.

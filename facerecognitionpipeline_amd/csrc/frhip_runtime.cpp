@@ -2050,18 +2050,27 @@ int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, co
   return FR_OK;
 }
 
-int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* scores) {
+int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int height, int width, int channels, double* scores) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
-  if (n < 0 || size < 3 || size > 256 || (n > 0 && (!crops || !scores)))
-    return fail(h, FR_ERR_INVALID_ARGUMENT, "bad blur arguments (size in [3, 256])");
+  if (n < 0 || height < 1 || width < 1 || (long long)height * width >= (1ll << 31) ||
+      (channels != 1 && channels != 3 && channels != 4) || (n > 0 && (!crops || !scores)))
+    return fail(h, FR_ERR_INVALID_ARGUMENT, "bad blur arguments (height, width >= 1; channels 1, 3 or 4)");
   if (n == 0) return FR_OK;
   DeviceGuard dg(h->device);
   int rc = ensure_buf(h, &h->blur_out, &h->blur_out_cap, (size_t)n * sizeof(double));
   if (rc) return rc;
+  const size_t img = (size_t)height * width * channels;
+  const int per = 65535;  // images per launch (grid y of the multi-block form)
+  const size_t ws = blur_workspace_bytes(std::min(n, per), height, width);
+  if (ws && (rc = ensure_buf(h, &h->blur_ws, &h->blur_ws_cap, ws))) return rc;
   hipStream_t s = nullptr;
-  hipError_t e = launch_blur(crops, n, size, (double*)h->blur_out, s);
-  if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("blur launch: ") + hipGetErrorString(e));
+  for (int off = 0; off < n; off += per) {
+    const int m = std::min(per, n - off);
+    hipError_t e = launch_blur(crops + (size_t)off * img, m, height, width, channels, (double*)h->blur_out + off,
+                               h->blur_ws, s);
+    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("blur launch: ") + hipGetErrorString(e));
+  }
   FR_HIP(h, hipMemcpyAsync(scores, h->blur_out, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s));
   FR_HIP(h, hipStreamSynchronize(s));
   return check_dev_err(h);

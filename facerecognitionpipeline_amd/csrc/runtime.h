@@ -140,6 +140,8 @@ struct fr_handle {
   size_t align_m_cap = 0;
   void* blur_out = nullptr;  // [n] double
   size_t blur_out_cap = 0;
+  void* blur_ws = nullptr;  // multi-block blur: per (image, chunk) int64 L sums + double values
+  size_t blur_ws_cap = 0;
 
   // stream-K workspace shared by every body conv launch (launches are stream-ordered)
   int cus = 0;
@@ -288,6 +290,7 @@ struct fr_handle {
     (void)hipFree(sk_cnt);
     (void)hipFree(align_m);
     (void)hipFree(blur_out);
+    (void)hipFree(blur_ws);
     for (auto& t : chain_tabs) (void)hipFree(t.dev);
     (void)hipFree(chain_sync);
     if (dev_err) (void)hipHostFree(dev_err);

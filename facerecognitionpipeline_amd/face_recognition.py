@@ -55,9 +55,15 @@ class FaceAligner:
         self._ops = _DeviceOps(device)
 
     def align(self, image: np.ndarray, landmarks: np.ndarray, method: str = "similarity") -> np.ndarray:
-        """Host image in, host crop out (reference signature)."""
-        frame = torch.from_numpy(np.ascontiguousarray(image, dtype=np.uint8)).to(self._ops.device)
-        return self.align_batch(frame, np.asarray(landmarks, np.float32)[None], method)[0].cpu().numpy()
+        """Host image in, host crop out (reference signature).  A 2-D gray image gives a 2-D crop,
+        as cv2.warpAffine does (each channel of the warp is the single-channel warp)."""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        gray = img.ndim == 2
+        if gray:
+            img = np.repeat(img[:, :, None], 3, axis=2)
+        frame = torch.from_numpy(img).to(self._ops.device)
+        out = self.align_batch(frame, np.asarray(landmarks, np.float32)[None], method)[0].cpu().numpy()
+        return np.ascontiguousarray(out[..., 0]) if gray else out
 
     def align_batch(self, frame: torch.Tensor, landmarks: np.ndarray, method: str = "similarity") -> torch.Tensor:
         """Device form: uint8 [H,W,3] frame on the GPU, float32 [n,5,2] landmarks -> uint8 [n,S,S,3] on the GPU."""
@@ -101,15 +107,25 @@ class FaceQualityFilter:
         self._ops = _DeviceOps(device)
 
     def compute_blur_score(self, face_image) -> float:
-        # np.float64, like ndarray.var() in the reference (face_recognition.py:99)
-        return np.float64(self.compute_blur_scores(face_image[None] if isinstance(face_image, np.ndarray)
-                                                   else face_image.unsqueeze(0))[0])
+        """cv2.Laplacian(gray, CV_64F).var() of one image (face_recognition.py:94-99): a 3-D
+        [H,W,3] (or [H,W,4]) RGB image goes through RGB2GRAY, a 2-D one is the gray image.  Any
+        size.  Returns np.float64, like ndarray.var() in the reference."""
+        t = face_image if isinstance(face_image, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(face_image, np.uint8))
+        if t.dim() not in (2, 3):
+            raise ValueError(f"expected an HxW or HxWxC image, got {tuple(t.shape)}")
+        return np.float64(self.compute_blur_scores(t.unsqueeze(0))[0])
 
     def compute_blur_scores(self, crops) -> np.ndarray:
-        """uint8 [n,S,S,3] RGB crops (host array or device tensor) -> float64 [n]."""
+        """A batch of one size (host array or device tensor): uint8 [n,H,W,3|4] RGB(A) or
+        [n,H,W] gray -> float64 [n]."""
         t = crops if isinstance(crops, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(crops, np.uint8))
-        if t.dim() != 4 or t.shape[3] != 3 or t.shape[1] != t.shape[2]:
-            raise ValueError("expected uint8 [n,S,S,3] RGB crops")
+        if t.dtype != torch.uint8:
+            t = t.to(torch.uint8)
+        if t.dim() not in (3, 4) or (t.dim() == 4 and t.shape[3] not in (1, 3, 4)):
+            raise ValueError(f"expected uint8 [n,H,W] gray or [n,H,W,3] RGB images, got {tuple(t.shape)}")
+        if t.dim() == 4 and t.shape[3] == 1:
+            t = t[..., 0]
         return self._ops.handle.blur_scores(t.to(self._ops.device).contiguous())
 
     def compute_pose_angles(self, landmarks: np.ndarray) -> Dict[str, float]:
@@ -139,6 +155,20 @@ class FaceQualityFilter:
             if m["blur_score"] < self.blur_threshold:
                 return False, m
         return True, m
+
+
+def load_image_rgb(path: str) -> Optional[np.ndarray]:
+    """cv2.cvtColor(cv2.imread(path), COLOR_BGR2RGB) through PIL: uint8 [H,W,3] RGB, or None when
+    the file is missing or not a decodable image (cv2.imread returns None there).  imread's
+    default IMREAD_COLOR makes every image 3-channel: gray and palette images are expanded, an
+    alpha channel is dropped.  (8-bit images; imread's 16-bit down-conversion is not restated.)"""
+    try:
+        from PIL import Image
+        with Image.open(path) as im:
+            im.load()
+            return np.ascontiguousarray(np.asarray(im.convert("RGB"), dtype=np.uint8))
+    except (OSError, ValueError, SyntaxError):
+        return None
 
 
 class FaceDetector:
@@ -202,6 +232,16 @@ class FaceProcessor:
                                                                            device=device)
         self.aligner = FaceAligner(output_size=output_size, device=device)
         self.quality_filter = FaceQualityFilter(**(quality_filter_config or {}), device=device)
+
+    def process_image(self, image_path: str, return_all: bool = False) -> List[Dict]:
+        """face_recognition.py:174-182: read the file, convert to RGB, process_numpy.  The file is
+        decoded by PIL (cv2 is not in the image): lossless formats (PNG, BMP, TIFF) decode to the
+        same bytes cv2.imread gives; JPEG decoders may differ in rounding, so JPEG parity with
+        cv2.imread is unpinned.  Like cv2.imread, a file that cannot be read raises ValueError."""
+        image_rgb = load_image_rgb(image_path)
+        if image_rgb is None:
+            raise ValueError(f"Could not load image: {image_path}")
+        return self.process_numpy(image_rgb, return_all)
 
     def process_numpy(self, image_rgb: np.ndarray, return_all: bool = False) -> List[Dict]:
         faces = self.detector.detect(image_rgb)

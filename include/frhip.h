@@ -142,11 +142,14 @@ int fr_align_faces(fr_handle* h, const uint8_t* frame, int height, int width, co
  * FaceAligner.align(method != 'similarity'), face_recognition.py:66-67).  Synchronises. */
 int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, const double* tforms, int n,
                    int out_size, uint8_t* out, void* stream);
-/* FaceQualityFilter.compute_blur_score for n crops (face_recognition.py:94-99):
- * cv2.Laplacian(cvtColor(RGB2GRAY), CV_64F).var(), the variance summed in numpy's order (bitwise
- * ndarray.var).  crops: device uint8 [n][size][size][3], size in [3, 256]; scores: host double [n].
- * Synchronises. */
-int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int size, double* scores);
+/* FaceQualityFilter.compute_blur_score for n images of one size (face_recognition.py:94-99):
+ * cv2.Laplacian(gray, CV_64F).var() with gray = cvtColor(RGB2GRAY) of a 3- (or 4-) channel
+ * image, or the image itself for channels == 1 (the reference's 2-D branch); ksize 1,
+ * BORDER_REFLECT_101.  The variance is summed in numpy's order (ndarray.var's chunked pairwise
+ * sum; derived for and checked against numpy 2.2), so it is bitwise the reference's value there.
+ * crops: device uint8 [n][height][width][channels], any height, width >= 1 (height * width
+ * < 2^31); channels 1, 3 or 4; scores: host double [n].  Synchronises. */
+int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int height, int width, int channels, double* scores);
 
 /* FaceDetector.detect (face_recognition.py:31-48: insightface SCRFD det_10g at det_size
  * 640x640, det_thresh, NMS IoU 0.4) for n frames of one size.  The handle is created with

@@ -168,6 +168,19 @@ def test_align_kernel_bit_exact(S, n):
         assert np.array_equal(aff[i], A.warp_affine_linear(frame, affine_from_3_points(lms[i][:3], t[:3]), S))
 
 
+# blur_kernel restates numpy's float64 summation order as derived from numpy 2.2 (the build
+# image's 2.2.6): bitwise there; another numpy release may buffer its reduction differently, so
+# elsewhere the device value is held to a relative tolerance instead
+NUMPY_ORDER_PINNED = np.__version__.startswith("2.2.")
+
+
+def _blur_equal(got, ref):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    if NUMPY_ORDER_PINNED:
+        return np.array_equal(got, ref)
+    return np.allclose(got, ref, rtol=1e-12, atol=0.0)
+
+
 @pytest.mark.gpu
 def test_blur_kernel_matches_restatement():
     from facerecognitionpipeline_amd.face_recognition import FaceQualityFilter
@@ -179,20 +192,71 @@ def test_blur_kernel_matches_restatement():
     got = qf.compute_blur_scores(crops)
     ref = np.array([A.blur_score(c) for c in crops])
     # bitwise numpy's ndarray.var() (its chunked pairwise summation order), as the reference gets it
-    assert np.array_equal(got, ref)
+    assert _blur_equal(got, ref)
     assert got[1] == 0.0
     big = rng.integers(0, 256, (2, 224, 224, 3), dtype=np.uint8)
-    assert np.array_equal(qf.compute_blur_scores(big), [A.blur_score(c) for c in big])
-    # smooth crops (small variances, many equal Laplacians) and odd sizes: chunk and leaf edges
-    # ... up to the largest crop the C ABI takes (fr_blur_scores: S in [3, 256], 8 chunks)
-    for S in (7, 8, 9, 90, 91, 129, 200, 256):
+    assert _blur_equal(qf.compute_blur_scores(big), [A.blur_score(c) for c in big])
+    # smooth crops (small variances, many equal Laplacians) and odd sizes: chunk and leaf edges;
+    # up to 256 one block per image, beyond (320, 448: 13 / 25 chunks) the multi-block form
+    for S in (7, 8, 9, 90, 91, 129, 200, 256, 320, 448):
         yy, xx = np.mgrid[0:S, 0:S]
         sm = np.stack([(yy * 3 + xx) % 256, (xx * 2) % 256, (yy + 40) % 256], -1).astype(np.uint8)[None]
         sm = np.concatenate([sm, rng.integers(0, 256, (1, S, S, 3), dtype=np.uint8)])
-        assert np.array_equal(qf.compute_blur_scores(sm), [A.blur_score(c) for c in sm]), S
-    # larger crops are refused (an error, never a value computed another way)
+        assert _blur_equal(qf.compute_blur_scores(sm), [A.blur_score(c) for c in sm]), S
+
+
+@pytest.mark.gpu
+def test_blur_any_shape_gray_and_rgba():
+    """compute_blur_score takes what cv2.Laplacian(gray, CV_64F).var() takes (face_recognition.py:94-99):
+    a 2-D gray image or an RGB one, any height x width, never refused."""
+    import torch
+    from facerecognitionpipeline_amd.face_recognition import FaceQualityFilter
+    rng = np.random.default_rng(21)
+    qf = FaceQualityFilter()
+    for (H, W) in ((1, 1), (1, 9), (9, 1), (2, 2), (3, 5), (112, 96), (97, 300), (480, 640), (1080, 7)):
+        rgb = rng.integers(0, 256, (2, H, W, 3), dtype=np.uint8)
+        gray = rng.integers(0, 256, (2, H, W), dtype=np.uint8)
+        assert _blur_equal(qf.compute_blur_scores(rgb), [A.blur_score(c) for c in rgb]), (H, W)
+        assert _blur_equal(qf.compute_blur_scores(gray), [A.laplacian_var(g) for g in gray]), (H, W)
+        # the single-image reference signature: 3-D RGB, 2-D gray; np.float64 like ndarray.var()
+        one = qf.compute_blur_score(gray[0])
+        assert type(one) is np.float64 and _blur_equal([one], [A.laplacian_var(gray[0])])
+        assert _blur_equal([qf.compute_blur_score(rgb[1])], [A.blur_score(rgb[1])])
+        # an RGBA image: cvtColor(RGB2GRAY) ignores alpha
+        rgba = np.concatenate([rgb, rng.integers(0, 256, (2, H, W, 1), dtype=np.uint8)], axis=3)
+        assert _blur_equal(qf.compute_blur_scores(rgba), [A.blur_score(c) for c in rgb]), (H, W)
+    # the gray form of an RGB crop is the RGB crop's score (RGB2GRAY is what the kernel applies)
+    rgb = rng.integers(0, 256, (3, 320, 200, 3), dtype=np.uint8)
+    g = np.stack([A.rgb_to_gray(c) for c in rgb])
+    assert np.array_equal(qf.compute_blur_scores(g), qf.compute_blur_scores(rgb))
+    # device tensors in, same values
+    assert np.array_equal(qf.compute_blur_scores(torch.from_numpy(g).cuda()), qf.compute_blur_scores(g))
+    # an empty batch is an empty result; a wrong rank is refused
+    assert qf.compute_blur_scores(np.zeros((0, 8, 8, 3), np.uint8)).shape == (0,)
     with pytest.raises(ValueError):
-        qf.compute_blur_scores(np.zeros((1, 257, 257, 3), np.uint8))
+        qf.compute_blur_scores(np.zeros((8, 8), np.uint8))
+
+
+@pytest.mark.gpu
+def test_processor_large_output_size_and_gray_aligner():
+    """FaceProcessor(output_size=320): the reference blur-scores crops of any size; FaceAligner on a
+    2-D gray frame returns the 2-D crop, like cv2.warpAffine."""
+    from facerecognitionpipeline_amd.face_recognition import FaceAligner, FaceQualityFilter
+    rng = np.random.default_rng(22)
+    frame = rng.integers(0, 256, (400, 500, 3), dtype=np.uint8)
+    t = A.reference_template(320)
+    lm = (t - 160) * 0.9 + np.array([250.0, 200.0])
+    al = FaceAligner(output_size=320)
+    crop = al.align(frame, lm.astype(np.float32))
+    want = A.warp_affine_linear(frame, A.fit_similarity(lm.astype(np.float32), t), 320)
+    assert np.array_equal(crop, want)
+    qf = FaceQualityFilter()
+    assert _blur_equal([qf.compute_blur_score(crop)], [A.blur_score(want)])
+    gray = frame[..., 1].copy()
+    g = al.align(gray, lm.astype(np.float32))
+    assert g.ndim == 2 and np.array_equal(g, A.warp_affine_linear(gray[..., None], A.fit_similarity(
+        lm.astype(np.float32), t), 320)[..., 0])
+    assert _blur_equal([qf.compute_blur_score(g)], [A.laplacian_var(g)])
 
 
 @pytest.mark.gpu

@@ -54,11 +54,11 @@ def test_process_numpy_matches_reference_module(golden_dir):
         img = frames[rec["frame"]]
         # per detection: the host-API align (one face) and is_valid on its crop (device blur)
         for d, want in zip(dets, rec["per_face"]):
-            crop = fp.aligner.align(img if img.ndim == 3 else np.repeat(img[..., None], 3, 2), d["landmarks"])
-            if img.ndim == 2:
-                crop = np.ascontiguousarray(crop[..., 0])
+            # the reference's own calls: a 2-D gray frame gives a 2-D crop, blur-scored as 2-D
+            crop = fp.aligner.align(img, d["landmarks"])
+            assert crop.ndim == img.ndim
             assert _sha(crop) == want["crop_sha256"]
-            ok, m = fp.quality_filter.is_valid(d, crop if img.ndim == 3 else np.repeat(crop[..., None], 3, 2))
+            ok, m = fp.quality_filter.is_valid(d, crop)
             assert ok == want["is_valid"]
             _same(m, want["metrics"])
         for ra in (False, True):
@@ -71,3 +71,28 @@ def test_process_numpy_matches_reference_module(golden_dir):
                 _same(r["quality_metrics"], w["metrics"])
                 assert _sha(r["aligned_face"]) == w["crop_sha256"] and r["aligned_face"].ndim == w["crop_ndim"]
                 assert sorted(r) == w["keys"]
+
+
+def test_process_image_matches_reference_module(golden_dir, tmp_path):
+    """FaceProcessor.process_image (face_recognition.py:174-182) on the gate frame written as PNG vs
+    the reference's process_image on the same file (tools/make_golden.py image): same detections
+    back, same order, is_valid, crop bytes and blur scores; and equal to process_numpy on the
+    decoded array."""
+    from PIL import Image
+    from facerecognitionpipeline_amd.face_recognition import FaceProcessor, load_image_rgb
+    g = json.loads(str(np.load(os.path.join(golden_dir, "image.npz"))["process_image"]))
+    f = frame()
+    png = str(tmp_path / "gate_frame.png")
+    Image.fromarray(f, "RGB").save(png)
+    assert np.array_equal(load_image_rgb(png), f)
+    fp = FaceProcessor(output_size=S, detector=FixedDetector(detections()), device="cuda:0")
+    for ra in (False, True):
+        got = fp.process_image(png, return_all=ra)
+        want = g[str(ra)]
+        assert len(got) == len(want)
+        for r, w in zip(got, want):
+            assert np.array_equal(r["landmarks"], detections()[w["det"]]["landmarks"])
+            assert r["is_valid"] == w["is_valid"] and _sha(r["aligned_face"]) == w["crop_sha256"]
+            assert float(r["quality_metrics"].get("blur_score", -1.0)) == w["blur"]
+        same = fp.process_numpy(f, return_all=ra)
+        assert [_sha(r["aligned_face"]) for r in same] == [_sha(r["aligned_face"]) for r in got]

@@ -38,6 +38,13 @@ the reference's own ``face_embedder.FaceEmbedder`` and
   ``oracle/align_ref.py``, so this file pins the reference's gate logic,
   pose arithmetic, ordering and dict layout -- everything but cv2's own
   numerics.
+* ``image.npz`` + ``image_{rgb,gray,rgba}.png`` — small seeded PNG files (RGB, 8-bit
+  gray, RGBA) and the SHA-256 of the RGB array ``cv2.imread`` + ``COLOR_BGR2RGB`` yields
+  for each (gray expanded to 3 channels, alpha dropped: IMREAD_COLOR), computed from the
+  arrays the files were written from; and the reference ``FaceProcessor.process_image``
+  (face_recognition.py:174-182) on the gate frame written as PNG (``imread`` in the cv2
+  shim decodes through PIL: lossless, so the pixels are the frame's), with the gate's
+  fixed detections, default quality settings, ``return_all`` true and false.
 * ``ref_students.pkl`` / ``ref_students.json`` — the reference's own gallery
   FILES (gallery_manager.py:207-232): a reference ``GalleryManager`` built
   with ``add_student`` (samples + metadata) from
@@ -54,7 +61,7 @@ fixture).  Weights are the seeded synthetic checkpoint of
 format.  Crops are regenerated from their seeds at test time; their SHA-256 is
 stored to pin them.
 
-Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups] [refpkl] [gate]``
+Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups] [refpkl] [gate] [image]``
 (no argument: all).
 """
 from __future__ import annotations
@@ -125,6 +132,17 @@ def warpAffine(img, M, dsize, flags=INTER_LINEAR, borderMode=BORDER_CONSTANT, bo
     if img.ndim == 2:
         return _A().warp_affine_linear(img[:, :, None], M, int(dsize[0]))[:, :, 0]
     return _A().warp_affine_linear(img, M, int(dsize[0]))
+def imread(path, flags=1):
+    # IMREAD_COLOR of an 8-bit file: 3-channel BGR, or None when unreadable; decoded by PIL
+    # (lossless formats decode to the same bytes; this pins process_image's wrapper, not imread)
+    import numpy as np
+    try:
+        from PIL import Image
+        with Image.open(path) as im:
+            im.load()
+            return np.ascontiguousarray(np.asarray(im.convert("RGB"), dtype=np.uint8)[..., ::-1])
+    except (OSError, ValueError, SyntaxError):
+        return None
 def Laplacian(gray, ddepth):
     import numpy as np
     assert ddepth == CV_64F
@@ -155,7 +173,7 @@ def quiet():
 def main() -> None:
     if not os.path.isdir(REF):
         raise SystemExit("reference not present; golden files are generated in the build container only")
-    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups", "refpkl", "gate"}
+    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups", "refpkl", "gate", "image"}
     os.makedirs(OUT, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="frgolden_")
     with open(os.path.join(tmp, "cv2.py"), "w") as f:
@@ -342,6 +360,51 @@ def main() -> None:
                             records=np.array(json.dumps(records)))
         valid = sum(f["is_valid"] for r in records for f in r["per_face"])
         print("gate", len(records), "runs,", valid, "valid of", sum(len(r["per_face"]) for r in records))
+
+    if "image" in parts:
+        from PIL import Image
+        import face_recognition as ref_fr  # reference module (insightface / cv2 stubbed above)
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import _gate_inputs as GI
+        r = np.random.Generator(np.random.PCG64(0xFACE0B4D))
+        rgb = r.integers(0, 256, (48, 64, 3), dtype=np.uint8)
+        gray = r.integers(0, 256, (48, 64), dtype=np.uint8)
+        rgba = r.integers(0, 256, (48, 64, 4), dtype=np.uint8)
+        Image.fromarray(rgb, "RGB").save(os.path.join(OUT, "image_rgb.png"))
+        Image.fromarray(gray, "L").save(os.path.join(OUT, "image_gray.png"))
+        Image.fromarray(rgba, "RGBA").save(os.path.join(OUT, "image_rgba.png"))
+        want = {"image_rgb.png": sha(rgb), "image_gray.png": sha(np.repeat(gray[:, :, None], 3, axis=2)),
+                "image_rgba.png": sha(rgba[..., :3])}
+        frame = GI.frame()
+        dets = GI.detections()
+
+        class FixedDetector2:
+            def detect(self, image):
+                assert np.array_equal(image, frame)  # process_image handed process_numpy the RGB frame
+                return [{"bbox": d["bbox"].copy(), "landmarks": d["landmarks"].copy(), "det_score": d["det_score"],
+                         "pose": None, "age": None, "gender": None} for d in dets]
+
+        png = os.path.join(tmp, "gate_frame.png")
+        Image.fromarray(frame, "RGB").save(png)
+        fp = ref_fr.FaceProcessor.__new__(ref_fr.FaceProcessor)
+        fp.detector, fp.aligner, fp.quality_filter = (FixedDetector2(), ref_fr.FaceAligner(output_size=GI.S),
+                                                      ref_fr.FaceQualityFilter())
+        runs = {}
+        with quiet():
+            for ra in (False, True):
+                res = fp.process_image(png, return_all=ra)
+                runs[str(ra)] = [{"det": next(i for i, d in enumerate(dets)
+                                              if np.array_equal(d["landmarks"], r["landmarks"])),
+                                  "is_valid": bool(r["is_valid"]), "crop_sha256": sha(r["aligned_face"]),
+                                  "blur": float(r["quality_metrics"].get("blur_score", -1.0))} for r in res]
+            try:
+                fp.process_image(os.path.join(tmp, "missing.png"))
+                missing = None
+            except ValueError as e:
+                missing = str(e).replace(tmp, "<dir>")
+        np.savez_compressed(os.path.join(OUT, "image.npz"), decoded_sha256=np.array(json.dumps(want)),
+                            process_image=np.array(json.dumps(runs)), missing_error=np.array(missing))
+        print("image", {k: len(v) for k, v in runs.items()}, missing)
 
 
 if __name__ == "__main__":
