@@ -473,17 +473,27 @@ def main():
         from facerecognitionpipeline_amd.detector_arch import synthetic_detector_state_dict
         detector_sd = synthetic_detector_state_dict()
         detector = FaceDetector(device=dev, max_frames=min(32, frames.shape[0]), max_faces=64, state_dict=detector_sd)
-        # pipelined serving: batch i+1's detection runs on its own (non-blocking) stream while batch
-        # i's embed + match run on the main one.  Every step still detects exactly one batch of
-        # frames inside the timed region (the first batch's in warmup; the last step detects one
-        # batch that no timed step consumes, so the timed region holds K detections either way).
+        # pipelined serving: batch i+1's detection is started (on its own non-blocking stream, from
+        # a worker thread: fr_detect returns host detections and waits for its own stream) at the
+        # start of step i, before batch i's align / gate / embed + match are queued on the main
+        # stream, so the GPU always has the other workload queued while the host fits landmarks
+        # or waits for a sync.  Every step still detects exactly one batch of frames inside the
+        # timed region (the first batch's in warmup; the last step starts one detection that no
+        # timed step consumes, so the timed region holds K detections either way).
         det_stream = torch.cuda.Stream(device=dev)
         pending = []
+        det_pool = None
+        if args.c4_pipeline == "on":
+            from concurrent.futures import ThreadPoolExecutor
+            det_pool = ThreadPoolExecutor(1, thread_name_prefix="c4-detect")
+
+    def detect_job():
+        with torch.cuda.stream(det_stream):
+            return detector.model.detect(frames, detector.det_thresh, detector.max_faces)
 
     def detect_batch():
         if args.c4_pipeline == "on":
-            with torch.cuda.stream(det_stream):
-                return detector.model.detect(frames, detector.det_thresh, detector.max_faces)
+            return det_pool.submit(detect_job)
         return detector.model.detect(frames, detector.det_thresh, detector.max_faces)
 
     def step():
@@ -491,7 +501,10 @@ def main():
             # SCRFD on every frame (batched); each frame's top faces_per_frame detections are aligned
             # (a frame with fewer is topped up with the synthetic placements so every step embeds
             # exactly `batch` faces); blur + gate on all crops; one embed+match
-            dets, counts = pending.pop() if pending else detect_batch()
+            got = pending.pop() if pending else detect_batch()
+            dets, counts = got.result() if args.c4_pipeline == "on" else got
+            if args.c4_pipeline == "on":
+                pending.append(detect_batch())  # the next batch's detection, queued first
             o = 0
             for f in range(frames.shape[0]):
                 nf = min(args.faces_per_frame, args.batch - o)
@@ -502,15 +515,13 @@ def main():
                 det_stats["padded"] += nf - nd
                 emb.model.align_faces(frames[f], lm, 112, crops[o:o + nf])
                 o += nf
-            blur = emb.model.blur_scores(crops)  # syncs: the previous embed + match have finished
+            # syncs the main stream (the previous embed + match and this batch's aligns have
+            # finished); the next batch's detection keeps the GPU busy meanwhile
+            blur = emb.model.blur_scores(crops)
             if not (blur >= 0).all():
                 raise RuntimeError("bad blur scores")
+            # the next step's align writes the crops on the main stream, so it is ordered after this
             emb.model.embed_match(crops, k, idx, score, e_out)
-            if args.c4_pipeline == "on":
-                # fr_detect returns host detections (it syncs its own stream only); the embed + match
-                # just queued on the main stream run beside it.  The next step's align writes the
-                # crops on the main stream, so it is ordered after this embed.
-                pending.append(detect_batch())
         elif G > 0:
             emb.model.embed_match(rgb, k, idx, score, e_out)
         else:
@@ -693,6 +704,10 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    if args.config == "c4" and det_pool is not None:
+        for f in pending:
+            f.result()
+        det_pool.shutdown()
     if world > 1:
         dist.destroy_process_group()
 

@@ -168,6 +168,22 @@ __global__ __launch_bounds__(256) void upsample_add_kernel(float4* __restrict__ 
   big[i] = v;
 }
 
+// Row expansion of a reduced-height map (detector.cpp, row_plan): dst row r of each image is src
+// row r above m, src row m for the Hd - Hs rows from m on (copies of a row inside the invariant
+// run), src row r - (Hd - Hs) below them.  NHWC, one thread per (pixel, 4 channels).
+__global__ __launch_bounds__(256) void row_expand_kernel(const float4* __restrict__ x, int B, int Hs, int W, int C4,
+                                                         int m, int Hd, float4* __restrict__ y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * Hd * W * C4) return;
+  const int c = i % C4;
+  const int pix = i / C4;
+  const int col = pix % W, t = pix / W;
+  const int r = t % Hd, b = t / Hd;
+  const int ins = Hd - Hs;
+  const int sr = r < m ? r : (r < m + ins ? m : r - ins);
+  y[i] = x[((b * Hs + sr) * W + col) * C4 + c];
+}
+
 // Head outputs per level: [B][H*W][32] f32 = [cls a0, cls a1, bbox a0 (4), bbox a1 (4),
 // kps a0 (10), kps a1 (10), pad 2] logits / distances in stride units.
 __global__ __launch_bounds__(256) void decode_kernel(DetDecodeParams p) {
@@ -406,6 +422,15 @@ hipError_t launch_maxpool3(const float* x, int B, int H, int W, int C, float* y,
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool3_kernel, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(x), B, H, W, C / 4, reinterpret_cast<float4*>(y));
+  return hipGetLastError();
+}
+
+hipError_t launch_row_expand(const float* x, int B, int Hs, int W, int C, int m, int Hd, float* y, hipStream_t s) {
+  if (C % 4 || Hs < 1 || Hd < Hs || m < 0 || m >= Hs || (long long)B * Hd * W * C >= (1ll << 31))
+    return hipErrorInvalidValue;
+  const int n = B * Hd * W * (C / 4);
+  hipLaunchKernelGGL(row_expand_kernel, dim3((n + 255) / 256), dim3(256), 0, s, reinterpret_cast<const float4*>(x), B,
+                     Hs, W, C / 4, m, Hd, reinterpret_cast<float4*>(y));
   return hipGetLastError();
 }
 

@@ -63,6 +63,7 @@ struct Detector {
   int* dets_count = nullptr;
   int* tabs = nullptr;  // [det_w + det_h][4]
   int dets_cap = 0;
+  bool row_reduce = true;  // row_plan (frt_set_detector_row_reduction switches it off for A/B)
   std::vector<int> htabs;
   ~Detector() {
     (void)hipFree(arena);
@@ -71,6 +72,10 @@ struct Detector {
 };
 
 void detector_destroy(Detector* d) { delete d; }
+
+void detector_set_row_reduction(Detector* d, bool on) {
+  if (d) d->row_reduce = on;
+}
 
 void detector_convs(Detector* d, std::vector<ConvW*>& out) {
   if (!d) return;
@@ -389,7 +394,48 @@ namespace {
 struct Geometry {
   int new_w = 0, new_h = 0, simd_end = 0;
   double det_scale = 1.0;
+  int skip = 0;       // canvas rows the stem and stage 1 do not compute (row_plan)
+  int expand_at = 0;  // stage-1 output row whose copies stand in for the skipped rows
 };
+
+// Rows of a landscape letterbox the stem and stage 1 need not compute.  The canvas below the
+// resized frame (rows new_h..det_h-1) is all zeros, so every layer maps it to rows that are all
+// equal: a "run" [a, b) of identical rows between the rows the frame reaches (< a) and the rows
+// the conv zero padding below the canvas reaches (>= b).  A 3x3 pad-1 conv of stride s maps a
+// run [a, b) to [ceil((a + 1) / s), floor((b - 2) / s) + 1): each output row whose window lies in
+// the run is a run row, rows above and below it are computed from the same values at the same
+// distance from the frame / from the canvas bottom.  So the network on a canvas with D fewer run
+// rows (D a multiple of 32, every stride divides it, the bottom rows keep their parity) computes
+// the same values above and below the run, as long as the run keeps >= 3 rows at every layer --
+// which it does through stage 1 (1080p: new_h = 360, D = 192 of 640 rows, 30% of the stem's and
+// stage 1's work).  Before stage 2 the stage-1 output is expanded back to full height by copying
+// one run row into the D / 4 missing rows (launch_row_expand).  The values are the full canvas's
+// up to fp32 rounding: Winograd tiles round each row by its position in the tile, so run rows
+// equal each other mathematically, not bitwise (tests/test_gpu_detector_rows.py).  Returns D and
+// sets expand_at = the first run row of the reduced stage-1 output.
+int row_plan(int new_h, int DH, int* expand_at) {
+  *expand_at = 0;
+  if (new_h >= DH || new_h < 1) return 0;
+  int a = new_h, b = DH, s = 1, dmax = DH;
+  auto conv = [&](int stride) {
+    a = (a + 1 + stride - 1) / stride;
+    b = (b - 2) / stride + 1;
+    s *= stride;
+    const int room = (b - a - 3) * s;  // canvas rows the run can lose at this layer
+    dmax = std::min(dmax, room < 0 ? -1 : room / 32 * 32);
+  };
+  conv(2);  // stem 0 (3x3 s2)
+  conv(1);  // stem 1
+  conv(1);  // stem 2
+  conv(2);  // MaxPool2d(3, 2, 1)
+  for (int u = 0; u < STAGE_BLOCKS[0]; ++u) {  // stage 1 (stride 1, identity shortcuts)
+    conv(1);
+    conv(1);
+  }
+  if (dmax <= 0) return 0;
+  *expand_at = a;
+  return dmax;
+}
 
 // Letterbox geometry (scrfd.py detect; Python floats are doubles) and the resize tables.
 int setup_geometry(fr_handle* h, int height, int width, Geometry& g, hipStream_t s) {
@@ -409,6 +455,7 @@ int setup_geometry(fr_handle* h, int height, int width, Geometry& g, hipStream_t
   resize_axis_table(g.new_w, width, d->htabs.data());
   resize_axis_table(g.new_h, height, d->htabs.data() + 4 * g.new_w);
   g.simd_end = resize_simd_end(g.new_w * 3);
+  g.skip = d->row_reduce ? row_plan(g.new_h, DH, &g.expand_at) : 0;
   FR_HIP(h, hipMemcpyAsync(d->tabs, d->htabs.data(), d->htabs.size() * sizeof(int), hipMemcpyHostToDevice, s));
   return FR_OK;
 }
@@ -420,11 +467,13 @@ int forward_chunk(fr_handle* h, const uint8_t* fr, int B, int height, int width,
   const int* xtab = d->tabs;
   const int* ytab = d->tabs + 4 * g.new_w;
   const int c0 = pad32(STEM / 2);
-  const int H0 = DH / 2, W0 = DW / 2, H1 = H0 / 2;
+  // the stem and stage 1 run on a canvas of DH - skip rows (row_plan); W is the full width
+  const int Hc = DH - g.skip;
+  const int H0 = Hc / 2, W0 = DW / 2, H1 = H0 / 2, W1 = W0 / 2;
   const int new_w = g.new_w, new_h = g.new_h, simd_end = g.simd_end;
-  hipError_t e = launch_letterbox(fr, B, height, width, xtab, ytab, new_w, new_h, simd_end, DW, DH, d->canvas, s);
+  hipError_t e = launch_letterbox(fr, B, height, width, xtab, ytab, new_w, new_h, simd_end, DW, Hc, d->canvas, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("letterbox: ") + hipGetErrorString(e));
-  e = launch_det_stem(d->canvas, B, DH, DW, c0, d->stem_w, d->stem_scale, d->stem_shift, d->big0, s);
+  e = launch_det_stem(d->canvas, B, Hc, DW, c0, d->stem_w, d->stem_scale, d->stem_shift, d->big0, s);
   if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("det stem: ") + hipGetErrorString(e));
   int rc = dconv(h, d->stem1, d->big0, d->big1, B, H0, W0, EPI_AFFINE_PRELU, nullptr, s);
   if (rc) return rc;
@@ -439,25 +488,33 @@ int forward_chunk(fr_handle* h, const uint8_t* fr, int B, int height, int width,
       if (m != a && m != b) return m;
     return nullptr;
   };
-  int HW = H1;
+  int Hh = H1, Ww = W1;
   for (int st = 0; st < 4; ++st) {
+    if (st == 1 && g.skip) {  // stage 1's output back to full height
+      float* full = pick(x, nullptr);
+      e = launch_row_expand(x, B, Hh, Ww, pad32(STAGE_PLANES[0]), g.expand_at, DH / 4, full, s);
+      if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("row expand: ") + hipGetErrorString(e));
+      x = full;
+      Hh = DH / 4;
+    }
     for (size_t u = 0; u < d->blocks[st].size(); ++u) {
       const DetBlock& b = d->blocks[st][u];
-      const int Ho = (HW + 2 - 3) / b.conv1.stride + 1;
+      const int Ho = (Hh + 2 - 3) / b.conv1.stride + 1, Wo = (Ww + 2 - 3) / b.conv1.stride + 1;
       float* t = pick(x, nullptr);
       float* y = (st > 0 && u + 1 == d->blocks[st].size()) ? d->c_out[st - 1] : pick(x, t);
-      rc = dconv(h, b.conv1, x, t, B, HW, HW, EPI_AFFINE_PRELU, nullptr, s);
+      rc = dconv(h, b.conv1, x, t, B, Hh, Ww, EPI_AFFINE_PRELU, nullptr, s);
       if (rc) return rc;
       const float* res = x;
       if (b.has_down) {
-        rc = dconv(h, b.down, x, d->dbuf, B, HW, HW, EPI_AFFINE, nullptr, s);
+        rc = dconv(h, b.down, x, d->dbuf, B, Hh, Ww, EPI_AFFINE, nullptr, s);
         if (rc) return rc;
         res = d->dbuf;
       }
-      rc = dconv(h, b.conv2, t, y, B, Ho, Ho, EPI_AFFINE_RES_PRELU, res, s);
+      rc = dconv(h, b.conv2, t, y, B, Ho, Wo, EPI_AFFINE_RES_PRELU, res, s);
       if (rc) return rc;
       x = y;
-      HW = Ho;
+      Hh = Ho;
+      Ww = Wo;
     }
   }
   // PAFPN
@@ -573,8 +630,12 @@ int detector_forward(fr_handle* h, const uint8_t* frames, int n, int height, int
     FR_HIP(h, hipMemcpyAsync((char*)heads + off, d->hd[i], bytes, hipMemcpyDeviceToDevice, s));
     off += bytes;
   }
-  if (canvas)
-    FR_HIP(h, hipMemcpyAsync(canvas, d->canvas, (size_t)n * d->det_h * d->det_w * 3, hipMemcpyDeviceToDevice, s));
+  if (canvas) {  // the full det_h-row canvases (the rows row_plan skipped are zeros)
+    const size_t row = (size_t)d->det_w * 3, Hc = (size_t)(d->det_h - g.skip);
+    FR_HIP(h, hipMemcpy2DAsync(canvas, d->det_h * row, d->canvas, Hc * row, Hc * row, n, hipMemcpyDeviceToDevice, s));
+    if (g.skip)
+      FR_HIP(h, hipMemset2DAsync(canvas + Hc * row, d->det_h * row, 0, (size_t)g.skip * row, n, s));
+  }
   FR_HIP(h, hipStreamSynchronize(s));
   return FR_OK;
 }

@@ -2562,6 +2562,14 @@ int frt_detector_forward(fr_handle* h, const uint8_t* frames, int n, int height,
   return detector_forward(h, frames, n, height, width, heads, canvas, (hipStream_t)stream);
 }
 
+int frt_set_detector_row_reduction(fr_handle* h, int on) {
+  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!h->detector || !h->det) return fail(h, FR_ERR_STATE, "not a finalised detector handle");
+  detector_set_row_reduction(h->det, on != 0);
+  return FR_OK;
+}
+
 int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, void* stream) {
   if (k < 1 || k > G) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_topk: k must be in [1, G]");
   hipError_t e = launch_topk(scores, n, G, k, idx, val, (hipStream_t)stream);

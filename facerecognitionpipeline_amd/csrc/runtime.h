@@ -69,6 +69,7 @@ constexpr int MAX_LANES = 4;
 
 struct Detector;  // detector.cpp
 void detector_destroy(Detector* d);
+void detector_set_row_reduction(Detector* d, bool on);
 // every conv of the detector (for the Winograd filter builds); no-op for d == nullptr
 void detector_convs(Detector* d, std::vector<ConvW*>& out);
 

@@ -135,6 +135,9 @@ int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val,
  * or NULL.  Synchronises. */
 int frt_detector_forward(fr_handle* h, const uint8_t* frames, int n, int height, int width, float* heads,
                          uint8_t* canvas, void* stream);
+/* A/B: the stem and stage 1 skip the letterbox's invariant bottom rows (on, the default) or run
+ * the full 640-row canvas (0).  Both compute the same network to fp32 rounding. */
+int frt_set_detector_row_reduction(fr_handle* h, int on);
 
 #ifdef __cplusplus
 }

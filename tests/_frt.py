@@ -58,6 +58,8 @@ def lib():
         L.frt_topk.argtypes = [_P, _I, _I, _I, _P, _P, _P]
         L.frt_detector_forward.restype = _I
         L.frt_detector_forward.argtypes = [_P, _P, _I, _I, _I, _P, _P, _P]
+        L.frt_set_detector_row_reduction.restype = _I
+        L.frt_set_detector_row_reduction.argtypes = [_P, _I]
         L._frt_ready = True
     return L
 
@@ -124,6 +126,10 @@ def detector_forward(handle, frames):
         out.append(heads[off:off + n * h * w * 32].view(n, h, w, 32))
         off += n * h * w * 32
     return out, canvas
+
+
+def set_detector_row_reduction(handle, on):
+    _lib.check(lib().frt_set_detector_row_reduction(handle.h, int(on)), handle.h)
 
 
 def conv2d_s2band(x, w, B, H, W, post, res):

@@ -1,0 +1,55 @@
+"""The detector's row reduction (csrc/detector.cpp row_plan): the stem and stage 1 of SCRFD-10G skip
+the invariant zero rows below a landscape letterbox and stage 1's output is expanded back before
+stage 2.  It is the same network: head maps equal the full-canvas forward's to fp32 rounding (the
+Winograd tiles round each row by its tile position), detections the same boxes, and a frame whose
+letterbox has no bottom padding (portrait) runs exactly the full forward.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests import _frt
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(seed, n, H, W):
+    r = np.random.default_rng(seed)
+    f = r.integers(0, 256, (n, H, W, 3), dtype=np.uint8)
+    # smooth regions too, so the detector's score maps have structure
+    f[:, : H // 3] = (np.arange(W)[None, None, :, None] // 7 % 256).astype(np.uint8)
+    return torch.from_numpy(f).cuda()
+
+
+@pytest.fixture(scope="module")
+def det():
+    from facerecognitionpipeline_amd.detector_arch import synthetic_detector_state_dict
+    from facerecognitionpipeline_amd.face_recognition import FaceDetector
+    return FaceDetector(state_dict=synthetic_detector_state_dict(), max_frames=4)
+
+
+@pytest.mark.parametrize("shape", [(1080, 1920), (720, 1280), (600, 1400), (481, 367)])
+def test_row_reduction_is_the_full_canvas_network(det, shape):
+    frames = _frames(sum(shape), 3, *shape)
+    try:
+        _frt.set_detector_row_reduction(det.model, 0)
+        full, canvas_full = _frt.detector_forward(det.model, frames)
+        full = [x.clone() for x in full]
+        d_full, c_full = det.model.detect(frames, 0.5, 256)
+    finally:
+        _frt.set_detector_row_reduction(det.model, 1)
+    red, canvas_red = _frt.detector_forward(det.model, frames)
+    d_red, c_red = det.model.detect(frames, 0.5, 256)
+    assert torch.equal(canvas_full, canvas_red)
+    portrait = shape[0] >= shape[1]
+    for lv in range(3):
+        a, b = full[lv].cpu().numpy(), red[lv].cpu().numpy()
+        if portrait:  # no bottom padding: nothing skipped, the same launches
+            assert np.array_equal(a, b), lv
+        scale = np.abs(a).max()
+        assert np.abs(a - b).max() <= 1e-5 * scale, (shape, lv, np.abs(a - b).max() / scale)
+    assert np.array_equal(c_full, c_red)
+    for f in range(frames.shape[0]):
+        n = int(c_full[f])
+        assert n > 0
+        assert np.abs(d_full[f, :n] - d_red[f, :n]).max() <= 1e-3, (shape, f)

@@ -35,12 +35,16 @@ def pad32(c):
     return (c + 31) // 32 * 32
 
 
-def det_layers(B, W=640, H=640, src=(1080, 1920)):
+def det_layers(B, W=640, H=640, src=(1080, 1920), skip=192):
     """[(name, kind, alg_flop, exec_flop_wino4, exec_flop_direct, alg_bytes)] in launch order.
     kind: 'conv3' (3x3 stride 1: F(4x4) when eligible), 'convd' (direct: strided / 1x1 / 2x2),
-    or the elementwise kernel's name."""
+    or the elementwise kernel's name.  alg_flop is the reference network's (full 640-row canvas);
+    the executed FLOPs and bytes of the stem and stage 1 count the (H - skip)-row canvas they run
+    on (detector.cpp row_plan; 192 rows for a 1080p frame), and 'row_expand' (optional: absent
+    when nothing is skipped) restores stage 1's output to full height."""
     f4 = 4.0
     L = []
+    red = [(H - skip) / H]
 
     def conv(name, ci, co, hw_in, k, s, res=False):
         ho = (hw_in + 2 * (k // 2 if k == 3 else 0) - k) // s + 1
@@ -48,24 +52,28 @@ def det_layers(B, W=640, H=640, src=(1080, 1920)):
         alg = 2.0 * B * ho * ho * co * ci * k * k
         # F(4x4): 36 products per 4x4 tile (H % 4 == 0 here: no canvas separators), couts in
         # quarters of 16 (an idle quarter of a 64-cout item issues no MFMAs)
-        ex_w4 = 2.0 * 36 * B * (ho // 4) * (ho // 4) * cip * ((cop + 15) // 16 * 16)
-        ex_d = 2.0 * B * ho * ho * cop * cip * k * k
-        by = f4 * (B * hw_in * hw_in * cip + cop * cip * k * k + B * ho * ho * cop * (2 if res else 1))
+        ex_w4 = red[0] * 2.0 * 36 * B * (ho // 4) * (ho // 4) * cip * ((cop + 15) // 16 * 16)
+        ex_d = red[0] * 2.0 * B * ho * ho * cop * cip * k * k
+        by = red[0] * f4 * (B * hw_in * hw_in * cip + cop * cip * k * k + B * ho * ho * cop * (2 if res else 1))
         L.append((name, "conv3" if (k == 3 and s == 1) else "convd", alg, ex_w4, ex_d, by))
         return ho
 
     L.append(("letterbox", "letterbox", 0.0, 0.0, 0.0,
               # reads the frame rows the resize touches once (at most the whole frame), writes the canvas
-              float(B * src[0] * src[1] * 3 + B * W * H * 3)))
+              float(B * src[0] * src[1] * 3 + red[0] * B * W * H * 3)))
     h = H // 2
-    L.append(("stem0 3->28 s2 @640 (+blob)", "det_stem", 2.0 * B * h * h * 28 * 27, 2.0 * B * h * h * 32 * 28, 0.0,
-              float(B * W * H * 3) + f4 * B * h * h * 32))
+    L.append(("stem0 3->28 s2 @640 (+blob)", "det_stem", 2.0 * B * h * h * 28 * 27,
+              red[0] * 2.0 * B * h * h * 32 * 28, 0.0, red[0] * (float(B * W * H * 3) + f4 * B * h * h * 32)))
     conv("stem1 28->28 @320", 28, 28, h, 3, 1)
     conv("stem2 28->56 @320", 28, 56, h, 3, 1)
-    L.append(("maxpool3 s2 @320", "maxpool3", 0.0, 0.0, 0.0, f4 * B * (h * h + (h // 2) ** 2) * 64))
+    L.append(("maxpool3 s2 @320", "maxpool3", 0.0, 0.0, 0.0, red[0] * f4 * B * (h * h + (h // 2) ** 2) * 64))
     hw = h // 2
     cin = STEM
     for st, (n, c) in enumerate(zip(STAGE_BLOCKS, STAGE_PLANES)):
+        if st == 1:
+            L.append(("row_expand s1 out @160", "row_expand?", 0.0, 0.0, 0.0,
+                      f4 * B * hw * hw * 64 * (1 + red[0]) if skip else 0.0))
+            red[0] = 1.0
         for u in range(n):
             ci = cin if u == 0 else c
             s = 2 if (u == 0 and st > 0) else 1
@@ -123,6 +131,12 @@ def segments(rows, L):
             if li == len(L):
                 break
             kind = L[li][1]
+            if kind.endswith("?"):  # optional layer: present only when its kernel ran
+                if kind[:-1] + "_kernel" in kn:
+                    seg.append((li, [rows[j]]))
+                    j += 1
+                li += 1
+                continue
             want = any(c in kn for c in CONV_KERNELS) if kind in ("conv3", "convd") else (kind + "_kernel" in kn
                                                                                           or kind + "_mfma" in kn)
             if not want:
@@ -148,9 +162,12 @@ def main():
     ap.add_argument("--pmc", nargs="*", default=[])
     ap.add_argument("--json", default=None)
     ap.add_argument("--build", default=None)
+    ap.add_argument("--skip", type=int, default=None,
+                    help="canvas rows the stem and stage 1 skipped (default: 192 if row_expand_kernel ran, else 0)")
     a = ap.parse_args()
-    L = det_layers(a.frames)
     rows = read_csv(glob.glob(os.path.join(a.trace_dir, "*kernel_trace.csv"))[0])
+    skip = a.skip if a.skip is not None else (192 if any("row_expand" in r["Kernel_Name"] for r in rows) else 0)
+    L = det_layers(a.frames, skip=skip)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     segs = segments(rows, L)
     if not segs:
@@ -184,7 +201,8 @@ def main():
                     acc["GRBM_GUI_ACTIVE"] = ga
                 for cn, v in acc.items():
                     pmc[cn][li].append(v)
-    print(f"detects aligned: {len(segs)} (B = {a.frames} frames of 1080p, 640x640 letterbox)")
+    print(f"detects aligned: {len(segs)} (B = {a.frames} frames of 1080p, 640x640 letterbox; stem + stage 1 on "
+          f"{640 - skip} canvas rows)")
     print(f"detect wall (first dispatch start -> nms end), median: "
           f"{sorted(detect_ns)[len(detect_ns) // 2] / 1e6:.3f} ms")
     hdr = (f"{'layer':36s} {'kernel':22s} {'avg us':>8s} {'%time':>6s} {'algGF':>7s} {'algTF':>6s} {'exeTF':>6s}"
@@ -255,7 +273,7 @@ def main():
               f"{d['exec_tflops']:6.1f} {100 * d['exec_tflops'] / PEAK:5.1f} {d['alg_GBps']:7.0f} "
               + (f"{d['hbm_bytes'] / d['alg_bytes']:7.2f} " if "hbm_bytes" in d and d["alg_bytes"] else f"{'-':>7s} ")
               + (f"{100 * d['mfma_busy_frac']:7.1f}%" if "mfma_busy_frac" in d else f"{'-':>8s}"))
-    res = {"frames": a.frames, "detects": len(segs),
+    res = {"frames": a.frames, "detects": len(segs), "skip_rows": skip,
            "detect_wall_ms": sorted(detect_ns)[len(detect_ns) // 2] / 1e6,
            "kernel_ms": total / 1e6, "alg_flop": sum(x[2] for x in L), "layers": out_layers, "families": fams}
     if a.build:
