@@ -235,6 +235,80 @@ def profile_figures(traffic_json, family, build, same_workload):
     return traffic, kj.get("alg_bytes_per_launch"), kj.get("mfma_busy_frac"), src, None
 
 
+def detector_profile_figures(build):
+    """PMC figures of the detector's F(4x4) launches from the committed detector profile
+    (profiles/r*/det_layers_pmc.json, tools/gpu_det_profile.sh -> tools/det_prof_summary.py), only
+    when it was taken on this library build: (HBM bytes per launch, algorithmic bytes per launch,
+    MFMA-busy fraction, source, note)."""
+    import glob
+    cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "det_layers_pmc.json")))
+    if not cands:
+        return None, None, None, None, "no detector PMC profile found"
+    with open(cands[-1]) as f:
+        pj = json.load(f)
+    rel = os.path.relpath(cands[-1], REPO)
+    want = build_id_of(build)
+    if pj.get("build_id") != want:
+        return None, None, None, None, (f"{rel} was collected on build {pj.get('build_id')}, the loaded library is "
+                                        f"build {want}: its PMC figures are not attached")
+    fam = pj.get("families", {}).get("wino4_kernel", {})
+    n = fam.get("layers") or 0
+    if not n or "hbm_bytes" not in fam:
+        return None, None, None, None, f"{rel} has no PMC figures for wino4_kernel"
+    return (fam["hbm_bytes"] / n, fam["alg_bytes"] / n, fam.get("mfma_busy_frac"),
+            rel + f" (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of tools/det_time.py, build {want})", None)
+
+
+def detector_roofline(detector, frames, det_stream, build, reps=5):
+    """The detector's own roofline, measured live: `reps` fr_detect calls of the step's frames on the
+    detector stream with nothing else queued, HIP events around them (detect_ms per call, D2H of the
+    detections included) and the handle's per-launch event pairs (fr_profile_*) for the conv
+    families.  achieved / frac count the products F(4x4) performs on the MFMA pipe (fp32 peak)."""
+    dm = detector.model
+    torch.cuda.synchronize()
+    dm.profile_enable(True)
+    dm.profile_read()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(det_stream):
+        e0.record(det_stream)
+        for _ in range(reps):
+            dm.detect(frames, detector.det_thresh, detector.max_faces)
+        e1.record(det_stream)
+    e1.synchronize()
+    prof = dm.profile_read()
+    dm.profile_enable(False)
+    detect_ms = e0.elapsed_time(e1) / reps
+    w, d = prof["winograd"], prof["direct"]
+    n_fr = int(frames.shape[0])
+    alg = 2.0 * detector_macs() * n_fr
+    ach = w["exec_flop"] / (w["ms"] * 1e-3) / 1e12 if w["ms"] else 0.0
+    traffic, alg_bytes, busy, src, note = detector_profile_figures(build)
+    out = {"bound": "mfma",
+           "kernel": "wino4_kernel (detector instances: every stride-1 3x3 conv of SCRFD-10G, F(4x4,3x3) f32)",
+           "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+           "traffic": traffic, "traffic_from_profile": traffic is not None, "traffic_source": src,
+           "traffic_note": note, "alg_bytes_per_launch": alg_bytes,
+           "mfma_busy_frac_from_profile": round(busy, 4) if busy is not None else None,
+           "launches_per_detect": w["launches"] // reps, "avg_launch_ms": round(w["ms"] / max(w["launches"], 1), 5),
+           "flop_per_launch": w["exec_flop"] / max(w["launches"], 1),
+           "alg_equiv_tflops": round(w["flop"] / (w["ms"] * 1e-3) / 1e12, 3) if w["ms"] else 0.0,
+           "share_of_detect": round(w["ms"] / (detect_ms * reps), 4),
+           "other_conv_kernel": {"kernel": "conv_mfma_kernel (stride-2 / 2x2 / 1x1 convs)",
+                                 "tflops": round(d["flop"] / (d["ms"] * 1e-3) / 1e12, 3) if d["ms"] else 0.0,
+                                 "frac": round(d["flop"] / (d["ms"] * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)
+                                 if d["ms"] else 0.0,
+                                 "launches_per_detect": d["launches"] // reps,
+                                 "share_of_detect": round(d["ms"] / (detect_ms * reps), 4)},
+           "frames_per_detect": n_fr, "detect_ms": round(detect_ms, 4),
+           "alg_flop_per_detect": alg, "detect_alg_tflops": round(alg / (detect_ms * 1e-3) / 1e12, 3),
+           "library_build": build,
+           "note": ("standalone detects (nothing else queued) after the timed steps; alg_flop_per_detect is the "
+                    "reference network's direct-conv count (unpadded channels, full 640x640 canvas), "
+                    "detect_alg_tflops its rate over the whole detect (letterbox to NMS + D2H)")}
+    return out
+
+
 PRESETS = {"c2": ("ir_50", 0), "c3": ("ir_101", 1000), "c4": ("ir_101", 1000), "c5": ("ir_101", 100_000)}
 
 
@@ -469,7 +543,13 @@ def main():
     if args.config == "c4":
         from facerecognitionpipeline_amd.face_recognition import FaceDetector
         frames, lms = c4_inputs(args.batch, args.faces_per_frame, dev)
-        crops = torch.empty((args.batch, 112, 112, 3), dtype=torch.uint8, device=dev)
+        # two crop buffers: batch i's align + blur run on their own stream (aux) into one while batch
+        # i - 1's embed + match still read the other, so the blur's sync waits for this batch's
+        # aligns only, and the embed of batch i is queued before batch i - 1's has finished
+        crop_bufs = [torch.empty((args.batch, 112, 112, 3), dtype=torch.uint8, device=dev) for _ in range(2)]
+        aux = torch.cuda.Stream(device=dev)
+        embed_done = [None, None]  # event after the last embed + match that read each buffer
+        step_no = [0]
         from facerecognitionpipeline_amd.detector_arch import synthetic_detector_state_dict
         detector_sd = synthetic_detector_state_dict()
         detector = FaceDetector(device=dev, max_frames=min(32, frames.shape[0]), max_faces=64, state_dict=detector_sd)
@@ -505,23 +585,30 @@ def main():
             dets, counts = got.result() if args.c4_pipeline == "on" else got
             if args.c4_pipeline == "on":
                 pending.append(detect_batch())  # the next batch's detection, queued first
-            o = 0
-            for f in range(frames.shape[0]):
-                nf = min(args.faces_per_frame, args.batch - o)
-                nd = min(int(counts[f]), nf)
-                lm = lms[f][:nf].copy()
-                lm[:nd] = dets[f, :nd, 5:15].reshape(nd, 5, 2)
-                det_stats["detected"] += nd
-                det_stats["padded"] += nf - nd
-                emb.model.align_faces(frames[f], lm, 112, crops[o:o + nf])
-                o += nf
-            # syncs the main stream (the previous embed + match and this batch's aligns have
-            # finished); the next batch's detection keeps the GPU busy meanwhile
-            blur = emb.model.blur_scores(crops)
+            b = step_no[0] % 2
+            step_no[0] += 1
+            crops = crop_bufs[b]
+            with torch.cuda.stream(aux):
+                if embed_done[b] is not None:
+                    aux.wait_event(embed_done[b])  # the embed that last read this buffer
+                o = 0
+                for f in range(frames.shape[0]):
+                    nf = min(args.faces_per_frame, args.batch - o)
+                    nd = min(int(counts[f]), nf)
+                    lm = lms[f][:nf].copy()
+                    lm[:nd] = dets[f, :nd, 5:15].reshape(nd, 5, 2)
+                    det_stats["detected"] += nd
+                    det_stats["padded"] += nf - nd
+                    emb.model.align_faces(frames[f], lm, 112, crops[o:o + nf])
+                    o += nf
+                # syncs the aux stream only: this batch's aligns + blur
+                blur = emb.model.blur_scores(crops)
             if not (blur >= 0).all():
                 raise RuntimeError("bad blur scores")
-            # the next step's align writes the crops on the main stream, so it is ordered after this
+            main = torch.cuda.current_stream(dev)
+            main.wait_stream(aux)
             emb.model.embed_match(crops, k, idx, score, e_out)
+            embed_done[b] = main.record_event()
         elif G > 0:
             emb.model.embed_match(rgb, k, idx, score, e_out)
         else:
@@ -560,6 +647,11 @@ def main():
     tprof = timed_steps()
     prof = emb.model.profile_read()
     emb.model.profile_enable(False)
+    if args.config == "c4" and det_pool is not None:
+        for f in pending:  # the detection the last step started (no timed step consumes it)
+            f.result()
+        pending.clear()
+        det_pool.shutdown()
 
     # sanity: probes are noisy copies of gallery rows i % G
     top1_ok = (float((idx[:, 0].cpu().numpy() == np.arange(args.batch) % G0).mean())
@@ -685,6 +777,8 @@ def main():
             "top1_self_match": top1_ok,
             "roofline": roofline,
         }
+        if args.config == "c4":
+            roofline["detector"] = detector_roofline(detector, frames, det_stream, build)
         if world > 1:
             # the fastest and the slowest rank's timed region (value uses the slowest)
             out["rank_ms_per_step_min"], out["rank_ms_per_step_max"] = rank_ms
@@ -704,10 +798,6 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    if args.config == "c4" and det_pool is not None:
-        for f in pending:
-            f.result()
-        det_pool.shutdown()
     if world > 1:
         dist.destroy_process_group()
 

@@ -45,7 +45,7 @@ _SIGNATURES = {
     "fr_embed_match": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "fr_align_faces": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P, _P]),
     "fr_warp_affine": (_I, [_P, _P, _I, _I, _P, _I, _I, _P, _P]),
-    "fr_blur_scores": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "fr_blur_scores": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "fr_detect": (_I, [_P, _P, _I, _I, _I, ctypes.c_float, _I, _P, _P, _P]),
     "fr_set_precision": (_I, [_P, _I]),
     "fr_set_conv_algorithm": (_I, [_P, _I]),
@@ -242,8 +242,8 @@ class Handle:
         n = crops.shape[0]
         c = 1 if crops.dim() == 3 else crops.shape[3]
         out = np.empty(n, dtype=np.float64)
-        check(self._lib.fr_blur_scores(self.h, ptr(crops), n, crops.shape[1], crops.shape[2], c, out.ctypes.data),
-              self.h)
+        check(self._lib.fr_blur_scores(self.h, ptr(crops), n, crops.shape[1], crops.shape[2], c, out.ctypes.data,
+                                       stream_of(self.device)), self.h)
         return out
 
     # -- detector (arch "scrfd_10g") ---------------------------------------

@@ -394,47 +394,66 @@ namespace {
 struct Geometry {
   int new_w = 0, new_h = 0, simd_end = 0;
   double det_scale = 1.0;
-  int skip = 0;       // canvas rows the stem and stage 1 do not compute (row_plan)
-  int expand_at = 0;  // stage-1 output row whose copies stand in for the skipped rows
+  int skip1 = 0, skip2 = 0;  // canvas rows the stem + stage 1 / stage 2 do not compute (row_plan)
+  int at1 = 0, at2 = 0;      // stage-1 / stage-2 output rows whose copies stand in for skipped rows
 };
 
-// Rows of a landscape letterbox the stem and stage 1 need not compute.  The canvas below the
+// Rows of a landscape letterbox the stem and stages 1-2 need not compute.  The canvas below the
 // resized frame (rows new_h..det_h-1) is all zeros, so every layer maps it to rows that are all
 // equal: a "run" [a, b) of identical rows between the rows the frame reaches (< a) and the rows
 // the conv zero padding below the canvas reaches (>= b).  A 3x3 pad-1 conv of stride s maps a
-// run [a, b) to [ceil((a + 1) / s), floor((b - 2) / s) + 1): each output row whose window lies in
-// the run is a run row, rows above and below it are computed from the same values at the same
-// distance from the frame / from the canvas bottom.  So the network on a canvas with D fewer run
-// rows (D a multiple of 32, every stride divides it, the bottom rows keep their parity) computes
-// the same values above and below the run, as long as the run keeps >= 3 rows at every layer --
-// which it does through stage 1 (1080p: new_h = 360, D = 192 of 640 rows, 30% of the stem's and
-// stage 1's work).  Before stage 2 the stage-1 output is expanded back to full height by copying
-// one run row into the D / 4 missing rows (launch_row_expand).  The values are the full canvas's
-// up to fp32 rounding: Winograd tiles round each row by its position in the tile, so run rows
-// equal each other mathematically, not bitwise (tests/test_gpu_detector_rows.py).  Returns D and
-// sets expand_at = the first run row of the reduced stage-1 output.
-int row_plan(int new_h, int DH, int* expand_at) {
-  *expand_at = 0;
-  if (new_h >= DH || new_h < 1) return 0;
+// run [a, b) to [ceil((a + 1) / s), floor((b - 2) / s) + 1) (a 2x2 stride-2 pad-0 conv to
+// [ceil(a / 2), floor((b - 2) / 2) + 1)): each output row whose window lies in the run is a run
+// row, rows above and below it are computed from the same values at the same distance from the
+// frame / from the canvas bottom.  So the network on a canvas with D fewer run rows (D a
+// multiple of 32: every stride divides it, the bottom rows keep their parity) computes the same
+// values above and below the run, as long as the run keeps >= 3 rows at every layer.  For a
+// 1080p frame (new_h = 360) the stem and stage 1 run with D1 = 192 of 640 rows skipped, stage 2
+// with D2 = 64; stage 1's output is expanded from D1 to D2 skipped rows and stage 2's to the full
+// height by copying one run row into the missing rows (launch_row_expand).  The values are the
+// full canvas's up to fp32 rounding: Winograd tiles round each row by its position in the tile,
+// so run rows equal each other mathematically, not bitwise (tests/test_gpu_detector_rows.py).
+void row_plan(int new_h, int DH, Geometry& g) {
+  g.skip1 = g.skip2 = g.at1 = g.at2 = 0;
+  if (new_h >= DH || new_h < 1) return;
   int a = new_h, b = DH, s = 1, dmax = DH;
-  auto conv = [&](int stride) {
+  auto room = [&]() {
+    const int r = (b - a - 3) * s;  // canvas rows the run can lose at this layer
+    dmax = std::min(dmax, r < 0 ? -1 : r / 32 * 32);
+  };
+  auto conv3 = [&](int stride) {
     a = (a + 1 + stride - 1) / stride;
     b = (b - 2) / stride + 1;
     s *= stride;
-    const int room = (b - a - 3) * s;  // canvas rows the run can lose at this layer
-    dmax = std::min(dmax, room < 0 ? -1 : room / 32 * 32);
+    room();
   };
-  conv(2);  // stem 0 (3x3 s2)
-  conv(1);  // stem 1
-  conv(1);  // stem 2
-  conv(2);  // MaxPool2d(3, 2, 1)
+  conv3(2);  // stem 0 (3x3 s2)
+  conv3(1);  // stem 1
+  conv3(1);  // stem 2
+  conv3(2);  // MaxPool2d(3, 2, 1)
   for (int u = 0; u < STAGE_BLOCKS[0]; ++u) {  // stage 1 (stride 1, identity shortcuts)
-    conv(1);
-    conv(1);
+    conv3(1);
+    conv3(1);
   }
-  if (dmax <= 0) return 0;
-  *expand_at = a;
-  return dmax;
+  if (dmax <= 0) return;
+  g.skip1 = dmax;
+  g.at1 = a;
+  for (int u = 0; u < STAGE_BLOCKS[1]; ++u) {  // stage 2
+    if (u == 0) {  // conv1 3x3 s2 and the 2x2 s2 downsample both read the block input
+      const int da = (a + 1) / 2, db = (b - 2) / 2 + 1;
+      conv3(2);
+      conv3(1);
+      a = std::max(a, da);  // conv2 + downsample: rows equal in both are run rows
+      b = std::min(b, db);
+      room();
+    } else {
+      conv3(1);
+      conv3(1);
+    }
+  }
+  if (dmax <= 0) return;
+  g.skip2 = dmax;
+  g.at2 = a;
 }
 
 // Letterbox geometry (scrfd.py detect; Python floats are doubles) and the resize tables.
@@ -455,7 +474,7 @@ int setup_geometry(fr_handle* h, int height, int width, Geometry& g, hipStream_t
   resize_axis_table(g.new_w, width, d->htabs.data());
   resize_axis_table(g.new_h, height, d->htabs.data() + 4 * g.new_w);
   g.simd_end = resize_simd_end(g.new_w * 3);
-  g.skip = d->row_reduce ? row_plan(g.new_h, DH, &g.expand_at) : 0;
+  if (d->row_reduce) row_plan(g.new_h, DH, g);
   FR_HIP(h, hipMemcpyAsync(d->tabs, d->htabs.data(), d->htabs.size() * sizeof(int), hipMemcpyHostToDevice, s));
   return FR_OK;
 }
@@ -467,8 +486,8 @@ int forward_chunk(fr_handle* h, const uint8_t* fr, int B, int height, int width,
   const int* xtab = d->tabs;
   const int* ytab = d->tabs + 4 * g.new_w;
   const int c0 = pad32(STEM / 2);
-  // the stem and stage 1 run on a canvas of DH - skip rows (row_plan); W is the full width
-  const int Hc = DH - g.skip;
+  // the stem and stage 1 run on a canvas of DH - skip1 rows, stage 2 on DH - skip2 (row_plan)
+  const int Hc = DH - g.skip1;
   const int H0 = Hc / 2, W0 = DW / 2, H1 = H0 / 2, W1 = W0 / 2;
   const int new_w = g.new_w, new_h = g.new_h, simd_end = g.simd_end;
   hipError_t e = launch_letterbox(fr, B, height, width, xtab, ytab, new_w, new_h, simd_end, DW, Hc, d->canvas, s);
@@ -490,18 +509,26 @@ int forward_chunk(fr_handle* h, const uint8_t* fr, int B, int height, int width,
   };
   int Hh = H1, Ww = W1;
   for (int st = 0; st < 4; ++st) {
-    if (st == 1 && g.skip) {  // stage 1's output back to full height
+    if (st == 1 && g.skip1) {  // stage 1's output to stage 2's height
       float* full = pick(x, nullptr);
-      e = launch_row_expand(x, B, Hh, Ww, pad32(STAGE_PLANES[0]), g.expand_at, DH / 4, full, s);
+      e = launch_row_expand(x, B, Hh, Ww, pad32(STAGE_PLANES[0]), g.at1, (DH - g.skip2) / 4, full, s);
       if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("row expand: ") + hipGetErrorString(e));
       x = full;
-      Hh = DH / 4;
+      Hh = (DH - g.skip2) / 4;
+    }
+    if (st == 2 && g.skip2) {  // stage 2's output (the FPN's level-0 input) to full height
+      e = launch_row_expand(x, B, Hh, Ww, pad32(STAGE_PLANES[1]), g.at2, DH / 8, d->c_out[0], s);
+      if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("row expand: ") + hipGetErrorString(e));
+      x = d->c_out[0];
+      Hh = DH / 8;
     }
     for (size_t u = 0; u < d->blocks[st].size(); ++u) {
       const DetBlock& b = d->blocks[st][u];
       const int Ho = (Hh + 2 - 3) / b.conv1.stride + 1, Wo = (Ww + 2 - 3) / b.conv1.stride + 1;
       float* t = pick(x, nullptr);
-      float* y = (st > 0 && u + 1 == d->blocks[st].size()) ? d->c_out[st - 1] : pick(x, t);
+      // the stages' outputs go to c_out[] (the FPN's inputs); stage 2's through the expansion
+      const bool last = st > 0 && u + 1 == d->blocks[st].size() && !(st == 1 && g.skip2);
+      float* y = last ? d->c_out[st - 1] : pick(x, t);
       rc = dconv(h, b.conv1, x, t, B, Hh, Ww, EPI_AFFINE_PRELU, nullptr, s);
       if (rc) return rc;
       const float* res = x;
@@ -631,10 +658,10 @@ int detector_forward(fr_handle* h, const uint8_t* frames, int n, int height, int
     off += bytes;
   }
   if (canvas) {  // the full det_h-row canvases (the rows row_plan skipped are zeros)
-    const size_t row = (size_t)d->det_w * 3, Hc = (size_t)(d->det_h - g.skip);
+    const size_t row = (size_t)d->det_w * 3, Hc = (size_t)(d->det_h - g.skip1);
     FR_HIP(h, hipMemcpy2DAsync(canvas, d->det_h * row, d->canvas, Hc * row, Hc * row, n, hipMemcpyDeviceToDevice, s));
-    if (g.skip)
-      FR_HIP(h, hipMemset2DAsync(canvas + Hc * row, d->det_h * row, 0, (size_t)g.skip * row, n, s));
+    if (g.skip1)
+      FR_HIP(h, hipMemset2DAsync(canvas + Hc * row, d->det_h * row, 0, (size_t)g.skip1 * row, n, s));
   }
   FR_HIP(h, hipStreamSynchronize(s));
   return FR_OK;

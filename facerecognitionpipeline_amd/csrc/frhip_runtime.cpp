@@ -470,6 +470,8 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // (layers of at most convs_max_m(B) output pixels: stage 1's 112x112 conv1, 784 pixel blocks
   // x 4 cout blocks, stays on F(4x4) split-K, which is faster there: 54 vs ~20 us)
   if (convs_takes(h, cw, p, epi, nsplit, x2 != nullptr)) {
+    if (h->w4_blk)  // forward_lanes plans F(4x4) layouts only when no lane reaches this branch
+      return fail(h, FR_ERR_HIP, "internal: F(4x4) channel-blocked activations in the serving conv kernel");
     p.w = cw.w_frag;
     if (int rc = chain_flush(h, s)) return rc;
     p.blk = h->convs_blk;
@@ -777,7 +779,11 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
   // stem's, the stride-2 / shortcut / FC kernels' inputs and outputs -- stays NHWC.  The layouts
   // change nothing in the arithmetic: embeddings are bitwise the NHWC forward's (tested).
   std::vector<char> w4r_blk(nb, 0), w4y_blk(nb, 0);
-  if (h->w4_blocked && cnt[0] > h->convs_max_n && !h->chain_collect && !h->detector) {
+  // (every lane must be past the serving kernel's batch limit: with an uneven split a smaller lane
+  // could take the serving branch, which does not read the F(4x4) layout bits)
+  int cnt_min = cnt[0];
+  for (int l = 1; l < nl; ++l) cnt_min = std::min(cnt_min, cnt[l]);
+  if (h->w4_blocked && cnt_min > h->convs_max_n && !h->chain_collect && !h->detector) {
     std::vector<char> c1(nb, 0), c2(nb, 0);
     int hw = 112;
     for (size_t bi = 0; bi < nb; ++bi) {
@@ -2050,7 +2056,8 @@ int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, co
   return FR_OK;
 }
 
-int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int height, int width, int channels, double* scores) {
+int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int height, int width, int channels, double* scores,
+                   void* stream) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
   if (n < 0 || height < 1 || width < 1 || (long long)height * width >= (1ll << 31) ||
@@ -2064,7 +2071,7 @@ int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int height, int wi
   const int per = 65535;  // images per launch (grid y of the multi-block form)
   const size_t ws = blur_workspace_bytes(std::min(n, per), height, width);
   if (ws && (rc = ensure_buf(h, &h->blur_ws, &h->blur_ws_cap, ws))) return rc;
-  hipStream_t s = nullptr;
+  hipStream_t s = (hipStream_t)stream;
   for (int off = 0; off < n; off += per) {
     const int m = std::min(per, n - off);
     hipError_t e = launch_blur(crops + (size_t)off * img, m, height, width, channels, (double*)h->blur_out + off,

@@ -17,22 +17,29 @@ full re-upload; ``pending_delta`` gives the same delta to ship to other GPUs
 once on the GPU (``fr_build_templates``: quality filter + mean / median /
 weighted_mean + L2, ``:104-122``, ``:297-317``).
 
-Persistence: ``save`` writes one ``.npz`` (every array and, as a JSON string,
-every record's fields: a single atomic file) plus the reference's own
-informational ``.json`` sidecar (same keys as ``:211-229``; nothing reads it
-back).  ``load`` reads that ``.npz`` or the REFERENCE's gallery pickle
-(``pickle.dump(self.students)``, ``:207-210,234-244``) through a restricted
-unpickler that resolves only numpy's array reconstruction and the reference's
-``StudentRecord`` (mapped onto this module's dataclass) and executes nothing
-else from the file; an unreadable or foreign pickle raises, it never turns into
-an empty gallery.  ``load_backup`` reads the reference's ``export_for_backup``
-JSON (``:246-270``).
+Persistence: ``save`` writes the reference's own gallery file -- ``<stem>.pkl``
+= ``pickle.dump(dict[str, gallery_manager.StudentRecord])`` with the same
+fields (``:207-210``), so the reference's ``load`` and every reference tool
+reads enrollments made here -- plus one ``.npz`` (every array and, as a JSON
+string, every record's fields and the signature of the ``.pkl`` written with
+it: a single atomic file) and the reference's informational ``.json`` sidecar
+(same keys as ``:211-229``).  ``load`` reads the ``.npz`` or, when the ``.pkl``
+no longer matches the signature the ``.npz`` recorded (the reference app wrote
+it since), the ``.pkl``, through a restricted unpickler that resolves only
+numpy's array reconstruction and the reference's ``StudentRecord`` (mapped onto
+this module's dataclass) and executes nothing else from the file; an unreadable
+or foreign pickle raises, it never turns into an empty gallery.
+``export_for_backup`` copies the gallery files (``:246-270``: ``FileNotFoundError``
+when there is none) and ``load_backup`` reads its JSON.
 """
 from __future__ import annotations
 
 import copy
+import errno
+import hashlib
 import importlib
 import json
+import logging
 import os
 import pickle
 import shutil
@@ -145,14 +152,89 @@ def load_reference_pickle(path: str) -> Dict[str, "StudentRecord"]:
     return out
 
 
+# -- writing the reference's gallery pickle ------------------------------------------------------
+class _RefStudentRecord:
+    """Stand-in that pickles as the reference's ``gallery_manager.StudentRecord`` (never instantiated)."""
+
+
+_RECORD_FIELDS = ("student_id", "name", "embeddings", "template_embedding", "num_samples", "enrollment_date",
+                  "last_updated", "metadata")
+
+
+class _ReferencePickler(pickle._Pickler):
+    """``pickle.dump(self.students)`` as the reference's ``save`` runs it (gallery_manager.py:207-210):
+    each record is a ``gallery_manager.StudentRecord`` rebuilt by NEWOBJ + BUILD from its eight
+    dataclass fields in declaration order; numpy arrays pickle through numpy's own reduction.  The
+    reference's module need not be importable here: the class is written by name."""
+
+    def __init__(self, f):
+        super().__init__(f, protocol=pickle.DEFAULT_PROTOCOL)
+
+    def _save_record(self, obj):
+        # what save_reduce writes for copyreg.__newobj__(cls) + state, with the reference's class
+        self.save(_RefStudentRecord)
+        self.save(())
+        self.write(pickle.NEWOBJ)
+        self.memoize(obj)
+        self.save({k: getattr(obj, k) for k in _RECORD_FIELDS})
+        self.write(pickle.BUILD)
+
+    dispatch = dict(pickle._Pickler.dispatch)
+
+    def save_global(self, obj, name=None):
+        if obj is not _RefStudentRecord:
+            return super().save_global(obj, name)
+        if self.proto >= 4:
+            self.save("gallery_manager")
+            self.save("StudentRecord")
+            self.write(pickle.STACK_GLOBAL)
+        else:
+            self.write(pickle.GLOBAL + b"gallery_manager\nStudentRecord\n")
+        self.memoize(obj)
+
+
+_ReferencePickler.dispatch[StudentRecord] = _ReferencePickler._save_record
+
+
+def dump_reference_pickle(students: Dict[str, "StudentRecord"], f) -> None:
+    """Write ``students`` in the reference's gallery-file format (readable by its ``load``)."""
+    _ReferencePickler(f).dump(students)
+
+
+def _file_signature(path: str) -> Optional[Dict]:
+    """{"size", "sha256"} of a file, or None when it does not exist."""
+    try:
+        h = hashlib.sha256()
+        n = 0
+        with open(path, "rb") as f:
+            for chunk in iter(lambda: f.read(1 << 20), b""):
+                h.update(chunk)
+                n += len(chunk)
+        return {"size": n, "sha256": h.hexdigest()}
+    except FileNotFoundError:
+        return None
+
+
+_log = logging.getLogger(__name__)
+# the process umask, read once at import (os.umask can only be read by setting it)
+_UMASK = os.umask(0o022)
+os.umask(_UMASK)
+
+
 def _atomic_write(path: str, write) -> None:
     """``write(fileobj)`` into a uniquely named temporary in ``path``'s directory, then rename it
     over ``path``: readers see the old file or the new one, and concurrent savers (other managers,
-    other processes) never share a temporary."""
+    other processes) never share a temporary.  The file keeps the mode of the one it replaces, or
+    gets 0666 & ~umask when new -- as a plain ``open(path, "w")`` would (mkstemp creates 0600)."""
     fd, tmp = tempfile.mkstemp(prefix=os.path.basename(path) + ".", suffix=".tmp", dir=os.path.dirname(path) or ".")
     try:
         with os.fdopen(fd, "wb") as f:
             write(f)
+        try:
+            mode = os.stat(path).st_mode & 0o7777
+        except FileNotFoundError:
+            mode = 0o666 & ~_UMASK
+        os.chmod(tmp, mode)
         os.replace(tmp, path)
     except BaseException:
         if os.path.exists(tmp):
@@ -484,26 +566,56 @@ class GalleryManager:
         root, _ext = os.path.splitext(path)
         return root + ".pkl"
 
+    @staticmethod
+    def _recorded_pickle(npz: str):
+        """The ``.pkl`` signature a ``save`` recorded in its ``.npz`` ({"size", "sha256"}, or None
+        when it wrote no ``.pkl`` and none existed), or "unknown" for ``.npz`` files of earlier
+        rounds, which recorded nothing."""
+        try:
+            with np.load(npz) as arrays:
+                if "meta" not in arrays.files:
+                    return "unknown"
+                meta = json.loads(str(arrays["meta"]))
+        except (OSError, ValueError):
+            return "unknown"
+        return meta.get("pkl", "unknown")
+
     @classmethod
     def _source(cls, path: str) -> Optional[Tuple[str, str]]:
         """What ``load(path)`` reads: ("npz", file) -- this module's save -- or ("pkl", file) -- the
         reference's ``pickle.dump(self.students)`` (gallery_manager.py:207-210), or None.  When both
-        exist (a reference gallery saved here since), the more recently written one."""
+        exist, the ``.npz`` unless the ``.pkl`` differs from the one the ``.npz`` was saved with
+        (its size + SHA-256, recorded by ``save``): then the reference app has written the
+        ``.pkl`` since, and it is the newer gallery.  File times are not consulted (a copy or a
+        checkout resets them), except for ``.npz`` files of earlier rounds that recorded no
+        signature.  The choice is logged at warning level whenever both files exist."""
         npz, pkl = cls._arrays_path(path), cls._pickle_path(path)
         have_npz, have_pkl = os.path.exists(npz), os.path.exists(pkl)
         if have_npz and have_pkl:
-            return ("pkl", pkl) if os.path.getmtime(pkl) > os.path.getmtime(npz) else ("npz", npz)
+            rec = cls._recorded_pickle(npz)
+            if rec == "unknown":
+                pick = "pkl" if os.path.getmtime(pkl) > os.path.getmtime(npz) else "npz"
+                why = "the .npz records no .pkl signature (an earlier save); the newer file wins"
+            elif rec is not None and _file_signature(pkl) == rec:
+                pick, why = "npz", "the .pkl is the one saved with it"
+            else:
+                pick, why = "pkl", "the .pkl changed after the .npz was saved (written by another program)"
+            _log.warning("gallery %s: both %s and %s exist; loading the .%s: %s", path, os.path.basename(npz),
+                         os.path.basename(pkl), pick, why)
+            return (pick, pkl if pick == "pkl" else npz)
         if have_npz:
             return "npz", npz
         if have_pkl:
             return "pkl", pkl
         return None
 
-    def save(self, path: Optional[str] = None) -> None:
-        """Write ``<stem>.npz`` (templates, samples and every record field: the whole gallery in
-        one file, replaced atomically) and the reference's informational ``<stem>.json`` sidecar in
-        the reference's own format (gallery_manager.py:211-229).  A reference ``.pkl`` at the path
-        is left untouched; ``load`` then prefers the newer ``.npz``."""
+    def save(self, path: Optional[str] = None, reference_pickle: bool = True) -> None:
+        """Write the gallery: ``<stem>.pkl`` in the reference's own format (gallery_manager.py:207-210;
+        ``reference_pickle=False`` leaves any ``.pkl`` at the path as it is), ``<stem>.npz``
+        (templates, samples, every record field and the ``.pkl``'s signature: the whole gallery in
+        one file) and the reference's informational ``<stem>.json`` sidecar (:211-229).  Each file
+        is replaced atomically; the ``.pkl`` goes first, so a save cut short leaves an ``.npz``
+        whose recorded signature no longer matches, and ``load`` takes the newer ``.pkl``."""
         path = path or self.gallery_path
         # _save_lock orders whole saves of this manager (the later snapshot lands last); unique
         # temporaries keep saves of other managers / processes from mixing; the snapshot itself is
@@ -519,8 +631,16 @@ class GalleryManager:
                 fields = {s: {"student_id": r.student_id, "name": r.name, "num_samples": r.num_samples,
                               "enrollment_date": r.enrollment_date, "last_updated": r.last_updated,
                               "metadata": copy.deepcopy(r.metadata)} for s, r in self.students.items()}
-            meta = {"format": "frhip-gallery-1", "order": ids, "students": fields}
+                snap = None
+                if reference_pickle:  # records sharing nothing mutable with the live ones
+                    snap = {s: StudentRecord(r.student_id, r.name, arrays[f"e{i}"], arrays[f"t{i}"], r.num_samples,
+                                             r.enrollment_date, r.last_updated, fields[s]["metadata"])
+                            for i, (s, r) in enumerate(self.students.items())}
             os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+            pkl = self._pickle_path(path)
+            if snap is not None:
+                _atomic_write(pkl, lambda f: dump_reference_pickle(snap, f))
+            meta = {"format": "frhip-gallery-1", "order": ids, "students": fields, "pkl": _file_signature(pkl)}
             arrays["meta"] = np.array(json.dumps(meta))
             _atomic_write(self._arrays_path(path), lambda f: np.savez(f, **arrays))
             sidecar = {"num_students": len(ids), "last_saved": now, "students": fields}
@@ -564,11 +684,20 @@ class GalleryManager:
             self._touch()
 
     def export_for_backup(self, backup_dir: str, backup_name: Optional[str] = None) -> str:
+        """gallery_manager.py:246-270: copy the gallery file(s) -- the reference-format ``.pkl`` and
+        this module's ``.npz``, whichever exist -- into ``backup_dir`` as ``<name>_backup_<time>.*``,
+        then write the JSON export of every record.  With no gallery file at ``gallery_path`` it
+        raises ``FileNotFoundError`` before writing anything, as the reference's ``shutil.copy2``
+        does.  Returns the JSON's path."""
         os.makedirs(backup_dir, exist_ok=True)
         stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
         stem = f"{backup_name}_backup_{stamp}" if backup_name else f"gallery_backup_{stamp}"
-        if os.path.exists(self._arrays_path(self.gallery_path)):
-            shutil.copy2(self._arrays_path(self.gallery_path), os.path.join(backup_dir, stem + ".npz"))
+        files = [f for f in (self._pickle_path(self.gallery_path), self._arrays_path(self.gallery_path))
+                 if os.path.exists(f)]
+        if not files:
+            raise FileNotFoundError(errno.ENOENT, os.strerror(errno.ENOENT), self.gallery_path)
+        for f in files:
+            shutil.copy2(f, os.path.join(backup_dir, stem + os.path.splitext(f)[1]))
         out = os.path.join(backup_dir, stem + ".json")
         with self._lock:  # snapshot: to_dict() copies every record into plain lists
             doc = {"backup_date": datetime.now().isoformat(), "backup_name": backup_name,

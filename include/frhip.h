@@ -148,8 +148,10 @@ int fr_warp_affine(fr_handle* h, const uint8_t* frame, int height, int width, co
  * BORDER_REFLECT_101.  The variance is summed in numpy's order (ndarray.var's chunked pairwise
  * sum; derived for and checked against numpy 2.2), so it is bitwise the reference's value there.
  * crops: device uint8 [n][height][width][channels], any height, width >= 1 (height * width
- * < 2^31); channels 1, 3 or 4; scores: host double [n].  Synchronises. */
-int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int height, int width, int channels, double* scores);
+ * < 2^31); channels 1, 3 or 4; scores: host double [n].  Runs on `stream` (NULL: the null stream)
+ * and synchronises that stream only. */
+int fr_blur_scores(fr_handle* h, const uint8_t* crops, int n, int height, int width, int channels, double* scores,
+                   void* stream);
 
 /* FaceDetector.detect (face_recognition.py:31-48: insightface SCRFD det_10g at det_size
  * 640x640, det_thresh, NMS IoU 0.4) for n frames of one size.  The handle is created with

@@ -52,4 +52,8 @@ def test_row_reduction_is_the_full_canvas_network(det, shape):
     for f in range(frames.shape[0]):
         n = int(c_full[f])
         assert n > 0
-        assert np.abs(d_full[f, :n] - d_red[f, :n]).max() <= 1e-3, (shape, f)
+        # the same boxes; two detections of near-equal score may trade places in the score order
+        a, b = d_full[f, :n], d_red[f, :n]
+        for row in b:
+            assert np.abs(a - row).max(axis=1).min() <= 1e-3, (shape, f, row)
+        assert np.abs(np.sort(a[:, 4]) - np.sort(b[:, 4])).max() <= 1e-5, (shape, f)

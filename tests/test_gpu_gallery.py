@@ -60,6 +60,22 @@ def test_search_on_reference_gallery_pickle(tmp_path, golden_dir):
     assert [ids.index(s) for s, _n, _sc in one] == f["search_idx"][9][:3].tolist()
 
 
+def test_search_on_dropin_written_gallery_equals_reference(tmp_path, golden_dir):
+    """A gallery saved by this module (tests/golden/dropin_students.pkl) and read by the REFERENCE
+    GalleryManager gives the reference's search results (tools/make_golden.py dropin); the GPU
+    search of the same file gives the same top-5 rows, scores within 1e-6."""
+    import shutil
+    from facerecognitionpipeline_amd.gallery_manager import GalleryManager
+    fx = np.load(os.path.join(golden_dir, "dropin_students.npz"))
+    shutil.copyfile(os.path.join(golden_dir, "dropin_students.pkl"), tmp_path / "students.pkl")
+    gm = GalleryManager(gallery_path=str(tmp_path / "students.pkl"), device="cuda:0", verbose=False)
+    ids = [str(s) for s in fx["ids"]]
+    q = np.concatenate([np.asarray(r.embeddings, np.float32) for r in gm.students.values()])
+    res = gm.search_batch(q, top_k=5)
+    assert np.array_equal(np.array([[ids.index(s) for s, _n, _sc in r] for r in res]), fx["search_idx"])
+    assert np.abs(np.array([[sc for _s, _n, sc in r] for r in res]) - fx["search_score"]).max() <= 1e-6
+
+
 @pytest.mark.parametrize("method", ["mean", "median", "weighted_mean"])
 def test_build_templates_random_vs_oracle(handle, method):
     """Ragged students (1..40 samples), clusters loose enough that the 0.70 filter drops

@@ -35,13 +35,13 @@ def pad32(c):
     return (c + 31) // 32 * 32
 
 
-def det_layers(B, W=640, H=640, src=(1080, 1920), skip=192):
+def det_layers(B, W=640, H=640, src=(1080, 1920), skip=192, skip2=64):
     """[(name, kind, alg_flop, exec_flop_wino4, exec_flop_direct, alg_bytes)] in launch order.
     kind: 'conv3' (3x3 stride 1: F(4x4) when eligible), 'convd' (direct: strided / 1x1 / 2x2),
     or the elementwise kernel's name.  alg_flop is the reference network's (full 640-row canvas);
     the executed FLOPs and bytes of the stem and stage 1 count the (H - skip)-row canvas they run
-    on (detector.cpp row_plan; 192 rows for a 1080p frame), and 'row_expand' (optional: absent
-    when nothing is skipped) restores stage 1's output to full height."""
+    on (detector.cpp row_plan; 192 rows for a 1080p frame; stage 2: skip2 = 64), and 'row_expand'
+    (optional: absent when nothing is skipped) restores stage 1's / stage 2's output height."""
     f4 = 4.0
     L = []
     red = [(H - skip) / H]
@@ -71,8 +71,13 @@ def det_layers(B, W=640, H=640, src=(1080, 1920), skip=192):
     cin = STEM
     for st, (n, c) in enumerate(zip(STAGE_BLOCKS, STAGE_PLANES)):
         if st == 1:
+            r2 = (H - skip2) / H
             L.append(("row_expand s1 out @160", "row_expand?", 0.0, 0.0, 0.0,
-                      f4 * B * hw * hw * 64 * (1 + red[0]) if skip else 0.0))
+                      f4 * B * hw * hw * 64 * (r2 + red[0]) if skip else 0.0))
+            red[0] = r2
+        if st == 2:
+            L.append(("row_expand s2 out @80", "row_expand?", 0.0, 0.0, 0.0,
+                      f4 * B * hw * hw * 96 * (1 + red[0]) if skip2 else 0.0))
             red[0] = 1.0
         for u in range(n):
             ci = cin if u == 0 else c
@@ -166,8 +171,11 @@ def main():
                     help="canvas rows the stem and stage 1 skipped (default: 192 if row_expand_kernel ran, else 0)")
     a = ap.parse_args()
     rows = read_csv(glob.glob(os.path.join(a.trace_dir, "*kernel_trace.csv"))[0])
-    skip = a.skip if a.skip is not None else (192 if any("row_expand" in r["Kernel_Name"] for r in rows) else 0)
-    L = det_layers(a.frames, skip=skip)
+    nexp = sum("row_expand" in r["Kernel_Name"] for r in rows) / max(1, sum("letterbox" in r["Kernel_Name"]
+                                                                            for r in rows))
+    skip = a.skip if a.skip is not None else (192 if nexp >= 1 else 0)
+    skip2 = 64 if nexp >= 2 else 0
+    L = det_layers(a.frames, skip=skip, skip2=skip2)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     segs = segments(rows, L)
     if not segs:
@@ -202,7 +210,7 @@ def main():
                 for cn, v in acc.items():
                     pmc[cn][li].append(v)
     print(f"detects aligned: {len(segs)} (B = {a.frames} frames of 1080p, 640x640 letterbox; stem + stage 1 on "
-          f"{640 - skip} canvas rows)")
+          f"{640 - skip} canvas rows, stage 2 on {640 - skip2})")
     print(f"detect wall (first dispatch start -> nms end), median: "
           f"{sorted(detect_ns)[len(detect_ns) // 2] / 1e6:.3f} ms")
     hdr = (f"{'layer':36s} {'kernel':22s} {'avg us':>8s} {'%time':>6s} {'algGF':>7s} {'algTF':>6s} {'exeTF':>6s}"
@@ -273,7 +281,7 @@ def main():
               f"{d['exec_tflops']:6.1f} {100 * d['exec_tflops'] / PEAK:5.1f} {d['alg_GBps']:7.0f} "
               + (f"{d['hbm_bytes'] / d['alg_bytes']:7.2f} " if "hbm_bytes" in d and d["alg_bytes"] else f"{'-':>7s} ")
               + (f"{100 * d['mfma_busy_frac']:7.1f}%" if "mfma_busy_frac" in d else f"{'-':>8s}"))
-    res = {"frames": a.frames, "detects": len(segs), "skip_rows": skip,
+    res = {"frames": a.frames, "detects": len(segs), "skip_rows": skip, "skip_rows_stage2": skip2,
            "detect_wall_ms": sorted(detect_ns)[len(detect_ns) // 2] / 1e6,
            "kernel_ms": total / 1e6, "alg_flop": sum(x[2] for x in L), "layers": out_layers, "families": fams}
     if a.build:

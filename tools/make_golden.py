@@ -45,6 +45,11 @@ the reference's own ``face_embedder.FaceEmbedder`` and
   (face_recognition.py:174-182) on the gate frame written as PNG (``imread`` in the cv2
   shim decodes through PIL: lossless, so the pixels are the frame's), with the gate's
   fixed detections, default quality settings, ``return_all`` true and false.
+* ``dropin_students.pkl`` + ``dropin_students.npz`` — a gallery written by THIS repo's
+  ``GalleryManager.save`` (``ref_students.pkl`` loaded, one student enrolled, one updated,
+  one deleted through the drop-in), then loaded by the REFERENCE ``GalleryManager`` (the real
+  ``pickle.load`` of gallery_manager.py:241-242): the records it sees (ids, names, sample
+  counts, dates, array checksums) and its ``search(top_k=5)`` of every stored sample.
 * ``ref_students.pkl`` / ``ref_students.json`` — the reference's own gallery
   FILES (gallery_manager.py:207-232): a reference ``GalleryManager`` built
   with ``add_student`` (samples + metadata) from
@@ -61,7 +66,7 @@ fixture).  Weights are the seeded synthetic checkpoint of
 format.  Crops are regenerated from their seeds at test time; their SHA-256 is
 stored to pin them.
 
-Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups] [refpkl] [gate] [image]``
+Usage: ``python tools/make_golden.py [embed] [c3] [resize] [backups] [refpkl] [gate] [image] [dropin]``
 (no argument: all).
 """
 from __future__ import annotations
@@ -173,7 +178,7 @@ def quiet():
 def main() -> None:
     if not os.path.isdir(REF):
         raise SystemExit("reference not present; golden files are generated in the build container only")
-    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups", "refpkl", "gate", "image"}
+    parts = set(sys.argv[1:]) or {"embed", "c3", "resize", "backups", "refpkl", "gate", "image", "dropin"}
     os.makedirs(OUT, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="frgolden_")
     with open(os.path.join(tmp, "cv2.py"), "w") as f:
@@ -405,6 +410,40 @@ def main() -> None:
         np.savez_compressed(os.path.join(OUT, "image.npz"), decoded_sha256=np.array(json.dumps(want)),
                             process_image=np.array(json.dumps(runs)), missing_error=np.array(missing))
         print("image", {k: len(v) for k, v in runs.items()}, missing)
+
+    if "dropin" in parts:
+        import shutil
+        from facerecognitionpipeline_amd.gallery_manager import GalleryManager as DropIn
+        d = os.path.join(tmp, "dropin")
+        os.makedirs(d)
+        shutil.copyfile(os.path.join(OUT, "ref_students.pkl"), os.path.join(d, "students.pkl"))
+        ours = DropIn(gallery_path=os.path.join(d, "students.pkl"), verbose=False)
+        sids = list(ours.students)
+        r = np.random.Generator(np.random.PCG64(0xFACE0D1D))
+
+        def unit(n):
+            x = r.standard_normal((n, 512)).astype(np.float32)
+            return x / np.linalg.norm(x, axis=1, keepdims=True)
+
+        ours.add_student("NEW0001", "Enrolled Through The Drop-In", unit(3), metadata={"source": "frhip"})
+        ours.update_embeddings(sids[1], unit(2), mode="append")
+        ours.delete_student(sids[2])
+        ours.save()
+        shutil.copyfile(os.path.join(d, "students.pkl"), os.path.join(OUT, "dropin_students.pkl"))
+        with quiet():
+            ref = ref_gm.GalleryManager(gallery_path=os.path.join(d, "students.pkl"))  # the reference's load
+        ids = list(ref.students)
+        recs = [{"student_id": x.student_id, "name": x.name, "num_samples": int(x.num_samples),
+                 "enrollment_date": x.enrollment_date, "last_updated": x.last_updated, "metadata": x.metadata,
+                 "class": type(x).__module__ + "." + type(x).__name__,
+                 "embeddings_sha256": sha(np.asarray(x.embeddings)), "embeddings_dtype": str(x.embeddings.dtype),
+                 "template_sha256": sha(np.asarray(x.template_embedding))} for x in ref.students.values()]
+        queries = np.concatenate([np.asarray(x.embeddings, np.float32) for x in ref.students.values()])
+        gal, idx, sc = search_arrays(ref, queries)
+        np.savez_compressed(os.path.join(OUT, "dropin_students.npz"), ids=np.array(ids),
+                            records=np.array(json.dumps(recs)), queries_sha256=np.array(sha(queries)),
+                            search_idx=idx, search_score=sc, gallery_sha256=np.array(sha(gal.astype(np.float32))))
+        print("dropin", len(ids), "students read back by the reference; queries", queries.shape)
 
 
 if __name__ == "__main__":
