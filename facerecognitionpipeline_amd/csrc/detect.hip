@@ -168,6 +168,23 @@ __global__ __launch_bounds__(256) void upsample_add_kernel(float4* __restrict__ 
   big[i] = v;
 }
 
+// AvgPool2d(2, 2) in NHWC (SCRFD's downsample shortcut, before its 1x1 conv): ((a + b) + c) + d
+// over the window in row-major order, times 1/4 (exact), one thread per (output pixel, 4 channels).
+__global__ __launch_bounds__(256) void avgpool2_kernel(const float4* __restrict__ x, int B, int H, int W, int C4,
+                                                       float4* __restrict__ y) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * Ho * Wo * C4) return;
+  const int c = i % C4;
+  const int pix = i / C4;
+  const int ox = pix % Wo, t = pix / Wo;
+  const int oy = t % Ho, b = t / Ho;
+  const int r0 = (b * H + 2 * oy) * W + 2 * ox;
+  const float4 p = x[r0 * C4 + c], q = x[(r0 + 1) * C4 + c], u = x[(r0 + W) * C4 + c], v = x[(r0 + W + 1) * C4 + c];
+  y[i] = make_float4((((p.x + q.x) + u.x) + v.x) * 0.25f, (((p.y + q.y) + u.y) + v.y) * 0.25f,
+                     (((p.z + q.z) + u.z) + v.z) * 0.25f, (((p.w + q.w) + u.w) + v.w) * 0.25f);
+}
+
 // Row expansion of a reduced-height map (detector.cpp, row_plan): dst row r of each image is src
 // row r above m, src row m for the Hd - Hs rows from m on (copies of a row inside the invariant
 // run), src row r - (Hd - Hs) below them.  NHWC, one thread per (pixel, 4 channels).
@@ -422,6 +439,14 @@ hipError_t launch_maxpool3(const float* x, int B, int H, int W, int C, float* y,
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool3_kernel, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(x), B, H, W, C / 4, reinterpret_cast<float4*>(y));
+  return hipGetLastError();
+}
+
+hipError_t launch_avgpool2(const float* x, int B, int H, int W, int C, float* y, hipStream_t s) {
+  if (C % 4 || H % 2 || W % 2 || (long long)B * H * W * C >= (1ll << 31)) return hipErrorInvalidValue;
+  const int n = B * (H / 2) * (W / 2) * (C / 4);
+  hipLaunchKernelGGL(avgpool2_kernel, dim3((n + 255) / 256), dim3(256), 0, s, reinterpret_cast<const float4*>(x), B, H,
+                     W, C / 4, reinterpret_cast<float4*>(y));
   return hipGetLastError();
 }
 

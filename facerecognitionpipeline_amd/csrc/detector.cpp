@@ -31,6 +31,7 @@ constexpr int STEM = 56, NECK = 56, HEADC = 80;
 constexpr int STRIDES[3] = {8, 16, 32};
 
 int pad32(int c) { return (c + 31) / 32 * 32; }
+int pad16(int c) { return (c + 15) / 16 * 16; }
 
 struct DetBlock {
   ConvW conv1, conv2, down;
@@ -57,6 +58,7 @@ struct Detector {
   float *c_out[3] = {nullptr, nullptr, nullptr}, *lat[3] = {nullptr, nullptr, nullptr};
   float *inter[3] = {nullptr, nullptr, nullptr}, *outs[3] = {nullptr, nullptr, nullptr};
   float *tA = nullptr, *tB = nullptr, *hd[3] = {nullptr, nullptr, nullptr};
+  float* pool = nullptr;  // AvgPool2d(2, 2) of a stage's input (the downsample shortcut's 1x1 conv input)
   float* cand = nullptr;
   int* count = nullptr;
   float* dets = nullptr;
@@ -172,9 +174,11 @@ std::vector<float> padv(const std::vector<float>& v, int n) {
   return r;
 }
 
-void set_geom(ConvW& c, int cin, int cout, int k, int stride, int pad) {
-  c.cin = pad32(cin);
-  c.cout = pad32(cout);
+// Channels are padded to 32 (the direct kernel's K-step); the head towers, whose convs all run on
+// F(4x4) (16-channel K-steps), to 16: 80 channels, not 96 (head_pad16)
+void set_geom(ConvW& c, int cin, int cout, int k, int stride, int pad, bool p16 = false) {
+  c.cin = p16 ? pad16(cin) : pad32(cin);
+  c.cout = p16 ? pad16(cout) : pad32(cout);
   c.kh = c.kw = k;
   c.stride = stride;
   c.pad = pad;
@@ -190,8 +194,8 @@ int detector_finalize(fr_handle* h) {
   std::vector<float> sc, sh;
   // conv + BN(+ReLU): weights packed, BN folded into post scale/shift, ReLU = zero slopes
   auto conv_bn = [&](ConvW& c, const std::string& wk, const std::string& bnk, int cin, int cout, int k, int stride,
-                     int pad, bool relu, int taps_rep = 1, float mul = 1.f) {
-    set_geom(c, cin, cout, k * taps_rep, stride, pad);
+                     int pad, bool relu, int taps_rep = 1, float mul = 1.f, bool p16 = false) {
+    set_geom(c, cin, cout, k * taps_rep, stride, pad, p16);
     pk.put(&c.w, pack_w(P(wk), cout, cin, k, c.cout, c.cin, taps_rep, mul));
     bn_fold(&P(bnk + ".weight"), &P(bnk + ".bias"), P(bnk + ".running_mean"), P(bnk + ".running_var"), sc, sh);
     pk.put(&c.post_scale, padv(sc, c.cout));
@@ -236,9 +240,8 @@ int detector_finalize(fr_handle* h) {
       conv_bn(b.conv2, p + "conv2.weight", p + "bn2", co, co, 3, 1, 1, true);
       if (u == 0 && (s > 0 || ci != co)) {
         b.has_down = true;
-        // AvgPool2d(2, 2) then conv1x1 == conv 2x2 stride 2 with w/4 on each tap
-        conv_bn(b.down, p + "downsample.1.weight", p + "downsample.2", ci, co, 1, stride, 0, false,
-                stride, 1.f / (float)(stride * stride));
+        // AvgPool2d(2, 2) (launch_avgpool2) then this conv1x1 + BN; stage 1 (stride 1): conv1x1 alone
+        conv_bn(b.down, p + "downsample.1.weight", p + "downsample.2", ci, co, 1, 1, 0, false);
       }
     }
     cin = STAGE_PLANES[s];
@@ -257,12 +260,13 @@ int detector_finalize(fr_handle* h) {
     }
     for (int j = 0; j < 3; ++j) {
       const std::string t = "bbox_head.towers." + l + "." + std::to_string(j);
-      conv_bn(d->tower[i][j], t + ".conv.weight", t + ".bn", j == 0 ? NECK : HEADC, HEADC, 3, 1, 1, true);
+      conv_bn(d->tower[i][j], t + ".conv.weight", t + ".bn", j == 0 ? NECK : HEADC, HEADC, 3, 1, 1, true, 1, 1.f,
+              true);
     }
     // cls | reg | kps as one conv 80 -> 30 (channel order = the ONNX outputs' per-anchor layout)
     {
       ConvW& c = d->head[i];
-      set_geom(c, HEADC, 30, 3, 1, 1);
+      set_geom(c, HEADC, 30, 3, 1, 1, true);
       std::vector<float> w((size_t)30 * HEADC * 9), b(30);
       const auto& wc = P("bbox_head.cls." + l + ".weight");
       const auto& wr = P("bbox_head.reg." + l + ".weight");
@@ -329,6 +333,7 @@ int detector_finalize(fr_handle* h) {
     take((void**)&d->outs[i], B * hw[i] * nk * f4);
     take((void**)&d->hd[i], B * hw[i] * 32 * f4);
   }
+  take((void**)&d->pool, B * hw[0] * pad32(STEM) * f4);  // the largest: stage 2's input pooled to 80x80
   take((void**)&d->tA, B * hw[0] * hc * f4);
   take((void**)&d->tB, B * hw[0] * hc * f4);
   d->dets_cap = 1024;
@@ -533,7 +538,13 @@ int forward_chunk(fr_handle* h, const uint8_t* fr, int B, int height, int width,
       if (rc) return rc;
       const float* res = x;
       if (b.has_down) {
-        rc = dconv(h, b.down, x, d->dbuf, B, Hh, Ww, EPI_AFFINE, nullptr, s);
+        const float* xd = x;
+        if (b.conv1.stride == 2) {
+          e = launch_avgpool2(x, B, Hh, Ww, b.down.cin, d->pool, s);
+          if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("avgpool: ") + hipGetErrorString(e));
+          xd = d->pool;
+        }
+        rc = dconv(h, b.down, xd, d->dbuf, B, Ho, Wo, EPI_AFFINE, nullptr, s);
         if (rc) return rc;
         res = d->dbuf;
       }

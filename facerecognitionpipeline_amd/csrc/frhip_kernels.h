@@ -290,6 +290,8 @@ hipError_t launch_det_stem(const uint8_t* img, int n, int H, int W, int C, const
                            const float* shift, float* y, hipStream_t s);
 hipError_t launch_maxpool3(const float* x, int B, int H, int W, int C, float* y, hipStream_t s);
 hipError_t launch_upsample_add(float* big, const float* small, int B, int h, int w, int C, hipStream_t s);
+// AvgPool2d(2, 2), NHWC, even H and W, C % 4 == 0.
+hipError_t launch_avgpool2(const float* x, int B, int H, int W, int C, float* y, hipStream_t s);
 // [B][Hs][W][C] -> [B][Hd][W][C]: rows [m, m + Hd - Hs) are copies of src row m (C % 4 == 0).
 hipError_t launch_row_expand(const float* x, int B, int Hs, int W, int C, int m, int Hd, float* y, hipStream_t s);
 hipError_t launch_decode(const DetDecodeParams& p, int n, hipStream_t s);

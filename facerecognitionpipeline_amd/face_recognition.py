@@ -166,7 +166,7 @@ def load_image_rgb(path: str) -> Optional[np.ndarray]:
         from PIL import Image
         with Image.open(path) as im:
             im.load()
-            return np.ascontiguousarray(np.asarray(im.convert("RGB"), dtype=np.uint8))
+            return np.array(im.convert("RGB"), dtype=np.uint8)  # a writable copy
     except (OSError, ValueError, SyntaxError):
         return None
 

@@ -84,7 +84,10 @@ def det_layers(B, W=640, H=640, src=(1080, 1920), skip=192, skip2=64):
             s = 2 if (u == 0 and st > 0) else 1
             ho = conv(f"s{st + 1}.{u}.conv1 {ci}->{c} @{hw}{'/s2' if s == 2 else ''}", ci, c, hw, 3, s)
             if u == 0 and (st > 0 or ci != c):
-                conv(f"s{st + 1}.{u}.down 2x2s2 {ci}->{c} @{hw}", ci, c, hw, 2, 2)
+                if s == 2:  # AvgPool2d(2, 2) then the 1x1 conv
+                    L.append((f"s{st + 1}.{u}.avgpool2 @{hw}", "avgpool2", 0.0, 0.0, 0.0,
+                              red[0] * f4 * B * (hw * hw + ho * ho) * pad32(ci)))
+                conv(f"s{st + 1}.{u}.down 1x1 {ci}->{c} @{ho}", ci, c, ho, 1, 1)
             conv(f"s{st + 1}.{u}.conv2 {c}->{c} @{ho} +res", c, c, ho, 3, 1, res=True)
             hw = ho
         cin = c
