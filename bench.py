@@ -80,9 +80,6 @@ def parse():
                     help="stride-1 3x3 convs: Winograd F(4x4,3x3), F(2x2,3x3) or the direct implicit GEMM (all f32)")
     ap.add_argument("--lanes-min", type=int, default=None,
                     help="a forward of n >= 2x this many crops runs as two concurrent halves (0: one lane; default: library's)")
-    ap.add_argument("--wino4s", choices=["on", "off"], default=None,
-                    help="F(4x4) launches of whole items on the symmetric-wave kernel (on) or on wino4_kernel "
-                         "(off); default: the library's choice (A/B and profiles)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--exchange-reps", type=int, default=3,
@@ -480,12 +477,6 @@ def main():
             dist.init_process_group("gloo")
 
     from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
-    if args.wino4s is not None:
-        from facerecognitionpipeline_amd import _lib as frlib0
-        L0 = frlib0.load()
-        L0.frt_set_wino4s.argtypes = [ctypes.c_int]
-        if L0.frt_set_wino4s(int(args.wino4s == "on")) != 0:
-            sys.exit("frt_set_wino4s failed")
     sd = W.synthetic_state_dict(args.arch, model_type=args.model_type)
     emb = FaceEmbedder(architecture=args.arch, model_type=args.model_type, state_dict=sd, device=dev, max_batch=args.batch,
                        precision=args.precision, conv_algorithm=args.conv_algorithm, lanes_min=args.lanes_min)
@@ -679,15 +670,11 @@ def main():
         build = frlib.load().fr_version().decode()
         same_workload = (args.config == "c3" and args.model_type == "adaface" and args.arch == "ir_101"
                          and args.batch == 256 and G == 1000 and args.precision == "fp32"
-                         and args.conv_algorithm == "winograd4" and args.wino4s != "on")
+                         and args.conv_algorithm == "winograd4")
         traffic, alg_bytes, mfma_busy, traffic_src, traffic_note = profile_figures(
             args.traffic_json, dom, build, same_workload)
         if args.conv_algorithm != "winograd4":
             wino_name = "wino_kernel (Winograd F(2x2,3x3) f32, every stride-1 3x3 conv)"
-        elif args.wino4s == "on":
-            wino_name = ("wino4s_kernel + wino4_kernel (Winograd F(4x4,3x3) f32, 16x16x4 MFMA, fused transforms; "
-                         "every stride-1 3x3 conv: whole-item grids on the symmetric-wave wino4s_kernel, split-K "
-                         "grids on wino4_kernel)")
         else:
             wino_name = ("wino4_kernel (Winograd F(4x4,3x3) f32: fused input transform, 16x16x4 MFMA, lane-local "
                          "output transform; every stride-1 3x3 conv)")
@@ -762,7 +749,6 @@ def main():
                        "gallery_exchange": (("rccl broadcast" if args.dist_backend == "nccl" else "gloo broadcast")
                                             if world > 1 else "none"),
                        **({"ranks_share_gpu": True} if args.same_gpu and world > 1 else {}),
-                       **({"wino4s": args.wino4s} if args.wino4s is not None else {}),
                        # concurrent half-batch forwards per GPU (fr_set_lanes; library default 64 crops
                        # per lane, at most 2 lanes); the roofline pass always runs one lane
                        "lanes": (1 if args.lanes_min == 0 else

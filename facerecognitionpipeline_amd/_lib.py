@@ -15,7 +15,8 @@ from typing import Optional
 
 import torch  # noqa: F401  (must precede the CDLL load, see module doc)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfrhip.so")
+# FRHIP_LIB: another build of the library (tools' A/B of two builds in one tree); default: in-tree
+LIB_PATH = os.environ.get("FRHIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfrhip.so")
 
 FR_OK = 0
 FR_ERR_INVALID_ARGUMENT = -1

@@ -22,14 +22,14 @@ LIB = os.path.join(PKG, "libfrhip.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = "gfx950"
-SOURCES = ["conv_winograd4.hip", "conv_winograd4s.hip", "conv_winograd.hip", "conv_s2.hip", "conv_small.hip","conv_f32_w4.hip", "conv_f32_w8.hip", "conv_bf16x3.hip", "conv_det.hip", "conv_mfma.hip",
+SOURCES = ["conv_winograd4.hip", "conv_winograd.hip", "conv_s2.hip", "conv_small.hip","conv_f32_w4.hip", "conv_f32_w8.hip", "conv_bf16x3.hip", "conv_det.hip", "conv_mfma.hip",
            "embed_misc.hip", "align.hip", "gallery.hip", "detect.hip", "frhip_runtime.cpp", "detector.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
 # F(4x4): the input / output transforms are packed f32 where the source says so (explicit f2
 # vectors: measured 2-5% faster than their scalar form); the SLP vectorizer is kept
 # from packing the rest (offset arithmetic, the MFMA waves' U-ring bookkeeping) behind our back
-EXTRA = {"conv_winograd4.hip": ["-fno-slp-vectorize"], "conv_winograd4s.hip": ["-fno-slp-vectorize"],
+EXTRA = {"conv_winograd4.hip": ["-fno-slp-vectorize"],
          # the stem's MFMA accumulators in VGPRs: no v_accvgpr_read per output before its epilogue
          "embed_misc.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 LDFLAGS = ["-shared", f"--offload-arch={ARCH}", f"-Wl,-rpath,{ROCM}/lib", "-Wl,--no-undefined"]

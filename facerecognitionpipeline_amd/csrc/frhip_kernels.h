@@ -132,21 +132,13 @@ struct Wino4Params {
   int B, H, W, Cin, Cout;
   int Pr, Pc, NC, TWc, ntiles, mblocks, nblocks;  // set by launch_wino4 (wino4_canvas)
   int nbg;  // tile blocks per XCD group of items (set by launch_wino4)
-  // split-K / stream-K workspace (optional): compact raw partial outputs, one 16-tile x 16-pixel
+  // split-K workspace (optional): compact raw partial outputs, one 16-tile x 16-pixel
   // x 64-cout slot (64 KiB) per item part; launch_wino4 splits the K loop of a small grid's items
   // when part_floats holds the slots
   float* part;
   long long part_floats;
   int ksplit, ks_per;      // set by launch_wino4
   int item0, nitem;        // set by launch_wino4: the launch's range of the layer's item order
-  // 0: whole items only; 1: whole-item rounds + a stream-K tail (the last, part-empty round's
-  // item-steps cut into equal ranges, cut items finished in-kernel) when the grid has more items
-  // than CUs and the last round is part-empty; 2: stream-K over all item-steps whenever the grid
-  // has more items than CUs (experiments); uses part for the cut items' raw partials
-  int sk_mode;
-  int sk_dp;  // set by launch_wino4: whole-item rounds before a stream-K tail (MODE 2)
-  int* cnt;   // MODE 2 tail tickets [tail items][4 MFMA waves], zeroed once, re-armed in-kernel
-  int cnt_cap;
   int no_split;  // 1: never split-K (tests compare the two schedules)
   int max_split;  // > 0: at most this many K parts per item in a split-K launch (serving sweeps)
   // ring hand-off guard: a wave that has polled its LDS counters poll_max times without seeing
@@ -162,30 +154,9 @@ struct Wino4Params {
   int nbg_override;  // > 0: tile blocks per XCD item group instead of the rule (A/B only)
 };
 constexpr int W4_BLK_X = 1, W4_BLK_RES = 2, W4_BLK_Y = 4;
-// The symmetric-wave F(4x4) kernel (conv_winograd4s.hip) for launches of whole items: same U
-// (launch_wino4_weights), same results up to rounding.  Reads x, u, y, pre_t, post_*, prelu, res, B,
-// H, W, Cin, Cout, blk and sk_mode of p.  Takes pre-BN + BN + PReLU, BN + residual and BN + PReLU
-// launches with Cout % 64 == 0 whose grid has at least `cus` items (sk_mode 2 stays on wino4).
-bool wino4s_takes(const Wino4Params& p, bool pre, Epi epi, int cus);
-hipError_t launch_wino4s(const Wino4Params& p, bool pre, Epi epi, hipStream_t s);
 constexpr int WINO4_POLL_DEFAULT = 1 << 16;
 constexpr int FR_DEVERR_W4_HANDOFF = 1;
 bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad);  // Cin % 16, Cout % 16
-
-// One layer of a chained launch (wino4_chain_kernel, conv_winograd4.hip): a split-K (MODE 1)
-// layer planned by wino4_chain_plan.  kind 0: IR conv1 (pre-BN, BN, PReLU), 1: IR conv2 (BN +
-// identity residual).  nwg: its workgroups (items x splits); cbase: its item counters in sync.
-struct W4Link {
-  Wino4Params p;
-  int kind, nwg, cbase, pad_;
-};
-// Plans `p` (pre: conv1 kind) as one layer of a chain: true when it is a split-K launch of at most
-// one round of workgroups on `cus` CUs (the serving sizes); fills the canvas / split fields.
-bool wino4_chain_plan(Wino4Params& p, bool pre, Epi epi, int cus);
-// One launch of nl planned layers (links: device copy), grid = max nwg <= CUs; sync: ncnt
-// zeroed ints (1 + nl + the layers' items), left zeroed by the launch.
-hipError_t launch_wino4_chain(const W4Link* links, int nl, int grid, int* sync, int ncnt, int* err, int poll_max,
-                              hipStream_t s);
 
 // Serving-batch 3x3 convs (conv_small.hip): pad 1, stride 1 or 2, optional fused shortcut
 // (Cin2 / x2, weight rows 9*Cin + Cin2), one workgroup per 16 pixels x 16 couts with the whole K

@@ -282,19 +282,10 @@ struct ProfScope {
   }
 };
 
-// F(4x4) stream-K schedule for large layers (frt_set_wino4_streamk: A/B and tests).  Off by
-// default: measured neutral on the IR-101 layers where its policy applies (stage 2, B=256:
-// 241-246 vs 239-243 us whole items), DESIGN.md §4.
-static int g_wino4_streamk = 0;
 // A/B (frt_set_conv2sc_tile): the tile of the fused stride-2 conv2 + conv-shortcut launches, -1 = the rule
 static int g_conv2sc_tile = -1;
 // A/B (frt_set_wino4_nbg): tile blocks per XCD item group of the F(4x4) launches, 0 = the rule
 static int g_wino4_nbg = 0;
-// F(4x4) launches of whole items (at least one item per CU) on the symmetric-wave kernel
-// (conv_winograd4s.hip) instead of wino4_kernel (frt_set_wino4s: A/B and tests).  Off by default:
-// 5-8% faster per launch in isolation (two lanes, cold caches), 11% slower in the C3 forward
-// 
-static int g_wino4s = 0;
 // cap on the F(4x4) split-K parts of small grids (frt_set_wino4_max_split: serving sweeps); 0 = none
 static int g_wino4_max_split = 0;
 // the stage-1 stride-2 conv2 on its band kernel (frt_set_s2_band: tests compare it with the
@@ -303,65 +294,6 @@ static int g_s2band = 1;
 // poll bound of wino4_kernel's ring hand-off waits (frt_set_wino4_poll_limit: tests force expiry)
 static int g_wino4_poll = WINO4_POLL_DEFAULT;
 
-// Launches the collected chain: its layers' link table (uploaded once per (n, run): a table
-// found with the same contents is reused, so a graph capture of the forward never uploads) and
-// one wino4_chain_kernel launch; a single layer, a table that does not fit the counters, or a
-// capture without an uploaded table launch the layers one by one instead.
-int chain_flush(fr_handle* h, hipStream_t s) {
-  if (h->chain_pending.empty()) return FR_OK;
-  std::vector<W4Link> links;
-  std::vector<Wino4Params> raw;
-  std::vector<bool> pre;
-  links.swap(h->chain_pending);
-  raw.swap(h->chain_raw);
-  pre.swap(h->chain_pre);
-  const int seq = h->chain_seq++;
-  const int nl = (int)links.size();
-  int ncnt = 1 + nl, grid = 0;
-  for (auto& lk : links) {
-    lk.cbase = ncnt;
-    ncnt += lk.p.nitem;
-    grid = std::max(grid, lk.nwg);
-  }
-  W4Link* dev = nullptr;
-  if (nl >= 2 && ncnt <= fr_handle::CHAIN_SYNC_INTS && grid <= h->cus && h->chain_sync) {
-    for (auto& t : h->chain_tabs)
-      if (t.n == h->chain_n && t.seq == seq && t.host.size() == links.size() &&
-          std::memcmp(t.host.data(), links.data(), links.size() * sizeof(W4Link)) == 0)
-        dev = t.dev;
-    if (!dev && !h->capturing) {
-      fr_handle::ChainTab* t = nullptr;
-      for (auto& e : h->chain_tabs)
-        if (e.n == h->chain_n && e.seq == seq) t = &e;
-      if (t && t->host.size() != links.size()) {
-        FR_HIP(h, hipStreamSynchronize(s));  // no launch of this stream still reads the old table
-        FR_HIP(h, hipFree(t->dev));
-        t->dev = nullptr;
-      }
-      if (!t) {
-        h->chain_tabs.push_back({h->chain_n, seq, {}, nullptr});
-        t = &h->chain_tabs.back();
-      }
-      if (!t->dev) FR_HIP(h, hipMalloc((void**)&t->dev, links.size() * sizeof(W4Link)));
-      // stream-ordered: launches queued before this one that read the previous contents finish first
-      FR_HIP(h, hipStreamSynchronize(s));
-      FR_HIP(h, hipMemcpy(t->dev, links.data(), links.size() * sizeof(W4Link), hipMemcpyHostToDevice));
-      t->host = links;
-      dev = t->dev;
-    }
-  }
-  if (dev) {
-    const hipError_t e = launch_wino4_chain(dev, nl, grid, h->chain_sync, ncnt, h->dev_err,
-                                            g_wino4_poll > 0 ? g_wino4_poll : -1, s);
-    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 chain launch: ") + hipGetErrorString(e));
-    return FR_OK;
-  }
-  for (int l = 0; l < nl; ++l) {
-    const hipError_t e = launch_wino4(raw[l], pre[l], links[l].kind == 0 ? EPI_AFFINE_PRELU : EPI_AFFINE_RES, s);
-    if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
-  }
-  return FR_OK;
-}
 
 // serving conv kernel: layers of at most this many output pixels (n * Ho * Wo).  Batch 1 also
 // takes stage 1's 56x56 layers: 1.0626 vs 1.0740 ms per embed + match, medians of 8 runs each
@@ -415,12 +347,6 @@ static bool w4_takes(const fr_handle* h, const ConvW& cw, Epi epi, int res_H, in
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
              const LaneWs* L, const float* x2) {
-  // a layer that does not join the chain being collected: the chain goes out first
-  // (the Winograd branch below decides for itself; everything else flushes here)
-  const bool w4_candidate = h->winograd && h->wino_m == 4 && h->prec == PREC_F32 && cw.wino4 &&
-                            wino4_supported(cw.cin, cw.cout, cw.kh, cw.kw, cw.stride, cw.pad);
-  if (!w4_candidate)
-    if (int rc = chain_flush(h, s)) return rc;
   float* const sk_ws = L ? L->sk_ws : h->sk_ws;
   int* const sk_cnt = L ? L->sk_cnt : h->sk_cnt;
   float* const w4part = L ? L->w4part : h->w4part;
@@ -473,7 +399,6 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     if (h->w4_blk)  // forward_lanes plans F(4x4) layouts only when no lane reaches this branch
       return fail(h, FR_ERR_HIP, "internal: F(4x4) channel-blocked activations in the serving conv kernel");
     p.w = cw.w_frag;
-    if (int rc = chain_flush(h, s)) return rc;
     p.blk = h->convs_blk;
     if (h->convs_y2 && epi != EPI_AFFINE_PRELU) {
       p.y2 = h->convs_y2;
@@ -508,34 +433,13 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.W = W;
     wp.Cin = cw.cin;
     wp.Cout = cw.cout;
-    // the workspace's tail holds the stream-K tail tickets (zeroed at allocation, re-armed in-kernel)
     wp.part = w4part;
-    wp.part_floats = w4part ? fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS : 0;
-    wp.cnt = w4part ? reinterpret_cast<int*>(w4part + (fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS)) : nullptr;
-    wp.cnt_cap = w4part ? (int)fr_handle::W4CNT_INTS : 0;
-    wp.sk_mode = g_wino4_streamk;
+    wp.part_floats = w4part ? fr_handle::W4PART_FLOATS : 0;
     wp.max_split = g_wino4_max_split;
     wp.err = h->dev_err;
     wp.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     wp.blk = h->w4_blk;  // forward_lanes' plan of channel-blocked activations
     wp.nbg_override = g_wino4_nbg;
-    // a serving forward's conv1 / conv2: collected into the current chain when it plans as a
-    // one-round split-K launch (the chain launches at the next layer that cannot join it)
-    if (h->chain_collect && (epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE_RES)) {
-      Wino4Params plan = wp;
-      if (wino4_chain_plan(plan, cw.pre_scale != nullptr, epi, h->cus)) {
-        W4Link lk;
-        std::memset(&lk, 0, sizeof lk);
-        std::memcpy(&lk.p, &plan, sizeof plan);
-        lk.kind = cw.pre_scale != nullptr ? 0 : 1;
-        lk.nwg = plan.nitem * plan.ksplit;
-        h->chain_pending.push_back(lk);
-        h->chain_raw.push_back(wp);
-        h->chain_pre.push_back(cw.pre_scale != nullptr);
-        return FR_OK;
-      }
-    }
-    if (int rc = chain_flush(h, s)) return rc;
     Wino4Params cv = wp;
     cv.blk = 0;
     wino4_canvas(cv);
@@ -543,12 +447,10 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     const double exec = 2.0 * 36.0 * cv.ntiles * (double)cw.cin * cw.cout;
     ProfScope ps(h, s, flop, FR_PROF_CONV_WINOGRAD, exec);
     const bool pre = cw.pre_scale != nullptr;
-    hipError_t e = g_wino4s && wino4s_takes(wp, pre, epi, h->cus) ? launch_wino4s(wp, pre, epi, s)
-                                                                   : launch_wino4(wp, pre, epi, s);
+    hipError_t e = launch_wino4(wp, pre, epi, s);
     if (e != hipSuccess) return fail(h, FR_ERR_HIP, std::string("winograd4 launch: ") + hipGetErrorString(e));
     return FR_OK;
   }
-  if (int rc = chain_flush(h, s)) return rc;
   if (h->w4_blk)  // forward_lanes only sets it for layers the F(4x4) branch above takes
     return fail(h, FR_ERR_HIP, "internal: channel-blocked activations outside the F(4x4) kernel");
   // Winograd F(2x2,3x3) for the stride-1 3x3 convs (f32 parity path only)
@@ -700,7 +602,6 @@ int ensure_lane(fr_handle* h, int l, int batch) {
   }
   if (!L.w4part) {
     FR_HIP(h, hipMalloc((void**)&L.w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
-    FR_HIP(h, hipMemset(L.w4part + (fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS), 0, fr_handle::W4CNT_INTS * sizeof(int)));
   }
   if (ensure_stream_k(h->device, &h->cus, &L.sk_ws, &L.sk_ws_floats, &L.sk_cnt, &L.sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
@@ -716,21 +617,6 @@ int ensure_lane(fr_handle* h, int l, int batch) {
 // other lane's launch of the same layer is already queued.
 int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* cnt, int nl, float* out,
                   int normalize, const hipStream_t* st, const LaneWs* L) {
-  // serving forwards (one lane, n <= chain_max_n): chained F(4x4) layers (chain_flush).  Not
-  // under profiling (per-launch events) and never for a second lane: a chained launch assumes its
-  // workgroups have the CUs to themselves.
-  struct ChainScope {
-    fr_handle* h;
-    ~ChainScope() {
-      h->chain_collect = false;
-      h->chain_pending.clear();
-      h->chain_raw.clear();
-      h->chain_pre.clear();
-    }
-  } chain_scope{h};
-  h->chain_collect = nl == 1 && cnt[0] <= h->chain_max_n && !h->prof && h->chain_sync != nullptr && !h->detector;
-  h->chain_seq = 0;
-  h->chain_n = cnt[0];
   for (int l = 0; l < nl; ++l) {
     const int n = cnt[l];
     ProfScope ps(h, st[l], 2.0 * n * 112.0 * 112.0 * 64 * 27, 0);
@@ -783,7 +669,7 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
   // could take the serving branch, which does not read the F(4x4) layout bits)
   int cnt_min = cnt[0];
   for (int l = 1; l < nl; ++l) cnt_min = std::min(cnt_min, cnt[l]);
-  if (h->w4_blocked && cnt_min > h->convs_max_n && !h->chain_collect && !h->detector) {
+  if (h->w4_blocked && cnt_min > h->convs_max_n && !h->detector) {
     std::vector<char> c1(nb, 0), c2(nb, 0);
     int hw = 112;
     for (size_t bi = 0; bi < nb; ++bi) {
@@ -874,8 +760,6 @@ int forward_lanes(fr_handle* h, const uint8_t* rgb, const int* off, const int* c
     cur = nxt;
     HW = Ho;
   }
-  if (int rc = chain_flush(h, st[0])) return rc;
-  h->chain_collect = false;
   for (int l = 0; l < nl; ++l) {
     const int n = cnt[l];
     const long long split_stride = (long long)n * 512;
@@ -1740,9 +1624,6 @@ int fr_finalize(fr_handle* h) {
     FR_HIP(h, hipMalloc((void**)&h->rs_stage, mb * 112 * 112 * 3));
     FR_HIP(h, hipMalloc((void**)&h->emb_stage, mb * 512 * sizeof(float)));
     FR_HIP(h, hipMalloc((void**)&h->w4part, fr_handle::W4PART_FLOATS * sizeof(float)));
-    FR_HIP(h, hipMemset(h->w4part + (fr_handle::W4PART_FLOATS - fr_handle::W4CNT_INTS), 0, fr_handle::W4CNT_INTS * sizeof(int)));
-    FR_HIP(h, hipMalloc((void**)&h->chain_sync, fr_handle::CHAIN_SYNC_INTS * sizeof(int)));
-    FR_HIP(h, hipMemset(h->chain_sync, 0, fr_handle::CHAIN_SYNC_INTS * sizeof(int)));
   }
   if (ensure_stream_k(h->device, &h->cus, &h->sk_ws, &h->sk_ws_floats, &h->sk_cnt, &h->sk_cnt_cap) != FR_OK)
     return fail(h, FR_ERR_HIP, "stream-K workspace allocation failed");
@@ -2314,11 +2195,6 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 }
 
 static int g_frt_wino4_split = 1;
-int frt_set_wino4s(int on) {
-  if (on != 0 && on != 1) return FR_ERR_INVALID_ARGUMENT;
-  g_wino4s = on;
-  return FR_OK;
-}
 int frt_set_wino4_nbg(int nbg) {
   if (nbg < 0) return FR_ERR_INVALID_ARGUMENT;
   g_wino4_nbg = nbg;
@@ -2327,10 +2203,6 @@ int frt_set_wino4_nbg(int nbg) {
 int frt_set_conv2sc_tile(int tile) {
   if (tile < -1 || tile >= TILE_COUNT) return FR_ERR_INVALID_ARGUMENT;
   g_conv2sc_tile = tile;
-  return FR_OK;
-}
-int frt_set_wino4_streamk(int on) {
-  g_wino4_streamk = on < 0 ? 0 : (on > 2 ? 2 : on);
   return FR_OK;
 }
 int frt_set_wino4_max_split(int s) {
@@ -2454,14 +2326,6 @@ int frt_set_small_conv_blocked(fr_handle* h, int on) {
   clear_graphs(h);
   return FR_OK;
 }
-int frt_set_wino4_chain(fr_handle* h, int max_n) {
-  if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
-  std::lock_guard<std::mutex> lk(h->mu);
-  DeviceGuard dg(h->device);
-  h->chain_max_n = std::max(0, max_n);
-  clear_graphs(h);
-  return FR_OK;
-}
 int frt_set_fuse_shortcut(fr_handle* h, int on) {
   if (!h) return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "NULL handle");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -2514,28 +2378,15 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.W = W;
     p.Cin = cin;
     p.Cout = cout;
-    p.sk_mode = g_wino4_streamk;
     p.no_split = !g_frt_wino4_split;
     p.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     p.err = frt_err;
-    if (g_frt_wino4_split || g_wino4_streamk) {  // split-K / stream-K partial slots (64 KiB each) + tail tickets
+    if (g_frt_wino4_split) {  // split-K partial slots (64 KiB each)
       p.part_floats = 257ll * 2 * 16 * 16 * 64;
-      p.cnt_cap = 1 << 16;
-      if (hipMalloc((void**)&part, p.part_floats * sizeof(float) + p.cnt_cap * sizeof(int)) != hipSuccess)
-        e = hipErrorOutOfMemory;
-      else {
-        p.cnt = reinterpret_cast<int*>(part + p.part_floats);
-        e = hipMemset(p.cnt, 0, p.cnt_cap * sizeof(int));
-      }
+      if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;
       p.part = part;
     }
-    if (e == hipSuccess) {
-      int cus = 256, dev = 0;
-      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      const bool pre = pre_scale != nullptr;
-      e = g_wino4s && wino4s_takes(p, pre, (Epi)epi, cus) ? launch_wino4s(p, pre, (Epi)epi, s)
-                                                          : launch_wino4(p, pre, (Epi)epi, s);
-    }
+    if (e == hipSuccess) e = launch_wino4(p, pre_scale != nullptr, (Epi)epi, s);
   }
   const hipError_t se = hipStreamSynchronize(s);
   (void)hipFree(u);

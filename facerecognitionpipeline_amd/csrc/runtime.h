@@ -160,7 +160,6 @@ struct fr_handle {
   float* convs_arena = nullptr;  // the serving conv kernel's filters (ConvW::w_frag), built at fr_finalize
   float* w4part = nullptr;         // F(4x4) split-K partial outputs (small batches), W4PART_FLOATS
   static constexpr long long W4PART_FLOATS = 16ll << 20;
-  static constexpr long long W4CNT_INTS = 1 << 16;  // its last 256 KB: F(4x4) stream-K tail tickets
 
   // lanes (fr_set_lanes): a forward of n crops runs as min(lane_max, n / lane_min) concurrent
   // parts, lane 0 on the caller's stream with the workspace above, lane l >= 1 on lane_stream[l]
@@ -187,15 +186,6 @@ struct fr_handle {
   hipStream_t cap_stream = nullptr;
   std::vector<GraphEntry> graphs;
 
-  // chained F(4x4) split-K layers (wino4_chain_kernel): in a one-lane forward of n <= chain_max_n
-  // crops, each run of consecutive conv1 / conv2 layers that plan as split-K launches of one round
-  // goes out as ONE launch (run_conv collects them into chain_pending, chain_flush launches).  The
-  // link tables are uploaded once per (n, run) and reused (also by graph replays).  Off by default
-  // (frt_set_wino4_chain): measured slower than per-layer launches (batch 1: 1.86 vs 1.58 ms per
-  // embed; its in-launch seams -- waiting for the previous layer's slowest workgroup, for the
-  // item's slowest split, then the reduction -- cost more than the two kernel boundaries they
-  // replace).
-  int chain_max_n = 0;
   // forwards of n <= convs_max_n crops run every body 3x3 conv on conv_small.hip's kernel (one
   // launch per layer, whole K per 16x16 tile) instead of F(4x4) split-K + fixup / the split-K
   // direct convs (frt_set_small_conv)
@@ -217,20 +207,6 @@ struct fr_handle {
   // the Wino4Params::blk of the next launch); frt_set_wino4_blocked: A/B
   int w4_blk = 0;
   bool w4_blocked = true;
-  bool chain_collect = false;
-  int chain_seq = 0;  // index of the next run in the current forward
-  std::vector<frhip::W4Link> chain_pending;
-  std::vector<frhip::Wino4Params> chain_raw;  // the same layers as run_conv built them (unplanned)
-  std::vector<bool> chain_pre;
-  struct ChainTab {
-    int n, seq;
-    std::vector<frhip::W4Link> host;
-    frhip::W4Link* dev;
-  };
-  std::vector<ChainTab> chain_tabs;
-  int chain_n = 0;  // crops of the current forward (the tables' key)
-  int* chain_sync = nullptr;  // zeroed counters, left zeroed by every chained launch
-  static constexpr int CHAIN_SYNC_INTS = 1 << 15;
 
   // device-side error word (host-pinned, coherent): kernels that detect a broken invariant
   // store an FR_DEVERR_* code here (wino4_kernel: a ring hand-off that timed out); the runtime
@@ -292,8 +268,6 @@ struct fr_handle {
     (void)hipFree(align_m);
     (void)hipFree(blur_out);
     (void)hipFree(blur_ws);
-    for (auto& t : chain_tabs) (void)hipFree(t.dev);
-    (void)hipFree(chain_sync);
     if (dev_err) (void)hipHostFree(dev_err);
   }
 };
@@ -347,8 +321,6 @@ int ensure_buf(fr_handle* h, void** p, size_t* cap, size_t bytes);
 int ensure_stream_k(int device, int* cus, float** ws, long long* ws_floats, int** cnt, int* cnt_cap);
 // L: the lane whose stream-K / split-K workspace the launch uses (nullptr: the handle's own)
 // x2: the fused shortcut's input (cw.cin2 > 0)
-// Launches the layers run_conv collected for a chain (one launch for >= 2), in order, on s.
-int chain_flush(fr_handle* h, hipStream_t s);
 int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int H, int W, frhip::Epi epi,
              const float* res, int res_H, int res_W, int nsplit, long long split_stride, hipStream_t s,
              const LaneWs* L = nullptr, const float* x2 = nullptr);

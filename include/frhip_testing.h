@@ -39,23 +39,12 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
  * cin % 16 == 0, cout % 16 == 0.  frt_conv2d_winograd4 gives launch_wino4 a split-K workspace
  * (small grids then split the K loop over items + a reduce pass) unless frt_set_wino4_split(0). */
 int frt_set_wino4_split(int on);
-/* F(4x4) schedule of large layers (grids with more items than CUs), for handles too:
- * 0 = whole items round-robin over the persistent grid; 1 = whole-item rounds, then the last
- * part-empty round's item-steps in equal ranges per workgroup (cut items finished in the launch
- * by their last-arriving wave); 2 = every item-step in equal ranges (experiments).
- * Applies to launches issued after the call (captured graphs keep theirs). */
-int frt_set_wino4_streamk(int on);
 /* A/B (process-wide): the ConvTile of the fused stride-2 conv2 + conv-shortcut launches of
  * non-serving batches (-1: the built-in rule).  Forwards already captured in graphs keep theirs. */
 int frt_set_conv2sc_tile(int tile);
 /* A/B (process-wide): tile blocks per XCD item group of the F(4x4) launches (0: the built-in rule,
  * 32 items per group; 8 x 8 at 512 channels).  Forwards already captured in graphs keep theirs. */
 int frt_set_wino4_nbg(int nbg);
-/* F(4x4) launches of whole items (grids of at least one 16-tile x 64-cout item per CU: the batch-256
- * forward, frt_conv2d_winograd4 at such sizes) on the symmetric-wave kernel (conv_winograd4s.hip,
- * on = 1) or on wino4_kernel (0, default), process-wide; graphs captured before the call keep
- * theirs. */
-int frt_set_wino4s(int on);
 /* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
  * before the call keep their schedule). */
 int frt_set_wino4_max_split(int s);
@@ -102,13 +91,6 @@ int frt_conv2d_small(const float* x, const float* x2, const float* w, float* y, 
                      int cin2, int cout, int stride, const float* pre_scale, const float* pre_shift,
                      const float* post_scale, const float* post_shift, const float* prelu, const float* res, int epi,
                      void* stream);
-/* Handle h chains the F(4x4) layers of forwards of n <= max_n crops (default 0 = never):
- * every run of consecutive conv1 / conv2 layers that plan as one-round split-K launches goes out
- * as one wino4_chain_kernel launch (per layer: the split's partial, an in-launch reduction by the
- * item's workgroups, a counter the next layer waits on) instead of a conv launch + a fixup launch
- * per layer.  Outputs are bitwise those of the unchained forward; measured slower than the
- * per-layer launches at batch 1, hence off.  Drops captured graphs. */
-int frt_set_wino4_chain(fr_handle* h, int max_n);
 /* Handle h runs the stride-2 conv2 of a block with a conv shortcut and that shortcut as one
  * GEMM (on = 1, default: BN scales folded into the weights, extra K-steps over the block input)
  * or as two launches (0).  Drops captured graphs. */

@@ -20,14 +20,10 @@ def lib():
         L.frt_conv2d_winograd4.argtypes = [_P, _P, _P] + [_I] * 5 + [_P] * 6 + [_I, _P]
         L.frt_set_wino4_split.restype = _I
         L.frt_set_wino4_split.argtypes = [_I]
-        L.frt_set_wino4_streamk.restype = _I
-        L.frt_set_wino4_streamk.argtypes = [_I]
         L.frt_set_conv2sc_tile.restype = _I
         L.frt_set_conv2sc_tile.argtypes = [_I]
         L.frt_set_wino4_nbg.restype = _I
         L.frt_set_wino4_nbg.argtypes = [_I]
-        L.frt_set_wino4s.restype = _I
-        L.frt_set_wino4s.argtypes = [_I]
         L.frt_set_wino4_max_split.restype = _I
         L.frt_set_wino4_max_split.argtypes = [_I]
         L.frt_set_wino4_poll_limit.restype = _I
@@ -38,8 +34,6 @@ def lib():
         L.frt_conv2d_s2band.argtypes = [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P]
         L.frt_set_fuse_shortcut.restype = _I
         L.frt_set_fuse_shortcut.argtypes = [_P, _I]
-        L.frt_set_wino4_chain.restype = _I
-        L.frt_set_wino4_chain.argtypes = [_P, _I]
         L.frt_set_small_conv.restype = _I
         L.frt_set_small_conv.argtypes = [_P, _I]
         L.frt_set_small_conv_pre_epilogue.restype = _I

@@ -46,32 +46,26 @@ def test_blocked_forward_is_bitwise_nhwc(arch, model_type):
                 e = emb.embed_tensor(crops[:8].contiguous()).clone()
                 nhwc = e if nhwc is None else nhwc
                 assert torch.equal(e, nhwc)
-            # the stream-K tail of part-empty last rounds (experiments' schedule) addresses the
-            # residual and the outputs itself
-            assert L.frt_set_wino4_streamk(1) == 0
-            got, ref = _both(emb, crops[:96].contiguous(), L)
-            assert torch.equal(got, ref), (got - ref).abs().max().item()
     finally:
-        assert L.frt_set_wino4_streamk(0) == 0
         assert L.frt_set_wino4_blocked(emb.model.h, 1) == 0
 
 
-def test_blocked_forward_is_bitwise_nhwc_symmetric_waves():
-    """The same with the whole-item F(4x4) launches on the symmetric-wave kernel (frt_set_wino4s):
-    its layout bits move addresses only too."""
+def test_blocked_plan_with_uneven_lanes():
+    """lanes of 3 and 2 crops (lanes_min 2, n = 5).  The 2-crop lane is within the
+    serving kernel's batch limit, so no F(4x4) layout bit may be planned for the forward (the
+    serving branch does not read them): embeddings bitwise the all-NHWC forward's, and equal to
+    one-lane forwards of each lane's crops."""
     from facerecognitionpipeline_amd.face_embedder import FaceEmbedder
     from tests import _frt
     L = _frt.lib()
     sd = W.synthetic_state_dict("ir_101")
-    emb = FaceEmbedder(architecture="ir_101", state_dict=sd, device="cuda:0", max_batch=256)
-    crops = torch.from_numpy(W.synthetic_crops(256, seed=W.CROP_SEED_GALLERY)).cuda()
+    emb = FaceEmbedder(architecture="ir_101", state_dict=sd, device="cuda:0", max_batch=8, lanes_min=2)
+    crops = torch.from_numpy(W.synthetic_crops(5, seed=W.CROP_SEED_GALLERY)).cuda()
     try:
-        assert L.frt_set_wino4s(1) == 0
         got, ref = _both(emb, crops, L)
         assert torch.equal(got, ref), (got - ref).abs().max().item()
-        assert L.frt_set_wino4s(0) == 0
-        w4 = emb.embed_tensor(crops).clone()
-        assert (got - w4).abs().max().item() <= 1e-5  # the two F(4x4) kernels round differently
     finally:
-        L.frt_set_wino4s(0)  # the library default
         assert L.frt_set_wino4_blocked(emb.model.h, 1) == 0
+    one = FaceEmbedder(architecture="ir_101", state_dict=sd, device="cuda:0", max_batch=8, lanes_min=0)
+    parts = torch.cat([one.embed_tensor(crops[:3].contiguous()), one.embed_tensor(crops[3:].contiguous())])
+    assert torch.equal(got, parts), (got - parts).abs().max().item()

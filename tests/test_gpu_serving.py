@@ -117,37 +117,6 @@ def test_match_batcher_equals_match_single_face(embedder, tmp_path):
         embedder.model.set_graph_batch(0)
 
 
-def test_chained_layers_bit_identical_to_per_layer_launches(embedder):
-    """With frt_set_wino4_chain(h, 8), serving forwards (n <= 8) run each stage's F(4x4) layers
-    as ONE chained launch (wino4_chain_kernel: split partials, in-launch reduction by the item's
-    workgroups, a counter per layer; off by default, slower than per-layer launches).  Its reduction is the fixup kernel's code, so embeddings must be bitwise those of
-    the per-layer launches, eagerly and under graph replay, run after run (the counters re-arm)."""
-    from tests import _frt
-
-    L = _frt.lib()
-    h = embedder.model
-    crops = torch.from_numpy(W.synthetic_crops(12, seed=W.CROP_SEED_GALLERY)).cuda()
-    ns = (1, 2, 3, 5, 8, 12)  # 12 > the chain's default max: per-layer launches either way
-    try:
-        assert L.frt_set_small_conv(h.h, 0) == 0  # batch 1 otherwise takes conv_small.hip's kernel
-        assert L.frt_set_wino4_chain(h.h, 0) == 0
-        per_layer = {n: embedder.embed_tensor(crops[:n]).clone() for n in ns}
-        assert L.frt_set_wino4_chain(h.h, 8) == 0
-        for rep in range(3):
-            for n in ns:
-                got = embedder.embed_tensor(crops[:n])
-                assert torch.equal(got, per_layer[n]), (n, rep, (got - per_layer[n]).abs().max().item())
-        h.set_graph_batch(8)
-        for rep in range(3):  # rep 0 eager + capture, then replays of the chained graphs
-            for n in (1, 3, 8):
-                assert torch.equal(embedder.embed_tensor(crops[:n]), per_layer[n]), (n, rep)
-        assert h.graph_count() == 3
-    finally:
-        h.set_graph_batch(0)
-        assert L.frt_set_wino4_chain(h.h, 0) == 0
-        assert L.frt_set_small_conv(h.h, 2) == 0  # the default
-
-
 def test_serving_conv_path_vs_winograd_path(embedder):
     """Batch 1 runs every body 3x3 conv on conv_small.hip's kernel (frt_set_small_conv, default
     n <= 2); with it off the same forward takes the F(4x4) split-K + fixup and split-K direct

@@ -72,14 +72,8 @@ def test_winograd_non_square_map(m):
     (96, 14, 256, 256),  # 344 workgroups > CUs: a full round plus a partial one
     (32, 112, 64, 64),   # 1568 workgroups, Cin = 64 (4 K-steps)
 ])
-@pytest.mark.parametrize("w4s", [1, 0])
-def test_winograd4_multi_round(B, H, cin, cout, w4s):
-    L = _frt.lib()
-    try:
-        assert L.frt_set_wino4s(w4s) == 0
-        got, ref = _wino_case(B, H, cin, cout, 2, seed=500 + H, m=4)
-    finally:
-        L.frt_set_wino4s(0)  # the library default
+def test_winograd4_multi_round(B, H, cin, cout):
+    got, ref = _wino_case(B, H, cin, cout, 2, seed=500 + H, m=4)
     _close(got, ref, rel=REL[4])
 
 
@@ -93,24 +87,13 @@ def test_winograd4_multi_round(B, H, cin, cout, w4s):
     (1023, 8, 14, 32, 64),    # pre-BN: 4 | H but not W, a partial last canvas row (separator row added)
 ])
 @pytest.mark.parametrize("epi", [1, 2])
-def test_winograd4_symmetric_waves(B, H, W, cin, cout, epi):
-    """Launches of whole items (at least one per CU) run on the symmetric-wave kernel
-    (conv_winograd4s.hip): matches the CPU conv, the shipping wino4_kernel to the same bar, and is
-    deterministic run to run."""
-    L = _frt.lib()
-    outs = {}
-    try:
-        for on in (1, 0):
-            assert L.frt_set_wino4s(on) == 0
-            got, ref = _wino_case(B, H, cin, cout, epi, seed=1500 + H + cin + epi, W=W, m=4)
-            _close(got, ref, rel=REL[4])
-            outs[on] = got
-        assert L.frt_set_wino4s(1) == 0
-        again, _ = _wino_case(B, H, cin, cout, epi, seed=1500 + H + cin + epi, W=W, m=4)
-        assert torch.equal(again, outs[1]), "symmetric-wave F(4x4) is not run-to-run deterministic"
-    finally:
-        L.frt_set_wino4s(0)  # the library default
-    _close(outs[1], outs[0], rel=REL[4])
+def test_winograd4_whole_item_grids(B, H, W, cin, cout, epi):
+    """Launches of whole items (at least one per CU, several rounds, a part-empty last round)
+    match the CPU conv and are deterministic run to run."""
+    got, ref = _wino_case(B, H, cin, cout, epi, seed=1500 + H + cin + epi, W=W, m=4)
+    _close(got, ref, rel=REL[4])
+    again, _ = _wino_case(B, H, cin, cout, epi, seed=1500 + H + cin + epi, W=W, m=4)
+    assert torch.equal(again, got), "F(4x4) is not run-to-run deterministic"
 
 
 @pytest.mark.parametrize("B,H,cin,cout", [
@@ -149,40 +132,6 @@ def test_winograd4_pre_bn_partial_canvas_row(B, H, W):
     out of every stored output's window."""
     got, ref = _wino_case(B, H, 32, 48, 1, seed=910 + B + H + W, W=W, m=4)
     _close(got, ref, rel=REL[4])
-
-
-@pytest.mark.parametrize("B,H,cin,cout", [
-    (256, 28, 128, 128),  # IR-101 stage 2: 1568 items = 6 rounds + a 32-item tail (1 K-step per workgroup)
-    (256, 14, 256, 256),  # IR-101 stage 3: 900 items = 3 rounds + 132 (8.25 K-steps per workgroup)
-    (64, 56, 64, 64),     # stage 1 at B=64: 784 items + 16 * 4 tail steps: most workgroups' tail is empty
-    (96, 28, 128, 128),   # 588 items = 2.3 rounds
-    (160, 14, 128, 128),  # canvas of 14x14 images, 600 items
-])
-@pytest.mark.parametrize("epi", [1, 2])
-def test_winograd4_stream_k(B, H, cin, cout, epi):
-    """Large grids whose items leave the last round part-empty: whole-item rounds, then the tail
-    items' K-steps in equal ranges per workgroup (mode 1), or every item-step that way (mode 2);
-    the last-arriving wave of a cut item sums its raw partials in workgroup order and finishes it
-    in the launch.  Matches the CPU conv, the whole-item schedule to the same bar, and is
-    deterministic run to run."""
-    L = _frt.lib()
-    outs = {}
-    try:
-        assert L.frt_set_wino4s(0) == 0  # wino4_kernel's schedules (the symmetric kernel takes whole items only)
-        for mode in (1, 2, 0):
-            L.frt_set_wino4_streamk(mode)
-            got, ref = _wino_case(B, H, cin, cout, epi, seed=1300 + H + cin + epi, m=4)
-            _close(got, ref, rel=REL[4])
-            outs[mode] = got
-        for mode in (1, 2):
-            L.frt_set_wino4_streamk(mode)
-            again, _ = _wino_case(B, H, cin, cout, epi, seed=1300 + H + cin + epi, m=4)
-            assert torch.equal(again, outs[mode]), f"stream-K mode {mode} is not run-to-run deterministic"
-    finally:
-        L.frt_set_wino4_streamk(0)
-        L.frt_set_wino4s(0)  # the library default
-    _close(outs[1], outs[0], rel=REL[4])
-    _close(outs[2], outs[0], rel=REL[4])
 
 
 def test_winograd4_small_cin():

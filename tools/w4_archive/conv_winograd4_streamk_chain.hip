@@ -89,11 +89,14 @@ constexpr int BIGOFF = 0x7F000000;   // row/column offset of padding: any sum wi
 // output-geometry tables of the items in flight: the transform waves' load stream runs at most
 // NBUF + 2 K-steps (so items) ahead of the MFMA waves' consumption
 constexpr int NGEO = 8;
+// MODE 2: segments of a workgroup's stream (whole-item rounds + at most 3 tail segments), kept in
+// an LDS table (item, first step) so the schedule's scalars do not stay live across the K loop
+constexpr int MAXSEG = 64;
 static_assert(NGEO > NBUF + 2, "geometry table overwritten while an epilogue may still read it");
 // output geometry per tile: 4 rows (image-row base, y * W) and 4 columns (image base, x), so the
 // epilogue can address the output and the residual in either layout (NHWC or channel-blocked)
 constexpr int GEOW = 16;
-static_assert((NBUF * VSTEP + NGEO * FT * GEOW + 8) * 4 <= 160 * 1024, "LDS budget");
+static_assert((NBUF * VSTEP + NGEO * FT * GEOW + 8 + 2 * MAXSEG) * 4 <= 160 * 1024, "LDS budget");
 static_assert(NXI % uring_depth<EPI_AFFINE_RES>() == 0 && NXI % uring_depth<EPI_AFFINE>() == 0,
               "U ring phase must repeat every K-step");
 
@@ -275,19 +278,23 @@ __device__ __forceinline__ Item item_of(const Wino4Params& p, int gi) {
 // A launch covers the items [item0, item0 + nitem) of the layer's item order.
 // MODE: 0 = whole items round-robin over the persistent grid; 1 = split-K (every item's K loop
 // cut into ksplit parts, raw partial outputs into compact slots [item][part][16 tiles]
-// [16 pixels][64 couts], summed in part order by wino4_part_fixup_kernel: small grids).
-// (Round 4's stream-K tail and round 4's chained serving layers, both measured slower or neutral,
-// are kept outside the library: tools/w4_archive/conv_winograd4_streamk_chain.hip.)
-// The kernel body of wino4_kernel (bid, nblk = blockIdx.x, gridDim.x); ring: the workgroup's LDS
-// (W4_LDS_FLOATS).
-constexpr int W4_LDS_FLOATS = NBUF * VSTEP + NGEO * FT * GEOW + 8;
+// [16 pixels][64 couts], summed in part order by wino4_part_fixup_kernel: small grids);
+// 2 = stream-K: p.sk_dp rounds of whole items round-robin (data-parallel), then the remaining
+// (tail) items' K-steps cut into equal contiguous ranges, one per workgroup.  An item cut by the
+// ranges leaves one raw partial per workgroup that worked on it; the last-arriving wave (a ticket
+// per item and MFMA wave) sums them in workgroup order and finishes the item in this launch.
+// The kernel body, for wino4_kernel (bid, nblk = blockIdx.x, gridDim.x) and for the layers of
+// wino4_chain_kernel (CH: the input patches are loaded device-coherent, sc1, since earlier layers
+// of the same launch wrote them from other CUs).  ring: the workgroup's LDS (W4_LDS_FLOATS).
+constexpr int W4_LDS_FLOATS = NBUF * VSTEP + NGEO * FT * GEOW + 8 + 2 * MAXSEG;
 // RMIX: the residual's layout differs from the output's, in an instance of its own (its offsets are
 // computed on their own: more live registers in the epilogue): 1 = residual NHWC, output
 // channel-blocked; 2 = residual channel-blocked, output NHWC.  0: p.blk's y and res layouts are the
 // same, and the residual is addressed with the output's offsets.
-template <bool PRE, int EPI, int MODE, int RMIX = 0>
+template <bool PRE, int EPI, int MODE, bool CH, int RMIX = 0>
 __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, const int bid, const int nblk) {
-  constexpr bool SPLIT = MODE == 1;
+  constexpr bool SPLIT = MODE == 1, SK = MODE == 2;
+  constexpr int XPOL = CH ? CPOL_SC1 : 0;
   __builtin_assume(bid >= 0 && bid < nblk && nblk <= 65535);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -295,10 +302,28 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   const int KST = Cin / KC;                       // K-steps of the whole reduction
   const int KS = SPLIT ? p.ks_per : KST;          // stream steps per item
   const int nitems = p.nitem * p.ksplit;
-  // this workgroup's items are bid, bid + nblk, ... of the XCD-remapped order (item_at(j), j local)
+  // MODE 0/1: this workgroup's items are bid, bid + nblk, ... of the
+  // XCD-remapped order (item_at(j), j local).  SK: segments j < sk_dp are the whole items
+  // bid + j * nblk of the XCD-remapped order of the first D = sk_dp * nblk
+  // items; then it owns the tail item-steps [u_lo, u_hi) of the (nT - D) * KST space (its logical
+  // index XCD-remapped, so an XCD's workgroups hold one contiguous run of tail items): segment
+  // sk_dp + i is tail item tt_first + i, the first one from step s_tail0.
   const int nloc = (nitems - bid + nblk - 1) / nblk;
-  const int t_last = nloc - 1;  // last item
+  const int nT = p.mblocks * p.nblocks;
+  const int D = SK ? p.sk_dp * nblk : 0;
+  const long long TT = SK ? (long long)(nT - D) * KST : 0;  // tail item-steps
+  const int bl = SK ? xcd_remap(bid, nblk) : 0;
+  const int u_lo = SK ? (int)((long long)bl * TT / nblk) : 0;
+  const int u_hi = SK ? (int)((long long)(bl + 1) * TT / nblk) : 0;
+  const int tt_first = u_lo / KST, s_tail0 = u_lo - tt_first * KST;
+  const int nseg = SK ? p.sk_dp + (u_hi > u_lo ? (u_hi - 1) / KST - tt_first + 1 : 0) : nloc;
+  const int t_last = nseg - 1;  // last segment
+  int* const segtab = reinterpret_cast<int*>(ring + NBUF * VSTEP + NGEO * FT * GEOW + 8);  // SK: [MAXSEG][item, step0]
+  auto seg_begin = [&](int j) {
+    return SK && j <= t_last ? __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j + 1]) : 0;
+  };
   auto item_at = [&](int j) {
+    if (SK) return item_of(p, __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j]));
     const int t = xcd_remap(bid + j * nblk, nitems);
     const int sp = t / p.nitem, li = t - sp * p.nitem;
     Item it = item_of(p, p.item0 + li);
@@ -309,12 +334,17 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   // K-steps item `it` really has (split-K: the last split may be short; its stream is padded
   // with steps whose patches load as zeros, so every item is KS stream steps long)
   auto steps_of = [&](const Item& it) { return SPLIT ? min(KS, KST - it.split * KS) : KST; };
-  const int G = nloc * KS;  // K-steps in this workgroup's stream
+  const int G = SK ? p.sk_dp * KST + (u_hi - u_lo) : nloc * KS;  // K-steps in this workgroup's stream
 
   int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [NGEO items][16 tiles][GEOW]
   int* const rdy = geo + NGEO * FT * GEOW;                        // [4] K-steps written, per transform wave
   int* const fre = rdy + 4;                                       // [4] K-steps read, per MFMA wave
   if (tid < 8) rdy[tid] = 0;
+  if (SK && tid < nseg) {
+    const int q = tid;
+    segtab[2 * q] = q < p.sk_dp ? xcd_remap(bid + q * nblk, D) : D + tt_first + (q - p.sk_dp);
+    segtab[2 * q + 1] = q == p.sk_dp ? s_tail0 : 0;
+  }
   __syncthreads();  // the kernel's only workgroup barrier
   if (G <= 0) return;
   if (wid >= 4) {
@@ -353,7 +383,8 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     // every image row when such a canvas row exists), so it may take the shift like an
     // in-image pixel.
     float rowm[6], colm[3];
-    int lj = 0, ls = 0, ks_real = KS, step0 = 0;
+    int lj = 0, ls = seg_begin(0), ks_real = KS, step0 = 0;
+    bool fresh = true;  // SK: the next load starts segment lj
     auto enter_item = [&](int j) {
       const Item it = item_at(min(j, t_last));
       ks_real = steps_of(it);
@@ -422,7 +453,8 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     Patch pa, pb, pc;
     // issue the patch loads of the next step of the stream (steps are loaded in order)
     auto load = [&](Patch& P) {
-      if (ls == 0) enter_item(lj);
+      if (SK ? fresh : ls == 0) enter_item(lj);
+      fresh = false;
       // split-K padding step: every load is out of range (num_records 0) and reads zeros, and
       // the BN shift is dropped
       // (readfirstlane: the stream counters are wave-uniform, but the compiler loses track of
@@ -435,7 +467,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       for (int a = 0; a < 6; ++a)
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, 0);
+          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, poff[a][b], soff, XPOL);
           P.d[a][b] = f2{__uint_as_float(v.x), __uint_as_float(v.y)};
         }
       if constexpr (PRE) {
@@ -447,7 +479,8 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       }
       if (++ls == KS) {
         ++lj;
-        ls = 0;
+        ls = seg_begin(lj);
+        fresh = true;
       }
     };
     // the ring address of (tile i, channels ch, ch+1): A-fragment slot lane 16 k + i
@@ -558,13 +591,14 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   auto ulast = [&](int j) {  // last real K-step of item j (split-K: the short last split)
     return SPLIT ? steps_of(item_at(min(j, t_last))) - 1 : KST - 1;
   };
-  // the stream: item j (local), steps [0, KS)
-  int j = 0;
+  // segments of the stream: MODE 0/1 item j (local) steps [0, KS); SK item j (global) steps
+  // [s0, s1) -- only the first and the last segment of a workgroup's range can be partial
+  int j = 0, s_beg = seg_begin(0);
   constexpr int URING = uring_depth<EPI>();
   f4 uring[URING];
   int ub = ubase(j), ul = ulast(j);
 #pragma unroll
-  for (int r = 0; r < URING; ++r) uring[r] = ld4(ur, lo, r * XS + ub);
+  for (int r = 0; r < URING; ++r) uring[r] = ld4(ur, lo, r * XS + ub + s_beg * 1024);
   const float* vrd = ring + vslot(lane) * 4;
   // B fragments (V) of the next xi pair, carried across K-steps: step g + 1's first pair is read
   // during step g's last MFMAs, once the transform waves have published it
@@ -580,7 +614,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   // accumulators that are not live yet at the start of a K-step, so it costs no registers at the
   // peak.  Before the first item nothing is pending (offsets past the range: stores dropped);
   // the last item's part B runs after the loop.
-  constexpr bool DEFER = !SPLIT;
+  constexpr bool DEFER = !SPLIT;  // MODE 2: its whole-item segments
   constexpr bool DRES = DEFER && (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU);
   const __amdgpu_buffer_rsrc_t yr_d = uniform_rsrc(p.y, p.B * H * W * Cout * 4);
   f4 pv[16], pres[16], psc = {1.f, 1.f, 1.f, 1.f}, psh = {0.f, 0.f, 0.f, 0.f}, pal = psh, pcl = psh;
@@ -612,10 +646,14 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
     __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, po[i], 0, 0);
   };
-  // One item of the stream: its K-steps, then its epilogue.
-  auto segment = [&]() {
+  // One segment of the stream: its K-steps, then its epilogue.  TAIL (MODE 2 after the whole-
+  // item rounds): no deferred part B, every segment goes through a slot and a ticket (below).
+  // The two kinds are separate loops over separate instances of this body, so the tail's extra
+  // state never competes with the whole items' registers.
+  auto segment = [&](auto tail_c) {
+    constexpr bool TAIL = decltype(tail_c)::value;
     const Item it = item_at(j);
-    const int s0 = 0, s1 = KS;
+    const int s0 = s_beg, s1 = TAIL ? min(KST, s0 + (G - g)) : KS;
     const bool live = it.nb * 64 + w * 16 < Cout;  // Cout % 64 != 0: idle quarter of the last block
     const int ub_next = ubase(j + 1);               // the next item's step 0; its first step (prefetched
                                                     // during this item's last one)
@@ -628,7 +666,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       const float* vn = vrd + ((g + 1) % NBUF) * VSTEP;
       // U refills: xi + URING of this step, or xi + URING - 36 of the next step (or item)
       const int cur = ub + min(s, ul) * 1024;
-      const int nxt = s + 1 < s1 ? ub + min(s + 1, ul) * 1024 : ub_next;
+      const int nxt = s + 1 < s1 ? ub + min(s + 1, ul) * 1024 : ub_next + seg_begin(j + 1) * 1024;
       // xi in pairs: the two accumulation chains interleave (a 16x16x4 MFMA's result is not
       // ready for the next one on the same accumulator at issue rate).  A fragments one pair
       // ahead (the LDS reads of pair x + 2 are in flight during pair x's MFMAs); an idle
@@ -663,7 +701,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
         __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
         // the previous item's pending output pixel x / 2 - 2 (after this pair's refills, so the
         // refills of earlier pairs never wait for its store)
-        if constexpr (DEFER && decltype(first_step)::value)
+        if constexpr (DEFER && !TAIL && decltype(first_step)::value)
           if (x >= 4) finish(x / 2 - 2);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -679,6 +717,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     for (int s = s0 + 1; s < s1; ++s) kstep(s, std::false_type{});
     ub = ub_next;
     ul = ulast(j + 1);
+    s_beg = seg_begin(j + 1);
     // an idle quarter (!live, Cout % 64 != 0) runs the epilogue too, with every store dropped
     // (no branch: a merge here costs the next K-step a full wait for stores)
     // ---- epilogue (lane-local): U is the A operand, so lane (tile n, row group rg) holds
@@ -762,6 +801,125 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
           for (int r = 0; r < 4; ++r) pcl[r] = pal[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
         }
       };
+      if constexpr (TAIL) {
+        {
+          // a tail item (usually cut across workgroups): this wave's raw partial outputs (linear in
+          // the K-steps, so the parts sum to the item's output) into its compact slot [16 tiles][16
+          // pixels][64 couts], write-through (sc1), so the release below has no dirty slot lines to
+          // write back: slot 2 bl for the item this workgroup's range starts in, 2 bl + 1 for the
+          // item it ends in.  Few registers live here: outputs go straight to the slot and the
+          // finish works four pixels at a time.
+          const int slot = 2 * bl + (j == p.sk_dp ? 0 : 1);
+          const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
+          auto soff = [&](int sl, int i) { return ((((sl * FT + n) * 16 + i) * FN) + w * 16 + 4 * rg) * 4; };
+          {
+            f4 z[6][4];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+              const f4 m6[6] = {acc[6 * a], acc[6 * a + 1], acc[6 * a + 2], acc[6 * a + 3], acc[6 * a + 4], acc[6 * a + 5]};
+              at6q(m6, z[a]);
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+              const f4 c6[6] = {z[0][x], z[1][x], z[2][x], z[3][x], z[4][x], z[5][x]};
+              f4 o[4];
+              at6q(c6, o);
+#pragma unroll
+              for (int y = 0; y < 4; ++y) {
+                const u32x4 bits = {__float_as_uint(o[y].x), __float_as_uint(o[y].y), __float_as_uint(o[y].z),
+                                    __float_as_uint(o[y].w)};
+                __builtin_amdgcn_raw_buffer_store_b128(bits, sr, soff(slot, 4 * y + x), 0, CPOL_SC1);
+              }
+            }
+          }
+          // parts of tail item ti come from the workgroups first .. last whose ranges meet its
+          // steps [t_lo, t_hi); this wave's ticket (one per item and MFMA wave, G16 counter form)
+          // tells whether it arrived last.  The last one sums the parts in workgroup order
+          // (independent of the arrival order: deterministic) and finishes the item.
+          const int P = nblk;
+          const int ti = __builtin_amdgcn_readfirstlane(((volatile lds_int*)segtab)[2 * j]) - p.sk_dp * P;  // tail index
+          const long long TTt = (long long)(p.mblocks * p.nblocks - p.sk_dp * P) * KST;
+          const long long t_lo = (long long)ti * KST, t_hi = t_lo + KST;
+          auto lo_of = [&](int x) { return (long long)x * TTt / P; };
+          int first = (int)(t_lo * P / TTt);
+          while (first + 1 < P && lo_of(first + 1) <= t_lo) ++first;
+          while (first > 0 && lo_of(first) > t_lo) --first;
+          int last = (int)((t_hi - 1) * P / TTt);
+          while (last + 1 < P && lo_of(last + 1) <= t_hi - 1) ++last;
+          while (last > 0 && lo_of(last) > t_hi - 1) --last;
+          // (with fewer tail steps than workgroups some ranges are empty: only non-empty ones hold parts)
+          int nparts = 0;
+          for (int c = first; c <= last; ++c) nparts += lo_of(c + 1) > lo_of(c) ? 1 : 0;
+          // hand-off without L2-wide fences (a release here wrote back every dirty line of the
+          // XCD's L2, an acquire invalidated it): the slot stores are device-scope write-through,
+          // so once they have completed (vmcnt) they are visible device-wide before the ticket,
+          // and the last arriver reads the parts with device-scope loads (sc1) after it
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          int ticket = 0;
+          if (lane == 0) ticket = __hip_atomic_fetch_add(p.cnt + ti * 4 + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ticket = __builtin_amdgcn_readfirstlane(ticket);
+          if (ticket != nparts - 1) return;
+          if (lane == 0) p.cnt[ti * 4 + w] = 0;  // re-arm for the next launch (zeroed at allocation)
+          const f4 sc = *reinterpret_cast<const f4*>(p.post_scale + cout0);
+          const f4 sh = *reinterpret_cast<const f4*>(p.post_shift + cout0);
+          f4 al = {0.f, 0.f, 0.f, 0.f}, cl = al;
+          if constexpr (EPI == EPI_AFFINE_PRELU || EPI == EPI_AFFINE_RES_PRELU) {
+            al = *reinterpret_cast<const f4*>(p.prelu + cout0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cl[r] = al[r] <= 1.f ? __builtin_inff() : -__builtin_inff();
+          }
+          auto ld4c = [&](int off) {  // device-scope (sc1) load of a part
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(sr, off, 0, CPOL_SC1);
+            return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+          };
+          // half the item's 16 pixels at a time, up to three parts' loads in flight per round (the
+          // sums stay in part order: deterministic), the half's residual issued with them
+          int troff[4][4];
+          if constexpr (DRES) tile_offsets(RMIX ? rblk : yblk, troff);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f4 sm[8], rv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              sm[k] = f4{0.f, 0.f, 0.f, 0.f};
+              if constexpr (DRES) rv[k] = ld4(rr, troff[(8 * h + k) >> 2][(8 * h + k) & 3]);
+            }
+            // the parts' workgroups in order, three at a time (empty ranges skipped)
+            int c = first;
+            while (c <= last) {
+              int cs[3], np3 = 0;
+              for (; c <= last && np3 < 3; ++c)
+                if (lo_of(c + 1) > lo_of(c)) cs[np3++] = c;
+              f4 part[3][8];
+#pragma unroll
+              for (int cc = 0; cc < 3; ++cc) {
+                const int pc = cs[min(cc, max(np3 - 1, 0))];
+                const int cslot = 2 * pc + (lo_of(pc) < t_lo ? 1 : 0);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) part[cc][k] = ld4c(soff(cslot, 8 * h + k));
+              }
+#pragma unroll
+              for (int cc = 0; cc < 3; ++cc)
+                if (cc < np3)
+#pragma unroll
+                  for (int k = 0; k < 8; ++k) sm[k] += part[cc][k];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const int o = oo[(8 * h + k) >> 2][(8 * h + k) & 3];
+              f4 v = __builtin_elementwise_fma(sm[k], sc, sh);
+              if constexpr (EPI == EPI_AFFINE_PRELU) v = prelu_q(v, al, cl);
+              if constexpr (DRES) {
+                v += rv[k];
+                if constexpr (EPI == EPI_AFFINE_RES_PRELU) v = prelu_q(v, al, cl);
+              }
+              const u32x4 bits = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+              __builtin_amdgcn_raw_buffer_store_b128(bits, yr_d, o, 0, 0);
+            }
+          }
+          return;
+        }
+      }
       transform_to_pv();
       set_pending();
       return;
@@ -796,23 +954,37 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       }
     }
   };
-  for (; j < nloc; ++j) segment();
-  if constexpr (DEFER)
+  if constexpr (SK) {
+    for (; j < p.sk_dp; ++j) segment(std::false_type{});
+    // the last whole item's part B before the tail, whose segments defer nothing
 #pragma unroll
-    for (int i = 0; i < 16; ++i) finish(i);  // the last item's part B
+    for (int i = 0; i < 16; ++i) finish(i);
+    while (g < G) {  // (segment advances g)
+      segment(std::true_type{});
+      ++j;
+    }
+  } else {
+    for (; j < nloc; ++j) segment(std::false_type{});
+    if constexpr (DEFER)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) finish(i);  // the last item's part B
+  }
   w4_report_handoff(rseen, p.err);
 }
 
 template <bool PRE, int EPI, int MODE, int RMIX = 0>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
-  wino4_body<PRE, EPI, MODE, RMIX>(p, ring, blockIdx.x, gridDim.x);
+  wino4_body<PRE, EPI, MODE, false, RMIX>(p, ring, blockIdx.x, gridDim.x);
 }
 
 // Split-K finish of one output element group: y = epilogue(sum of an item's raw partial outputs,
 // in part order: deterministic) at the item's in-image pixels.  idx = (tile n, pixel, cout quad)
-// of launch item li, whose parts are in slots li * S .. li * S + S - 1.
-template <int EPI>
+// of launch item li, whose parts are in slots li * S .. li * S + S - 1.  CH (wino4_chain_kernel):
+// the parts and the residual were written by other CUs of the same launch, so they are loaded
+// device-coherent (sc1); the arithmetic is the same code either way, so a chained layer's output
+// is bitwise the fixup kernel's.
+template <int EPI, bool CH>
 __device__ __forceinline__ void w4_fixup_elem(const Wino4Params& p, int li, int idx) {
   const int gi = p.item0 + li, slot0 = li * p.ksplit, S = p.ksplit;
   const Item it = item_of(p, gi);
@@ -830,6 +1002,7 @@ __device__ __forceinline__ void w4_fixup_elem(const Wino4Params& p, int li, int 
   const long long pix = (long long)(rs * p.NC * H + y) * W + (long long)cs * H * W + x;
   if (pix >= (long long)p.B * H * W) return;
   const float4* slab = reinterpret_cast<const float4*>(p.part);
+  const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.part, (int)min(p.part_floats * 4, 0x7fffffffll));
   float v[4] = {0.f, 0.f, 0.f, 0.f};
   // sixteen slot loads in flight at a time (every part of a split-K item: S <= 16 K-steps of
   // 16 channels per part at the serving sizes), summed in part order (deterministic): a loop of
@@ -840,7 +1013,12 @@ __device__ __forceinline__ void w4_fixup_elem(const Wino4Params& p, int li, int 
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const long long q = ((((long long)slot0 + s0 + u) * FT + n) * 16 + px) * (FN / 4) + cq;
-      a[u] = s0 + u < S ? slab[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (CH) {
+        const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(sr, s0 + u < S ? (int)(q * 16) : BIGOFF, 0, CPOL_SC1);
+        a[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
+      } else {
+        a[u] = s0 + u < S ? slab[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u)
@@ -860,8 +1038,17 @@ __device__ __forceinline__ void w4_fixup_elem(const Wino4Params& p, int li, int 
   const long long yo = at((p.blk & W4_BLK_Y) != 0), ro = at((p.blk & W4_BLK_RES) != 0);
   float rv[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == EPI_AFFINE_RES || EPI == EPI_AFFINE_RES_PRELU) {
+    if constexpr (CH) {
+      const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, p.B * H * W * p.Cout * 4);
+      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(ro * 4), 0, CPOL_SC1);
+      rv[0] = __uint_as_float(w.x);
+      rv[1] = __uint_as_float(w.y);
+      rv[2] = __uint_as_float(w.z);
+      rv[3] = __uint_as_float(w.w);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) rv[r] = p.res[ro + r];
+      for (int r = 0; r < 4; ++r) rv[r] = p.res[ro + r];
+    }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -882,7 +1069,86 @@ __device__ __forceinline__ void w4_fixup_elem(const Wino4Params& p, int li, int 
 // Split-K finish launch: grid (FT * 16 * FN / 4 / blockDim, items), blockIdx.y = launch item.
 template <int EPI>
 __global__ void wino4_part_fixup_kernel(Wino4Params p, int KST, int P) {
-  w4_fixup_elem<EPI>(p, blockIdx.y, blockIdx.x * blockDim.x + threadIdx.x);
+  w4_fixup_elem<EPI, false>(p, blockIdx.y, blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// ---- Chained split-K layers (serving batches) ------------------------------------------------
+// A run of consecutive F(4x4) layers of an IR stage (conv1: pre-BN + BN + PReLU, conv2: BN +
+// identity residual), each a split-K launch (MODE 1) of at most one round of workgroups, runs as
+// ONE persistent launch: workgroup b computes its split of layer l (the same body as
+// wino4_kernel's, patches loaded device-coherent), stores the raw partial into its slot, waits on
+// its item's arrival counter until all S splits have stored theirs, then finishes slice b of the
+// item's outputs (w4_fixup_elem: the fixup kernel's arithmetic) and counts itself into layer l's
+// counter.  Layer l + 1 starts once layer l's counter has every workgroup of layer l: its patches,
+// and for conv2 the residual two layers back, are complete.  That removes, per layer, the fixup
+// launch and both kernel boundaries (each ~1.5-2 us plus the cold start of a fresh grid).
+//   * Co-residency: the grid is at most one workgroup per CU (LDS 147 KiB each) and the runtime
+//     only chains when nothing else shares the CUs (one lane); every wait is bounded (poll_max),
+//     an expired one is reported like a ring hand-off (FR_DEVERR_W4_HANDOFF) and the launch ends.
+//   * Hand-off form (MI355X_MICROARCH.md, visibility table, first row): every partial / output
+//     store is sc1 (write-through) and drained by its wave (vmcnt(0)) before a workgroup barrier;
+//     one lane then adds to the agent-scope counter; the consumer polls it with sc1 loads and
+//     reads every handed-off byte with sc1 loads, behind a workgroup barrier.
+//   * sync: [0] workgroups finished, [1 + l] layer l's finished workgroups, [cbase_l + li] item
+//     li's stored splits.  The last workgroup to finish zeroes them all for the next launch.
+constexpr int W4CH_EPI_PRE = 0;  // kind: conv1 (PRE, EPI_AFFINE_PRELU)
+__device__ __forceinline__ bool w4_poll_ge(int* c, int target, int poll_max) {
+  int n = 0;
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (++n > poll_max) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(512, 1) void wino4_chain_kernel(const W4Link* __restrict__ links, int nl, int* sync,
+                                                             int ncnt, int* err, int poll_max) {
+  __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
+  __shared__ int last;
+  const int tid = threadIdx.x, bid = blockIdx.x;
+  bool ok = true;
+  for (int l = 0; l < nl; ++l) {
+    const W4Link& L = links[l];
+    const int nwg = L.nwg;
+    if (bid >= nwg) continue;
+    if (l > 0) {  // every workgroup of layer l - 1 has stored its slice of that layer's output
+      if (tid == 0) ok = w4_poll_ge(sync + l, links[l - 1].nwg, poll_max) && ok;
+      __syncthreads();
+    }
+    if (L.kind == W4CH_EPI_PRE)
+      wino4_body<true, EPI_AFFINE_PRELU, 1, true>(L.p, ring, bid, nwg);
+    else
+      wino4_body<false, EPI_AFFINE_RES, 1, true>(L.p, ring, bid, nwg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial-slot stores
+    __syncthreads();
+    const Wino4Params& p = L.p;
+    // this workgroup's (split, item): item_at(0) of the body
+    const int t = xcd_remap(bid, nwg);
+    const int sp = t / p.nitem, li = t - sp * p.nitem, S = p.ksplit;
+    if (tid == 0) {
+      __hip_atomic_fetch_add(sync + L.cbase + li, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = w4_poll_ge(sync + L.cbase + li, S, poll_max) && ok;
+    }
+    __syncthreads();
+    // slice sp of the item's FT * 16 * FN / 4 output groups
+    constexpr int NE = FT * 16 * FN / 4;
+    const int e1 = (sp + 1) * NE / S;
+    for (int e = sp * NE / S + tid; e < e1; e += 512) {
+      if (L.kind == W4CH_EPI_PRE)
+        w4_fixup_elem<EPI_AFFINE_PRELU, true>(p, li, e);
+      else
+        w4_fixup_elem<EPI_AFFINE_RES, true>(p, li, e);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(sync + 1 + l, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // the last workgroup to get here re-arms every counter (all waits of this launch are over)
+  if (tid == 0) last = __hip_atomic_fetch_add(sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (last)
+    for (int i = tid; i < ncnt; i += 512) __hip_atomic_store(sync + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0 && !ok && err) __hip_atomic_store(err, FR_DEVERR_W4_HANDOFF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // G g G^T of every (cout, cin) filter, in double then rounded once to f32, scattered into the
@@ -957,7 +1223,7 @@ bool wino4_supported(int Cin, int Cout, int kh, int kw, int stride, int pad) {
 }
 
 namespace {
-// validation + canvas + item blocks of a layer (launch_wino4)
+// validation + canvas + item blocks of a layer (launch_wino4, wino4_chain_plan)
 bool w4_setup(Wino4Params& p, bool pre) {
   p.poll_max = p.poll_max == 0 ? WINO4_POLL_DEFAULT : std::max(p.poll_max, 0);  // < 0: no polls (tests)
   if (!wino4_supported(p.Cin, p.Cout, 3, 3, 1, 1) || p.B < 1 || p.H < 1 || p.W < 1 ||
@@ -1015,6 +1281,28 @@ int w4_split_of(const Wino4Params& p, int n, int cus, int& ks_per) {
 }
 }  // namespace
 
+bool wino4_chain_plan(Wino4Params& p, bool pre, Epi epi, int cus) {
+  if (!((pre && epi == EPI_AFFINE_PRELU) || (!pre && epi == EPI_AFFINE_RES)) || !w4_setup(p, pre)) return false;
+  const int KST = p.Cin / KC, nT = p.mblocks * p.nblocks;
+  if (!p.part || p.no_split || !w4_aligned(p) || KST < 2 || nT > cus / 2) return false;
+  int ks_per = KST;
+  const int S = w4_split_of(p, nT, cus, ks_per);
+  if (S < 2 || nT * S > cus) return false;
+  p.item0 = 0;
+  p.nitem = nT;
+  p.ksplit = S;
+  p.ks_per = ks_per;
+  return true;
+}
+
+hipError_t launch_wino4_chain(const W4Link* links, int nl, int grid, int* sync, int ncnt, int* err, int poll_max,
+                              hipStream_t s) {
+  if (!links || nl < 1 || grid < 1 || !sync || ncnt < 1 + nl) return hipErrorInvalidValue;
+  poll_max = poll_max == 0 ? WINO4_POLL_DEFAULT : std::max(poll_max, 0);
+  hipLaunchKernelGGL(wino4_chain_kernel, dim3(grid), dim3(512), 0, s, links, nl, sync, ncnt, err, poll_max);
+  return hipGetLastError();
+}
+
 hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s) {
   Wino4Params p = p0;
   if (!w4_setup(p, pre)) return hipErrorInvalidValue;
@@ -1024,10 +1312,19 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   const int cus = w4_cus();
   const bool can_split = p.part && !p.no_split && aligned && KST > 1;
   auto split_of = [&](int n, int& ks_per) { return w4_split_of(p, n, cus, ks_per); };
-  // Whole-item launch of n items from item0 (MODE 0), or split-K launch (MODE 1) + fixup.  (A
-  // stream-K tail for the part-empty last round of whole items -- IR-101 B = 256: stage 3 3.52
-  // rounds run as 4 -- was built in round 4 and measured neutral; two concurrent lanes fill that
-  // round instead: tools/w4_archive/)
+  // stream-K (p.sk_mode): whole items for floor(nT / cus) rounds, then the tail items' K-steps in
+  // equal contiguous ranges, one per workgroup, so the part-empty last round of whole items
+  // (IR-101 B=256: stage 3 3.52 rounds run as 4, stage 2 6.13 as 7) becomes a fraction of a round;
+  // a cut item is finished in the launch by its last-arriving wave.  Whole items keep every
+  // workgroup on the same K-step of its item, so an XCD's workgroups read the same U slice at a
+  // time; stream-K ranges start at arbitrary steps and read all of U at once (round 2, stream-K
+  // over ALL item-steps at stage 3, U 9.4 MB: 238 -> 324 us), so only the tail runs that way.
+  // sk_mode 2 (tests, experiments) cuts every item-step.
+  const int sk_dp = p.sk_mode == 2 ? 0 : nT / cus;
+  const bool sk = p.sk_mode && p.part && p.cnt && aligned && nT > cus && cus % 8 == 0 && nT % cus != 0 &&
+                  (long long)(nT - sk_dp * cus) * 4 <= p.cnt_cap && (long long)2 * cus * SLOT <= p.part_floats;
+  // Whole-item launch of n items from item0 (MODE 0), or split-K launch (MODE 1) + fixup
+  p.sk_dp = sk_dp;
   Wino4Params pw = p;
   auto whole = [&](int item0, int n) {
     pw = p;
@@ -1045,14 +1342,15 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
   };
 #define FR_W4_LAUNCH(PRE_, EPI_, MODE_)                                                                     \
   {                                                                                                         \
-    const int nit = pw.nitem * pw.ksplit;                                                                   \
-    hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, MODE_>), dim3(std::min(nit, cus)), dim3(512), 0, s, pw);   \
+    const int nit = MODE_ == 2 ? nT : pw.nitem * pw.ksplit;                                                 \
+    hipLaunchKernelGGL((wino4_kernel<PRE_, EPI_, MODE_>), dim3(MODE_ == 2 ? cus : std::min(nit, cus)),      \
+                       dim3(512), 0, s, pw);                                                                \
     if (MODE_ == 1) /* 64-thread blocks: a serving grid's few items still spread over the CUs */          \
       hipLaunchKernelGGL((wino4_part_fixup_kernel<EPI_>), dim3(FT * 16 * FN / 4 / 64, pw.nitem),     \
                          dim3(64), 0, s, pw, KST, cus);                                                     \
   }
   // a residual whose layout differs from y's (p.blk: the seams between NHWC and channel-blocked
-  // activations): whole-item launches run instances of their own (RMIX); a split-K
+  // activations): whole-item and stream-K launches run instances of their own (RMIX); a split-K
   // launch's fixup addresses the residual on its own anyway, so split-K is the usual one
   const bool rmix = (((p.blk & W4_BLK_RES) != 0) != ((p.blk & W4_BLK_Y) != 0)) &&
                     (epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU);
@@ -1066,11 +1364,18 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
       return hipGetLastError();
     }
     whole(0, nT);
-    const dim3 grid(std::min(nT, cus));
-    if (p.blk & W4_BLK_Y)
-      hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 1>), grid, dim3(512), 0, s, pw);
-    else
-      hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 2>), grid, dim3(512), 0, s, pw);
+    const dim3 grid(sk ? cus : std::min(nT, cus));
+    if (p.blk & W4_BLK_Y) {
+      if (sk)
+        hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 2, 1>), grid, dim3(512), 0, s, pw);
+      else
+        hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 1>), grid, dim3(512), 0, s, pw);
+    } else {
+      if (sk)
+        hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 2, 2>), grid, dim3(512), 0, s, pw);
+      else
+        hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 2>), grid, dim3(512), 0, s, pw);
+    }
     return hipGetLastError();
   }
 #define FR_W4_CASE(PRE_, EPI_)                                                                              \
@@ -1086,6 +1391,9 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
         whole(0, nT);                                                                                       \
         FR_W4_LAUNCH(PRE_, EPI_, 0)                                                                         \
       }                                                                                                     \
+    } else if (sk) {                                                                                        \
+      whole(0, nT);                                                                                         \
+      FR_W4_LAUNCH(PRE_, EPI_, 2)                                                                           \
     } else {                                                                                                \
       /* whole items.  (Running a part-empty last round as a split-K launch of its own was      */          \
       /* measured neutral: stage 2, 6 rounds + 32 items, 244.6 -> 245.8 us; the short launch and  */          \

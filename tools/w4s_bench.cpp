@@ -1,5 +1,5 @@
 // Stand-alone check and timing of the symmetric-wave F(4x4) kernel
-// (csrc/conv_winograd4s.hip) against the shipping F(4x4) one on the same
+// (tools/w4_archive/conv_winograd4s.hip, in the library in round 5) against the F(4x4) one on the same
 // layer (same U), and both against a float64 direct convolution of the first images.
 // usage: w4s_bench B H Cin Cout epi iters [nimg_check] [lanes] [copies] [blk] [sk]   (epi 1 = pre-BN + BN + PReLU, 2 = BN + residual,
 //        3 = BN + PReLU without pre-BN; W6_ZERO_SHIFT=1: pre-BN shift 0; lanes 2: timing as two
@@ -18,7 +18,7 @@
 #include <random>
 #include <vector>
 
-#include "conv_winograd4s.hip"  // the symmetric-wave kernel (csrc/)
+#include "conv_winograd4s.hip"  // the symmetric-wave kernel (tools/w4_archive/)
 
 using namespace frhip;
 
