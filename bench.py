@@ -234,11 +234,11 @@ def profile_figures(traffic_json, family, build, same_workload):
 
 def detector_profile_figures(build):
     """PMC figures of the detector's F(4x4) launches from the committed detector profile
-    (profiles/r*/det_layers_pmc.json, tools/gpu_det_profile.sh -> tools/det_prof_summary.py), only
+    (profiles/r*/c4_layers_pmc.json, tools/gpu_det_profile.sh -> tools/det_prof_summary.py), only
     when it was taken on this library build: (HBM bytes per launch, algorithmic bytes per launch,
     MFMA-busy fraction, source, note)."""
     import glob
-    cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "det_layers_pmc.json")))
+    cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "c4_layers_pmc.json")))
     if not cands:
         return None, None, None, None, "no detector PMC profile found"
     with open(cands[-1]) as f:
