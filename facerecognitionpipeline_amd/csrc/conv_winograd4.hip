@@ -140,13 +140,20 @@ __device__ __forceinline__ int vslot(int l) {
 // Single writer per counter: a plain ds_write after the wave's earlier LDS operations have
 // completed (LDS serves a wave's operations in order); readers poll with volatile reads.
 typedef __attribute__((address_space(3))) int lds_int;  // LDS pointers: ds_* instructions, not flat_*
-__device__ __forceinline__ int lds_min4(const int* c) {
+template <int N>
+__device__ __forceinline__ int lds_min(const int* c) {
   const volatile lds_int* v = (const volatile lds_int*)c;
-  const int m = min(min(v[0], v[1]), min(v[2], v[3]));
+  int m;
+  if constexpr (N == 4)
+    m = min(min(v[0], v[1]), min(v[2], v[3]));
+  else if constexpr (N == 2)
+    m = min(v[0], v[1]);
+  else
+    m = min(min(min(v[0], v[1]), min(v[2], v[3])), min(v[4], v[5]));
   return __builtin_amdgcn_readfirstlane(m);
 }
 
-// Wait until min(c[0..3]) >= need; returns the value seen.  The spin is bounded (poll_max
+// Wait until min(c[0..N-1]) >= need; returns the value seen.  The spin is bounded (poll_max
 // polls, 2^16 = a few ms by default): a lost hand-off cannot hang the GPU.  An expired wait
 // returns the value seen with W4_EXPIRED set: the caller's counter copy then exceeds every later
 // `need`, so the wave waits no more, carries on (every global access of the kernel is
@@ -154,11 +161,12 @@ __device__ __forceinline__ int lds_min4(const int* c) {
 // (w4_report_handoff).  Folding the flag into the counter copy keeps the hot loop free of a
 // store and of a register of its own (a separate flag cost the conv2 kernel 2 spilled VGPRs).
 constexpr int W4_EXPIRED = 1 << 30;
-__device__ __forceinline__ int lds_wait_min4(const int* c, int need, int poll_max) {
-  int seen = lds_min4(c);
+template <int N = 4>
+__device__ __forceinline__ int lds_wait_min(const int* c, int need, int poll_max) {
+  int seen = lds_min<N>(c);
   for (int it = 0; seen < need && it < poll_max; ++it) {
     __builtin_amdgcn_s_sleep(1);
-    seen = lds_min4(c);
+    seen = lds_min<N>(c);
   }
   asm volatile("" ::: "memory");
   return seen < need ? (seen | W4_EXPIRED) : seen;
@@ -285,9 +293,17 @@ constexpr int W4_LDS_FLOATS = NBUF * VSTEP + NGEO * FT * GEOW + 8;
 // computed on their own: more live registers in the epilogue): 1 = residual NHWC, output
 // channel-blocked; 2 = residual channel-blocked, output NHWC.  0: p.blk's y and res layouts are the
 // same, and the residual is addressed with the output's offsets.
-template <bool PRE, int EPI, int MODE, int RMIX = 0>
+// NMW: MFMA waves per workgroup (the others transform).  4 (the default): items of 64 couts, four
+// transform waves of 4 tiles each.  6 (wino4w_kernel): items of 96 couts for layers of 65..96
+// output channels (the detector's 80 / 88 -> 96): six MFMA waves (two on SIMDs 0 and 1) and two
+// transform waves of 8 tiles each (two passes of 4), whole items only, no pre-BN.  A layer of 96
+// couts runs one item per 16 tiles instead of two with half of the second idle.
+template <bool PRE, int EPI, int MODE, int RMIX = 0, int NMW = 4>
 __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, const int bid, const int nblk) {
   constexpr bool SPLIT = MODE == 1;
+  constexpr int NTW = 8 - NMW;   // transform waves
+  constexpr int FNW = 16 * NMW;  // output channels per item
+  static_assert(NMW == 4 || (NMW == 6 && !PRE && MODE == 0 && RMIX == 0), "wide items: whole items, no pre-BN");
   __builtin_assume(bid >= 0 && bid < nblk && nblk <= 65535);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -312,12 +328,149 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   const int G = nloc * KS;  // K-steps in this workgroup's stream
 
   int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [NGEO items][16 tiles][GEOW]
-  int* const rdy = geo + NGEO * FT * GEOW;                        // [4] K-steps written, per transform wave
-  int* const fre = rdy + 4;                                       // [4] K-steps read, per MFMA wave
+  int* const rdy = geo + NGEO * FT * GEOW;                        // [NTW] K-steps written, per transform wave
+  int* const fre = rdy + NTW;                                     // [NMW] K-steps read, per MFMA wave
   if (tid < 8) rdy[tid] = 0;
   __syncthreads();  // the kernel's only workgroup barrier
   if (G <= 0) return;
-  if (wid >= 4) {
+  if constexpr (NTW == 2) {
+    if (wid >= NMW) {
+      // ---- two transform waves (wide items): wave t transforms tiles 8t .. 8t+7 of every K-step
+      // in two passes of four (q = 0, 1), each pass the lane mapping, loads, transform and ring
+      // writes of the four-wave form below (no pre-BN, whole items); the patches of step g + 1 are
+      // loaded while step g is transformed (two buffers per pass)
+      const int t = wid - NMW;
+      const int half = lane >> 5, ii = (lane >> 3) & 3, pr = lane & 7;
+      const int ch = 2 * pr;
+      const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x, p.B * H * W * Cin * 4);
+      const bool xblk = (p.blk & W4_BLK_X) != 0;
+      const int xppx = xblk ? KC : Cin;
+      const int xstep = xblk ? H * W * KC * 4 : KC * 4;
+      const bool sep_r = p.Pr > H, sep_c = p.Pc > W;
+      int poff[2][6][3];
+      int lj = 0, ls = 0;
+      auto enter_item = [&](int j) {
+        const Item it = item_at(min(j, t_last));
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int i = 8 * t + 4 * q + ii;
+          const int T = it.mb * FT + i;
+          const int tr = T / p.TWc, tc = T - tr * p.TWc;
+          const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
+          int roff[6], coff[3];
+#pragma unroll
+          for (int e = 0; e < 6; ++e) {
+            int rs;
+            const int y = canvas_coord(4 * tr - 1 + e, ir0, p.Pr, H, sep_r, rs);
+            roff[e] = y >= 0 && rs * p.NC < p.B && T < p.ntiles ? (rs * p.NC * H * W * Cin + y * W * xppx) * 4 : BIGOFF;
+          }
+#pragma unroll
+          for (int e = 0; e < 3; ++e) {
+            int cs;
+            const int x = canvas_coord(4 * tc - 1 + 3 * half + e, ic0, p.Pc, W, sep_c, cs);
+            coff[e] = x >= 0 && cs < p.NC ? (cs * H * W * Cin + x * xppx + ch) * 4 : BIGOFF;
+          }
+#pragma unroll
+          for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) poff[q][a][b] = (int)((unsigned)roff[a] + (unsigned)coff[b]);
+          if (half == 0 && pr == 0 && j <= t_last) {  // the item's output geometry (as below)
+            int* gt = geo + ((j % NGEO) * FT + i) * GEOW;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              int rs, cs;
+              const int y = canvas_coord(4 * tr + e, ir0, p.Pr, H, sep_r, rs);
+              const int x = canvas_coord(4 * tc + e, ic0, p.Pc, W, sep_c, cs);
+              const bool rok = y >= 0 && rs * p.NC < p.B && T < p.ntiles, cok = x >= 0 && cs < p.NC;
+              gt[e] = rok ? rs * p.NC * H * W * Cout : 0;
+              gt[4 + e] = rok ? y * W : -1;
+              gt[8 + e] = cok ? cs * H * W * Cout : 0;
+              gt[12 + e] = cok ? x : -1;
+            }
+          }
+        }
+      };
+      struct Patch2 {
+        f2 d[2][6][3];
+      };
+      auto load = [&](Patch2& P) {
+        if (ls == 0) enter_item(lj);
+        const int soff = __builtin_amdgcn_readfirstlane(min(ls, KST - 1)) * xstep;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+              const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, poff[q][a][b], soff, 0);
+              P.d[q][a][b] = f2{__uint_as_float(v.x), __uint_as_float(v.y)};
+            }
+        if (++ls == KS) {
+          ++lj;
+          ls = 0;
+        }
+      };
+      int dst_off[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) dst_off[q] = vslot(16 * (ch >> 2) + 8 * t + 4 * q + ii) * 4 + (ch & 3) + half * 18 * 256;
+      auto store = [&](Patch2& P, int g) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          f2 (&d)[6][3] = P.d[q];
+#pragma unroll
+          for (int b = 0; b < 3; ++b) {
+            f2 c[6], o[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) c[a] = d[a][b];
+            bt6v(c, o);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) d[a][b] = o[a];
+          }
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(d[k][b][e]),
+                                                                __float_as_uint(d[3 + k][b][e]), false, false);
+                d[k][b][e] = __uint_as_float(r[0]);
+                d[3 + k][b][e] = __uint_as_float(r[1]);
+              }
+          float* dst = ring + (g % NBUF) * VSTEP + dst_off[q];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const f2 row[6] = {d[k][0], d[k][1], d[k][2], d[3 + k][0], d[3 + k][1], d[3 + k][2]};
+            f2 v[6];
+            bt6v(row, v);
+#pragma unroll
+            for (int b = 0; b < 6; ++b) *reinterpret_cast<f2*>(dst + (6 * k + b) * 256) = v[b];
+          }
+        }
+      };
+      int fseen = 0;
+      auto put = [&](Patch2& P, int g) {
+        if (g - NBUF + 1 > fseen) fseen = lds_wait_min<NMW>(fre, g - NBUF + 1, p.poll_max);
+        store(P, g);
+        lds_publish(rdy + t, lane, g + 1);
+      };
+      Patch2 pa, pb;
+      load(pa);
+      for (int b = 0;; b += 2) {
+        load(pb);  // (past the stream's end it re-reads the clamped last item; never stored)
+        __builtin_amdgcn_sched_barrier(0);
+        put(pa, b);
+        if (b + 1 >= G) break;
+        load(pa);
+        __builtin_amdgcn_sched_barrier(0);
+        put(pb, b + 1);
+        if (b + 2 >= G) break;
+      }
+      w4_report_handoff(fseen, p.err);
+      return;
+    }
+  }
+  if (wid >= NMW) {
     // ---- transform waves: every K-step, wave t transforms tiles 4t .. 4t+3 of the item for
     // the step's 16 channels in packed f32, two channels per lane and half a patch per lane:
     // lane (half h, tile 4t + ii, channel pair pr) loads patch columns 3h .. 3h+2 of channels
@@ -506,7 +659,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     // compiler's wait-count tracking wait for the freshly issued loads before the store.
     int fseen = 0;
     auto put = [&](Patch& P, int g) {
-      if (g - NBUF + 1 > fseen) fseen = lds_wait_min4(fre, g - NBUF + 1, p.poll_max);
+      if (g - NBUF + 1 > fseen) fseen = lds_wait_min<NMW>(fre, g - NBUF + 1, p.poll_max);
       store(P, g);
       lds_publish(rdy + t, lane, g + 1);
     };
@@ -553,7 +706,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   const int XS = NB16 * KST * 1024;
   auto ubase = [&](int j) {  // byte offset of (item j, step 0 of its K range, xi 0)
     const Item it = item_at(min(j, t_last));
-    return (min(it.nb * 4 + w, NB16 - 1) * KST + (SPLIT ? it.split * KS : 0)) * 1024;
+    return (min(it.nb * NMW + w, NB16 - 1) * KST + (SPLIT ? it.split * KS : 0)) * 1024;
   };
   auto ulast = [&](int j) {  // last real K-step of item j (split-K: the short last split)
     return SPLIT ? steps_of(item_at(min(j, t_last))) - 1 : KST - 1;
@@ -568,7 +721,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   const float* vrd = ring + vslot(lane) * 4;
   // B fragments (V) of the next xi pair, carried across K-steps: step g + 1's first pair is read
   // during step g's last MFMAs, once the transform waves have published it
-  int rseen = lds_wait_min4(rdy, 1, p.poll_max);  // step 0 is in the ring
+  int rseen = lds_wait_min<NTW>(rdy, 1, p.poll_max);  // step 0 is in the ring
   f4 a0n = *reinterpret_cast<const f4*>(vrd), a1n = *reinterpret_cast<const f4*>(vrd + 256);
   int g = 0;
   // Whole-item launches (MODE 0) split each item's epilogue in two.  Part A, at the end of item
@@ -616,7 +769,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   auto segment = [&]() {
     const Item it = item_at(j);
     const int s0 = 0, s1 = KS;
-    const bool live = it.nb * 64 + w * 16 < Cout;  // Cout % 64 != 0: idle quarter of the last block
+    const bool live = it.nb * FNW + w * 16 < Cout;  // Cout % FNW != 0: idle wave of the last block
     const int ub_next = ubase(j + 1);               // the next item's step 0; its first step (prefetched
                                                     // during this item's last one)
     f4 acc[NXI];
@@ -638,7 +791,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
         const f4 a0 = a0n, a1 = a1n;
         // the last pair reads step g + 1's first fragments: wait until it is published (the
         // counter seen last time usually already covers it: no poll)
-        if (x + 2 == NXI && g + 1 < G && rseen < g + 2) rseen = lds_wait_min4(rdy, g + 2, p.poll_max);
+        if (x + 2 == NXI && g + 1 < G && rseen < g + 2) rseen = lds_wait_min<NTW>(rdy, g + 2, p.poll_max);
         const float* nb = x + 2 < NXI ? vb + (x + 2) * 256 : vn;
         a0n = *reinterpret_cast<const f4*>(nb);
         a1n = *reinterpret_cast<const f4*>(nb + 256);
@@ -685,7 +838,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     // couts 4rg .. 4rg+3 of tile n for every xi; Y = A^T M A per (tile, cout), BN (+PReLU |
     // +residual), one 16-byte store of the 4 couts per output pixel
     const int n = lane & 15, rg = lane >> 4;
-    const int cout0 = min(it.nb * 64 + w * 16, Cout - 16) + 4 * rg;  // (clamped for an idle quarter)
+    const int cout0 = min(it.nb * FNW + w * 16, Cout - 16) + 4 * rg;  // (clamped for an idle wave)
     const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.res, DRES ? p.B * H * W * Cout * 4 : 0);
     // byte offsets of tile n's 16 outputs = a row part + a column part (8 multiplies, not 16).
     // Padding rows / columns and an idle quarter get BIGOFF, so every sum with them lies past the
@@ -807,6 +960,13 @@ template <bool PRE, int EPI, int MODE, int RMIX = 0>
 __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
   __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
   wino4_body<PRE, EPI, MODE, RMIX>(p, ring, blockIdx.x, gridDim.x);
+}
+
+// Wide items (96 couts, six MFMA waves): whole-item launches of layers of 65..96 output channels
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void wino4w_kernel(Wino4Params p) {
+  __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
+  wino4_body<false, EPI, 0, 0, 6>(p, ring, blockIdx.x, gridDim.x);
 }
 
 // Split-K finish of one output element group: y = epilogue(sum of an item's raw partial outputs,
@@ -1071,6 +1231,23 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
       hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 1>), grid, dim3(512), 0, s, pw);
     else
       hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 2>), grid, dim3(512), 0, s, pw);
+    return hipGetLastError();
+  }
+  // wide items: a whole-item launch of a layer of 65..96 couts (the detector's 80-channel towers
+  // and heads) as one 96-cout item per 16 tiles on wino4w_kernel, not a 64-cout item plus one with
+  // three of its four MFMA waves idle (each with its own input transform)
+  if (p.wide && !pre && p.Cout > FN && p.Cout <= 96 && !(can_split && nT <= cus / 2) &&
+      (epi == EPI_AFFINE || epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE_RES_PRELU)) {
+    p.nblocks = 1;
+    p.nbg = std::max(1, std::min(p.mblocks, p.nbg_override > 0 ? p.nbg_override : 32));
+    whole(0, p.mblocks);
+    const dim3 grid(std::min(p.mblocks, cus));
+    if (epi == EPI_AFFINE)
+      hipLaunchKernelGGL((wino4w_kernel<EPI_AFFINE>), grid, dim3(512), 0, s, pw);
+    else if (epi == EPI_AFFINE_PRELU)
+      hipLaunchKernelGGL((wino4w_kernel<EPI_AFFINE_PRELU>), grid, dim3(512), 0, s, pw);
+    else
+      hipLaunchKernelGGL((wino4w_kernel<EPI_AFFINE_RES_PRELU>), grid, dim3(512), 0, s, pw);
     return hipGetLastError();
   }
 #define FR_W4_CASE(PRE_, EPI_)                                                                              \

@@ -152,6 +152,9 @@ struct Wino4Params {
   // NHWC (the same per-element arithmetic either way: outputs are bitwise the NHWC launch's)
   int blk;
   int nbg_override;  // > 0: tile blocks per XCD item group instead of the rule (A/B only)
+  // 1: a whole-item launch of a layer of 65..96 output channels without pre-BN runs items of 96
+  // couts on wino4w_kernel (six MFMA waves, two transform waves) instead of two 64-cout items
+  int wide;
 };
 constexpr int W4_BLK_X = 1, W4_BLK_RES = 2, W4_BLK_Y = 4;
 constexpr int WINO4_POLL_DEFAULT = 1 << 16;

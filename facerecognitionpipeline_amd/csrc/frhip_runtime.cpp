@@ -293,6 +293,8 @@ static int g_wino4_max_split = 0;
 static int g_s2band = 1;
 // poll bound of wino4_kernel's ring hand-off waits (frt_set_wino4_poll_limit: tests force expiry)
 static int g_wino4_poll = WINO4_POLL_DEFAULT;
+// layers of 65..96 couts on wide F(4x4) items (frt_set_wino4_wide: A/B and tests)
+static int g_wino4_wide = 1;
 
 
 // serving conv kernel: layers of at most this many output pixels (n * Ho * Wo).  Batch 1 also
@@ -440,6 +442,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     wp.blk = h->w4_blk;  // forward_lanes' plan of channel-blocked activations
     wp.nbg_override = g_wino4_nbg;
+    wp.wide = g_wino4_wide;
     Wino4Params cv = wp;
     cv.blk = 0;
     wino4_canvas(cv);
@@ -2195,6 +2198,10 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 }
 
 static int g_frt_wino4_split = 1;
+int frt_set_wino4_wide(int on) {
+  g_wino4_wide = on ? 1 : 0;
+  return FR_OK;
+}
 int frt_set_wino4_nbg(int nbg) {
   if (nbg < 0) return FR_ERR_INVALID_ARGUMENT;
   g_wino4_nbg = nbg;
@@ -2342,8 +2349,12 @@ int frt_set_wino4_split(int on) {
 int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H, int W, int cin, int cout,
                         const float* pre_scale, const float* pre_shift, const float* post_scale,
                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream) {
-  if (!wino4_supported(cin, cout, 3, 3, 1, 1) || (epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES) ||
-      (epi == EPI_AFFINE_PRELU && (!pre_scale || !pre_shift || !prelu)) || (epi == EPI_AFFINE_RES && (pre_scale || !res)) ||
+  // epilogues: the IR body's (1 with pre-BN, 2) and the detector's (0, 1 without pre-BN, 5)
+  const bool res_epi = epi == EPI_AFFINE_RES || epi == EPI_AFFINE_RES_PRELU;
+  const bool prelu_epi = epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE_RES_PRELU;
+  if (!wino4_supported(cin, cout, 3, 3, 1, 1) ||
+      (epi != EPI_AFFINE && epi != EPI_AFFINE_PRELU && epi != EPI_AFFINE_RES && epi != EPI_AFFINE_RES_PRELU) ||
+      (pre_scale && (epi != EPI_AFFINE_PRELU || !pre_shift)) || (prelu_epi && !prelu) || (res_epi != (res != nullptr)) ||
       !post_scale || !post_shift || B < 1 || H < 1 || W < 1)
     return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_conv2d_winograd4: bad arguments");
   hipStream_t s = (hipStream_t)stream;
@@ -2381,6 +2392,7 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.no_split = !g_frt_wino4_split;
     p.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     p.err = frt_err;
+    p.wide = g_wino4_wide;
     if (g_frt_wino4_split) {  // split-K partial slots (64 KiB each)
       p.part_floats = 257ll * 2 * 16 * 16 * 64;
       if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;

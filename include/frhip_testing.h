@@ -36,7 +36,8 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
                         const float* pre_scale, const float* pre_shift, const float* post_scale,
                         const float* post_shift, const float* prelu, const float* res, int epi, void* stream);
 /* Winograd F(4x4,3x3) (the FR_CONV_WINOGRAD4 path, conv_winograd4.hip), same arguments;
- * cin % 16 == 0, cout % 16 == 0.  frt_conv2d_winograd4 gives launch_wino4 a split-K workspace
+ * cin % 16 == 0, cout % 16 == 0; epi also 0 (affine) and 5 (affine + residual + PReLU), and 1 without
+ * pre-BN (the detector's convs).  frt_conv2d_winograd4 gives launch_wino4 a split-K workspace
  * (small grids then split the K loop over items + a reduce pass) unless frt_set_wino4_split(0). */
 int frt_set_wino4_split(int on);
 /* A/B (process-wide): the ConvTile of the fused stride-2 conv2 + conv-shortcut launches of
@@ -45,6 +46,10 @@ int frt_set_conv2sc_tile(int tile);
 /* A/B (process-wide): tile blocks per XCD item group of the F(4x4) launches (0: the built-in rule,
  * 32 items per group; 8 x 8 at 512 channels).  Forwards already captured in graphs keep theirs. */
 int frt_set_wino4_nbg(int nbg);
+/* A/B (process-wide, default on): whole-item F(4x4) launches of layers of 65..96 output channels
+ * without pre-BN (the detector's 80-channel towers and heads) run items of 96 couts (six MFMA
+ * waves, two transform waves) instead of two 64-cout items.  Graphs captured before keep theirs. */
+int frt_set_wino4_wide(int on);
 /* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
  * before the call keep their schedule). */
 int frt_set_wino4_max_split(int s);

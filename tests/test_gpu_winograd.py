@@ -124,6 +124,54 @@ def test_winograd4_split_k_small_grids(B, H, cin, cout, epi):
     assert torch.equal(again, outs[1]), "split-K result is not run-to-run deterministic"
 
 
+def _det_case(B, H, W, cin, cout, epi, seed):
+    """The detector's epilogues (no pre-BN): 0 affine, 1 affine + PReLU, 5 affine + residual + PReLU."""
+    x = _rand(B, cin, H, W, seed=seed)
+    w = _rand(cout, cin, 3, 3, seed=seed + 1) / (cin * 9) ** 0.5
+    post_s, post_b = _rand(cout, seed=seed + 4, lo=0.5, hi=1.5), _rand(cout, seed=seed + 5, lo=-0.2, hi=0.2)
+    al = _rand(cout, seed=seed + 6, lo=0.0, hi=0.4)
+    ref = F.conv2d(x, w, padding=1) * post_s.view(1, -1, 1, 1) + post_b.view(1, -1, 1, 1)
+    res = None
+    if epi == 5:
+        r = _rand(B, cout, H, W, seed=seed + 7)
+        ref = ref + r
+        res = _nhwc(r).to(DEV)
+    if epi in (1, 5):
+        ref = torch.where(ref > 0, ref, ref * al.view(1, -1, 1, 1))
+    got = _frt.conv2d_winograd(_nhwc(x).to(DEV), w.permute(0, 2, 3, 1).contiguous().to(DEV), B, H, W, cin, cout,
+                               post=(post_s.to(DEV), post_b.to(DEV)), prelu=al.to(DEV) if epi in (1, 5) else None,
+                               res=res, epi=epi, m=4)
+    torch.cuda.synchronize()
+    return got.cpu(), _nhwc(ref)
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout", [
+    (32, 40, 40, 80, 80),   # detector stride-16 tower conv at 32 frames: 200 wide items
+    (16, 20, 20, 80, 96),   # a full 96-cout item, 25 items
+    (3, 17, 23, 48, 80),    # odd map (separator rows / columns), 3 K-steps
+    (1, 4, 4, 16, 96),      # one item, one K-step, 15 of its 16 tiles outside
+    (64, 10, 10, 96, 96),   # canvas of 2 images per row (period 11 -> 2 per 4-aligned row), 6 K-steps
+])
+@pytest.mark.parametrize("epi", [0, 1, 5])
+def test_winograd4_wide_items(B, H, W, cin, cout, epi):
+    """Layers of 65..96 couts without pre-BN run items of 96 couts (wino4w_kernel: six MFMA waves,
+    two transform waves of two 4-tile passes) instead of a 64-cout item and a mostly idle one: both
+    match the CPU conv, and each other bitwise (every output's products and sums are the same)."""
+    L = _frt.lib()
+    outs = {}
+    try:
+        L.frt_set_wino4_split(0)  # whole items at every grid size (small grids would split K)
+        for wide in (1, 0):
+            L.frt_set_wino4_wide(wide)
+            got, ref = _det_case(B, H, W, cin, cout, epi, seed=1700 + H + cin + cout + epi)
+            _close(got, ref, rel=REL[4])
+            outs[wide] = got
+    finally:
+        L.frt_set_wino4_wide(1)
+        L.frt_set_wino4_split(1)
+    assert torch.equal(outs[1], outs[0]), "wide items differ from 64-cout items"
+
+
 @pytest.mark.parametrize("B,H,W", [(5, 8, 14), (3, 12, 5), (6, 16, 10)])
 def test_winograd4_pre_bn_partial_canvas_row(B, H, W):
     """Folded pre-BN (U from w * scale, shift / scale added at in-image pixels) on canvases
