@@ -288,22 +288,35 @@ __device__ __forceinline__ Item item_of(const Wino4Params& p, int gi) {
 // are kept outside the library: tools/w4_archive/conv_winograd4_streamk_chain.hip.)
 // The kernel body of wino4_kernel (bid, nblk = blockIdx.x, gridDim.x); ring: the workgroup's LDS
 // (W4_LDS_FLOATS).
-constexpr int W4_LDS_FLOATS = NBUF * VSTEP + NGEO * FT * GEOW + 8;
+constexpr int W4_LDS_FLOATS = NBUF * VSTEP + std::max(NGEO * FT, 6 * 2 * FT) * GEOW + 8;  // (tall items: 6 x 32 tiles)
+constexpr int W4_WIDE = 1, W4_TALL = 2;  // item shapes (wino4_body's VAR)
 // RMIX: the residual's layout differs from the output's, in an instance of its own (its offsets are
 // computed on their own: more live registers in the epilogue): 1 = residual NHWC, output
 // channel-blocked; 2 = residual channel-blocked, output NHWC.  0: p.blk's y and res layouts are the
 // same, and the residual is addressed with the output's offsets.
-// NMW: MFMA waves per workgroup (the others transform).  4 (the default): items of 64 couts, four
-// transform waves of 4 tiles each.  6 (wino4w_kernel): items of 96 couts for layers of 65..96
-// output channels (the detector's 80 / 88 -> 96): six MFMA waves (two on SIMDs 0 and 1) and two
-// transform waves of 8 tiles each (two passes of 4), whole items only, no pre-BN.  A layer of 96
-// couts runs one item per 16 tiles instead of two with half of the second idle.
-template <bool PRE, int EPI, int MODE, int RMIX = 0, int NMW = 4>
+// VAR: the item shape.  0 (the default): 16 tiles x 64 couts, four MFMA waves of 16 couts and four
+// transform waves of 4 tiles each.  Whole items without pre-BN only:
+//   W4_WIDE (wino4w_kernel): 16 tiles x 96 couts for layers of 65..96 output channels (the
+//     detector's 80 / 88 -> 96): six MFMA waves (two each on SIMDs 0 and 1) and two transform waves
+//     of 8 tiles each (two passes of 4).  One item per 16 tiles instead of two with most of the
+//     second's waves idle, each transforming the same patches.
+//   W4_TALL (wino4t_kernel): 32 tiles x 32 couts for layers of at most 32 output channels (the
+//     detector's stem conv and head outputs): MFMA wave w takes couts 16 (w & 1) of tile half w >> 1,
+//     so all four MFMA waves do useful products (a 64-cout item leaves two of them on clamped
+//     weights); four transform waves of 8 tiles (two passes of 4).  A ring slot holds 32 tiles
+//     (two 16-tile planes), two slots in the LDS of four.
+template <bool PRE, int EPI, int MODE, int RMIX = 0, int VAR = 0>
 __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, const int bid, const int nblk) {
   constexpr bool SPLIT = MODE == 1;
-  constexpr int NTW = 8 - NMW;   // transform waves
-  constexpr int FNW = 16 * NMW;  // output channels per item
-  static_assert(NMW == 4 || (NMW == 6 && !PRE && MODE == 0 && RMIX == 0), "wide items: whole items, no pre-BN");
+  constexpr int NMW = VAR == W4_WIDE ? 6 : 4;             // MFMA waves
+  constexpr int NTW = 8 - NMW;                            // transform waves
+  constexpr int FTT = VAR == W4_TALL ? 2 * FT : FT;       // tiles per item
+  constexpr int FNW = VAR == W4_TALL ? 32 : 16 * NMW;     // output channels per item
+  constexpr int NBT = VAR == W4_TALL ? NBUF / 2 : NBUF;   // ring slots
+  constexpr int SLOTF = (FTT / FT) * VSTEP;               // floats per ring slot
+  constexpr int NGT = VAR == W4_TALL ? 6 : NGEO;          // geometry tables
+  static_assert(NGT > NBT + 2 && (NBT * SLOTF + NGT * FTT * GEOW + 8) * 4 <= 160 * 1024, "LDS layout");
+  static_assert(VAR == 0 || (!PRE && MODE == 0 && RMIX == 0), "wide / tall items: whole items, no pre-BN");
   __builtin_assume(bid >= 0 && bid < nblk && nblk <= 65535);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -327,18 +340,18 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   auto steps_of = [&](const Item& it) { return SPLIT ? min(KS, KST - it.split * KS) : KST; };
   const int G = nloc * KS;  // K-steps in this workgroup's stream
 
-  int* const geo = reinterpret_cast<int*>(ring + NBUF * VSTEP);  // [NGEO items][16 tiles][GEOW]
-  int* const rdy = geo + NGEO * FT * GEOW;                        // [NTW] K-steps written, per transform wave
+  int* const geo = reinterpret_cast<int*>(ring + NBT * SLOTF);   // [NGT items][FTT tiles][GEOW]
+  int* const rdy = geo + NGT * FTT * GEOW;                        // [NTW] K-steps written, per transform wave
   int* const fre = rdy + NTW;                                     // [NMW] K-steps read, per MFMA wave
   if (tid < 8) rdy[tid] = 0;
   __syncthreads();  // the kernel's only workgroup barrier
   if (G <= 0) return;
-  if constexpr (NTW == 2) {
+  if constexpr (VAR != 0) {
     if (wid >= NMW) {
-      // ---- two transform waves (wide items): wave t transforms tiles 8t .. 8t+7 of every K-step
-      // in two passes of four (q = 0, 1), each pass the lane mapping, loads, transform and ring
-      // writes of the four-wave form below (no pre-BN, whole items); the patches of step g + 1 are
-      // loaded while step g is transformed (two buffers per pass)
+      // ---- transform waves of wide / tall items: wave t transforms tiles 8t .. 8t+7 of every
+      // K-step in two passes of four (q = 0, 1), each pass the lane mapping, loads, transform and
+      // ring writes of the four-wave form below (no pre-BN, whole items) into the slot's 16-tile
+      // plane of its tiles; the patches of step g + 1 are loaded while step g is transformed
       const int t = wid - NMW;
       const int half = lane >> 5, ii = (lane >> 3) & 3, pr = lane & 7;
       const int ch = 2 * pr;
@@ -354,7 +367,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int i = 8 * t + 4 * q + ii;
-          const int T = it.mb * FT + i;
+          const int T = it.mb * FTT + i;
           const int tr = T / p.TWc, tc = T - tr * p.TWc;
           const int ir0 = (4 * tr) / p.Pr, ic0 = (4 * tc) / p.Pc;
           int roff[6], coff[3];
@@ -375,7 +388,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
 #pragma unroll
             for (int b = 0; b < 3; ++b) poff[q][a][b] = (int)((unsigned)roff[a] + (unsigned)coff[b]);
           if (half == 0 && pr == 0 && j <= t_last) {  // the item's output geometry (as below)
-            int* gt = geo + ((j % NGEO) * FT + i) * GEOW;
+            int* gt = geo + ((j % NGT) * FTT + i) * GEOW;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               int rs, cs;
@@ -412,7 +425,10 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       };
       int dst_off[2];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) dst_off[q] = vslot(16 * (ch >> 2) + 8 * t + 4 * q + ii) * 4 + (ch & 3) + half * 18 * 256;
+      for (int q = 0; q < 2; ++q) {
+        const int i = 8 * t + 4 * q + ii;  // plane i / 16, tile i % 16 of it
+        dst_off[q] = (i >> 4) * VSTEP + vslot(16 * (ch >> 2) + (i & 15)) * 4 + (ch & 3) + half * 18 * 256;
+      }
       auto store = [&](Patch2& P, int g) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -437,7 +453,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
                 d[k][b][e] = __uint_as_float(r[0]);
                 d[3 + k][b][e] = __uint_as_float(r[1]);
               }
-          float* dst = ring + (g % NBUF) * VSTEP + dst_off[q];
+          float* dst = ring + (g % NBT) * SLOTF + dst_off[q];
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
             const f2 row[6] = {d[k][0], d[k][1], d[k][2], d[3 + k][0], d[3 + k][1], d[3 + k][2]};
@@ -450,7 +466,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       };
       int fseen = 0;
       auto put = [&](Patch2& P, int g) {
-        if (g - NBUF + 1 > fseen) fseen = lds_wait_min<NMW>(fre, g - NBUF + 1, p.poll_max);
+        if (g - NBT + 1 > fseen) fseen = lds_wait_min<NMW>(fre, g - NBT + 1, p.poll_max);
         store(P, g);
         lds_publish(rdy + t, lane, g + 1);
       };
@@ -696,8 +712,10 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     return;
   }
 
-  // ---- MFMA waves: wave w owns couts 16w .. 16w+15 of every item ----------------------------
-  const int w = wid;
+  // ---- MFMA waves: wave w owns couts 16w .. 16w+15 of every item (tall items: couts 16 (w & 1)
+  // of tile half w >> 1) ---------------------------------------------------------------------
+  const int w = VAR == W4_TALL ? (wid & 1) : wid;  // cout block of the item
+  const int th = VAR == W4_TALL ? (wid >> 1) : 0;  // 16-tile plane of the item
   const __amdgpu_buffer_rsrc_t ur = uniform_rsrc(p.u, NXI * Cout * Cin * 4);
   const int NB16 = Cout / 16;
   const int lo = lane * 16;
@@ -706,7 +724,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   const int XS = NB16 * KST * 1024;
   auto ubase = [&](int j) {  // byte offset of (item j, step 0 of its K range, xi 0)
     const Item it = item_at(min(j, t_last));
-    return (min(it.nb * NMW + w, NB16 - 1) * KST + (SPLIT ? it.split * KS : 0)) * 1024;
+    return (min(it.nb * (FNW / 16) + w, NB16 - 1) * KST + (SPLIT ? it.split * KS : 0)) * 1024;
   };
   auto ulast = [&](int j) {  // last real K-step of item j (split-K: the short last split)
     return SPLIT ? steps_of(item_at(min(j, t_last))) - 1 : KST - 1;
@@ -718,7 +736,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
   int ub = ubase(j), ul = ulast(j);
 #pragma unroll
   for (int r = 0; r < URING; ++r) uring[r] = ld4(ur, lo, r * XS + ub);
-  const float* vrd = ring + vslot(lane) * 4;
+  const float* vrd = ring + th * VSTEP + vslot(lane) * 4;
   // B fragments (V) of the next xi pair, carried across K-steps: step g + 1's first pair is read
   // during step g's last MFMAs, once the transform waves have published it
   int rseen = lds_wait_min<NTW>(rdy, 1, p.poll_max);  // step 0 is in the ring
@@ -777,8 +795,8 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     for (int x = 0; x < NXI; ++x) acc[x] = f4{0.f, 0.f, 0.f, 0.f};
     auto kstep = [&](int s, auto first_step) {
       // ring slot g % NBUF holds step g (published before this wave read its first pair)
-      const float* vb = vrd + (g % NBUF) * VSTEP;
-      const float* vn = vrd + ((g + 1) % NBUF) * VSTEP;
+      const float* vb = vrd + (g % NBT) * SLOTF;
+      const float* vn = vrd + ((g + 1) % NBT) * SLOTF;
       // U refills: xi + URING of this step, or xi + URING - 36 of the next step (or item)
       const int cur = ub + min(s, ul) * 1024;
       const int nxt = s + 1 < s1 ? ub + min(s + 1, ul) * 1024 : ub_next;
@@ -822,7 +840,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
       }
       ++g;
       // every fragment of step g - 1 has been read (they fed this step's MFMAs): free its slot
-      lds_publish(fre + w, lane, g);
+      lds_publish(fre + wid, lane, g);
     };
     // the item's first K-step is peeled off the loop: it follows the previous item's epilogue
     // in straight-line code, so the wait for its U fragments counts exactly the epilogue's
@@ -844,7 +862,7 @@ __device__ __forceinline__ void wino4_body(const Wino4Params& p, float* ring, co
     // Padding rows / columns and an idle quarter get BIGOFF, so every sum with them lies past the
     // buffer's range (unsigned) and the store / residual load is dropped by the range check,
     // which also drops the pixels of absent images in a partial last canvas row (>= B*H*W).
-    const int* gt = geo + ((j % NGEO) * FT + n) * GEOW;
+    const int* gt = geo + ((j % NGT) * FTT + th * FT + n) * GEOW;
     // byte offsets of the tile's 16 pixels (4 couts each) in a tensor of the output's shape, NHWC
     // (ppx = Cout floats per pixel, couts at cout0) or channel-blocked (ppx = 16, cout0's block)
     auto row_col_offsets = [&](bool blk, int (&ro)[4], int (&co)[4]) {
@@ -966,7 +984,14 @@ __global__ __launch_bounds__(512, 1) void wino4_kernel(Wino4Params p) {
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void wino4w_kernel(Wino4Params p) {
   __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
-  wino4_body<false, EPI, 0, 0, 6>(p, ring, blockIdx.x, gridDim.x);
+  wino4_body<false, EPI, 0, 0, W4_WIDE>(p, ring, blockIdx.x, gridDim.x);
+}
+
+// Tall items (32 tiles x 32 couts): whole-item launches of layers of at most 32 output channels
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void wino4t_kernel(Wino4Params p) {
+  __shared__ __attribute__((aligned(16))) float ring[W4_LDS_FLOATS];
+  wino4_body<false, EPI, 0, 0, W4_TALL>(p, ring, blockIdx.x, gridDim.x);
 }
 
 // Split-K finish of one output element group: y = epilogue(sum of an item's raw partial outputs,
@@ -1233,21 +1258,36 @@ hipError_t launch_wino4(const Wino4Params& p0, bool pre, Epi epi, hipStream_t s)
       hipLaunchKernelGGL((wino4_kernel<false, EPI_AFFINE_RES, 0, 2>), grid, dim3(512), 0, s, pw);
     return hipGetLastError();
   }
-  // wide items: a whole-item launch of a layer of 65..96 couts (the detector's 80-channel towers
+  // Wide items: a whole-item launch of a layer of 65..96 couts (the detector's 80-channel towers
   // and heads) as one 96-cout item per 16 tiles on wino4w_kernel, not a 64-cout item plus one with
-  // three of its four MFMA waves idle (each with its own input transform)
-  if (p.wide && !pre && p.Cout > FN && p.Cout <= 96 && !(can_split && nT <= cus / 2) &&
-      (epi == EPI_AFFINE || epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE_RES_PRELU)) {
+  // three of its four MFMA waves idle (each with its own input transform).  A wide item costs
+  // about two 64-cout items' time (SIMDs 0 and 1 run two MFMA waves each), so it only wins when the
+  // 64-cout items take more than one round of workgroups (detector head at stride 32, 100 items:
+  // 23.5 -> 32.9 us per tower conv as 50 wide items)
+  // Tall items likewise: a layer of at most 32 couts as 32-tile x 32-cout items on wino4t_kernel
+  // (a 64-cout item leaves two of its four MFMA waves on clamped weights), half the items at
+  // about a 64-cout item's time each.
+  const bool shape_epi = epi == EPI_AFFINE || epi == EPI_AFFINE_PRELU || epi == EPI_AFFINE_RES_PRELU;
+  const bool wide = p.Cout > FN && p.Cout <= 96, tall = p.Cout <= 32;
+  if (p.shapes && !pre && shape_epi && (wide || tall) && (nT > cus || p.shapes == 2)) {
+    if (tall) p.mblocks = (p.ntiles + 2 * FT - 1) / (2 * FT);
     p.nblocks = 1;
     p.nbg = std::max(1, std::min(p.mblocks, p.nbg_override > 0 ? p.nbg_override : 32));
     whole(0, p.mblocks);
     const dim3 grid(std::min(p.mblocks, cus));
-    if (epi == EPI_AFFINE)
-      hipLaunchKernelGGL((wino4w_kernel<EPI_AFFINE>), grid, dim3(512), 0, s, pw);
-    else if (epi == EPI_AFFINE_PRELU)
-      hipLaunchKernelGGL((wino4w_kernel<EPI_AFFINE_PRELU>), grid, dim3(512), 0, s, pw);
-    else
-      hipLaunchKernelGGL((wino4w_kernel<EPI_AFFINE_RES_PRELU>), grid, dim3(512), 0, s, pw);
+#define FR_W4_SHAPED(EPI_)                                                  \
+  if (wide)                                                                 \
+    hipLaunchKernelGGL((wino4w_kernel<EPI_>), grid, dim3(512), 0, s, pw);   \
+  else                                                                      \
+    hipLaunchKernelGGL((wino4t_kernel<EPI_>), grid, dim3(512), 0, s, pw);
+    if (epi == EPI_AFFINE) {
+      FR_W4_SHAPED(EPI_AFFINE)
+    } else if (epi == EPI_AFFINE_PRELU) {
+      FR_W4_SHAPED(EPI_AFFINE_PRELU)
+    } else {
+      FR_W4_SHAPED(EPI_AFFINE_RES_PRELU)
+    }
+#undef FR_W4_SHAPED
     return hipGetLastError();
   }
 #define FR_W4_CASE(PRE_, EPI_)                                                                              \

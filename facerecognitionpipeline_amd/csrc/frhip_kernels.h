@@ -152,9 +152,11 @@ struct Wino4Params {
   // NHWC (the same per-element arithmetic either way: outputs are bitwise the NHWC launch's)
   int blk;
   int nbg_override;  // > 0: tile blocks per XCD item group instead of the rule (A/B only)
-  // 1: a whole-item launch of a layer of 65..96 output channels without pre-BN runs items of 96
-  // couts on wino4w_kernel (six MFMA waves, two transform waves) instead of two 64-cout items
-  int wide;
+  // item shapes of whole-item launches without pre-BN: 1 = a layer of 65..96 output channels runs
+  // items of 16 tiles x 96 couts (wino4w_kernel), one of at most 32 channels items of 32 tiles x 32
+  // couts (wino4t_kernel), when its 64-cout items take more than one round of workgroups; 2 = at
+  // every grid size (tests); 0 = 64-cout items only
+  int shapes;
 };
 constexpr int W4_BLK_X = 1, W4_BLK_RES = 2, W4_BLK_Y = 4;
 constexpr int WINO4_POLL_DEFAULT = 1 << 16;

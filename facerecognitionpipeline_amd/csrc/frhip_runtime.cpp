@@ -293,8 +293,8 @@ static int g_wino4_max_split = 0;
 static int g_s2band = 1;
 // poll bound of wino4_kernel's ring hand-off waits (frt_set_wino4_poll_limit: tests force expiry)
 static int g_wino4_poll = WINO4_POLL_DEFAULT;
-// layers of 65..96 couts on wide F(4x4) items (frt_set_wino4_wide: A/B and tests)
-static int g_wino4_wide = 1;
+// F(4x4) item shapes for layers of 65..96 and of <= 32 couts (frt_set_wino4_shapes: A/B and tests)
+static int g_wino4_shapes = 1;
 
 
 // serving conv kernel: layers of at most this many output pixels (n * Ho * Wo).  Batch 1 also
@@ -442,7 +442,7 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
     wp.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     wp.blk = h->w4_blk;  // forward_lanes' plan of channel-blocked activations
     wp.nbg_override = g_wino4_nbg;
-    wp.wide = g_wino4_wide;
+    wp.shapes = g_wino4_shapes;
     Wino4Params cv = wp;
     cv.blk = 0;
     wino4_canvas(cv);
@@ -2198,8 +2198,9 @@ int frt_conv2d_winograd(const float* x, const float* w, float* y, int B, int H, 
 }
 
 static int g_frt_wino4_split = 1;
-int frt_set_wino4_wide(int on) {
-  g_wino4_wide = on ? 1 : 0;
+int frt_set_wino4_shapes(int mode) {
+  if (mode < 0 || mode > 2) return FR_ERR_INVALID_ARGUMENT;
+  g_wino4_shapes = mode;
   return FR_OK;
 }
 int frt_set_wino4_nbg(int nbg) {
@@ -2392,7 +2393,7 @@ int frt_conv2d_winograd4(const float* x, const float* w, float* y, int B, int H,
     p.no_split = !g_frt_wino4_split;
     p.poll_max = g_wino4_poll > 0 ? g_wino4_poll : -1;
     p.err = frt_err;
-    p.wide = g_wino4_wide;
+    p.shapes = g_wino4_shapes;
     if (g_frt_wino4_split) {  // split-K partial slots (64 KiB each)
       p.part_floats = 257ll * 2 * 16 * 16 * 64;
       if (hipMalloc((void**)&part, p.part_floats * sizeof(float)) != hipSuccess) e = hipErrorOutOfMemory;

@@ -46,10 +46,13 @@ int frt_set_conv2sc_tile(int tile);
 /* A/B (process-wide): tile blocks per XCD item group of the F(4x4) launches (0: the built-in rule,
  * 32 items per group; 8 x 8 at 512 channels).  Forwards already captured in graphs keep theirs. */
 int frt_set_wino4_nbg(int nbg);
-/* A/B (process-wide, default on): whole-item F(4x4) launches of layers of 65..96 output channels
- * without pre-BN (the detector's 80-channel towers and heads) run items of 96 couts (six MFMA
- * waves, two transform waves) instead of two 64-cout items.  Graphs captured before keep theirs. */
-int frt_set_wino4_wide(int on);
+/* A/B (process-wide, default 1): item shapes of whole-item F(4x4) launches without pre-BN.  A layer
+ * of 65..96 output channels (the detector's 80/88-channel convs) runs items of 16 tiles x 96 couts
+ * (six MFMA waves, two transform waves) instead of two 64-cout items; one of at most 32 (the
+ * detector's stem conv and head outputs) items of 32 tiles x 32 couts instead of 64-cout items
+ * with two idle MFMA waves.  mode 1: when the 64-cout items take more than one round of
+ * workgroups; 2: at every grid size (tests); 0: never.  Graphs captured before keep theirs. */
+int frt_set_wino4_shapes(int mode);
 /* At most s K parts per item when a small F(4x4) grid runs split-K (0 = no cap; graphs captured
  * before the call keep their schedule). */
 int frt_set_wino4_max_split(int s);

@@ -24,8 +24,8 @@ def lib():
         L.frt_set_conv2sc_tile.argtypes = [_I]
         L.frt_set_wino4_nbg.restype = _I
         L.frt_set_wino4_nbg.argtypes = [_I]
-        L.frt_set_wino4_wide.restype = _I
-        L.frt_set_wino4_wide.argtypes = [_I]
+        L.frt_set_wino4_shapes.restype = _I
+        L.frt_set_wino4_shapes.argtypes = [_I]
         L.frt_set_wino4_max_split.restype = _I
         L.frt_set_wino4_max_split.argtypes = [_I]
         L.frt_set_wino4_poll_limit.restype = _I

@@ -150,26 +150,33 @@ def _det_case(B, H, W, cin, cout, epi, seed):
     (16, 20, 20, 80, 96),   # a full 96-cout item, 25 items
     (3, 17, 23, 48, 80),    # odd map (separator rows / columns), 3 K-steps
     (1, 4, 4, 16, 96),      # one item, one K-step, 15 of its 16 tiles outside
-    (64, 10, 10, 96, 96),   # canvas of 2 images per row (period 11 -> 2 per 4-aligned row), 6 K-steps
+    (64, 10, 10, 96, 96),   # canvas of 2 images per row, 6 K-steps
+    (32, 56, 80, 32, 32),   # detector stem conv (28 -> 32 channels): 280 tall items, 2 K-steps
+    (32, 20, 20, 80, 32),   # detector head output (30 -> 32) at stride 16: 25 tall items, 5 K-steps
+    (3, 17, 23, 48, 16),    # 16 couts: the second cout block of every tall item idle
+    (1, 5, 3, 16, 32),      # one tall item, its second 16-tile plane empty
+    (9, 13, 13, 64, 32),    # 4 images per canvas row, ragged last canvas row, ragged last item
 ])
 @pytest.mark.parametrize("epi", [0, 1, 5])
-def test_winograd4_wide_items(B, H, W, cin, cout, epi):
-    """Layers of 65..96 couts without pre-BN run items of 96 couts (wino4w_kernel: six MFMA waves,
-    two transform waves of two 4-tile passes) instead of a 64-cout item and a mostly idle one: both
-    match the CPU conv, and each other bitwise (every output's products and sums are the same)."""
+def test_winograd4_item_shapes(B, H, W, cin, cout, epi):
+    """Layers of 65..96 couts without pre-BN run items of 16 tiles x 96 couts (wino4w_kernel: six
+    MFMA waves, two transform waves of two 4-tile passes), layers of at most 32 items of 32 tiles x
+    32 couts (wino4t_kernel: MFMA wave per cout block and 16-tile plane, four transform waves of
+    two passes), instead of 64-cout items: both match the CPU conv, and the 64-cout items bitwise
+    (every output's products and sums are the same)."""
     L = _frt.lib()
     outs = {}
     try:
         L.frt_set_wino4_split(0)  # whole items at every grid size (small grids would split K)
-        for wide in (1, 0):
-            L.frt_set_wino4_wide(wide)
+        for mode in (2, 0):  # shaped items at every grid size, 64-cout items only
+            L.frt_set_wino4_shapes(mode)
             got, ref = _det_case(B, H, W, cin, cout, epi, seed=1700 + H + cin + cout + epi)
             _close(got, ref, rel=REL[4])
-            outs[wide] = got
+            outs[mode] = got
     finally:
-        L.frt_set_wino4_wide(1)
+        L.frt_set_wino4_shapes(1)
         L.frt_set_wino4_split(1)
-    assert torch.equal(outs[1], outs[0]), "wide items differ from 64-cout items"
+    assert torch.equal(outs[2], outs[0]), "wide / tall items differ from 64-cout items"
 
 
 @pytest.mark.parametrize("B,H,W", [(5, 8, 14), (3, 12, 5), (6, 16, 10)])

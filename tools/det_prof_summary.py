@@ -113,7 +113,7 @@ def det_layers(B, W=640, H=640, src=(1080, 1920), skip=192, skip2=64):
     return L
 
 
-CONV_KERNELS = ("wino4_kernel", "wino4s_kernel", "wino_kernel", "conv_mfma_kernel", "convs_kernel", "s2c64_kernel")
+CONV_KERNELS = ("wino4_kernel", "wino4w_kernel", "wino4t_kernel", "wino_kernel", "conv_mfma_kernel", "convs_kernel", "s2c64_kernel")
 
 
 def is_attach(name):
@@ -242,7 +242,8 @@ def main():
         line = (f"{name[:36]:36s} {kn[:22]:22s} {ns / 1e3:8.1f} {100 * ns / total:6.1f} {alg / 1e9:7.2f}"
                 f" {row['alg_tflops']:6.1f} {row['exec_tflops']:6.1f} {100 * row['exec_tflops'] / PEAK:5.1f}"
                 f" {by / 1e6:7.1f} {by / ns:6.0f}")
-        f = fam[base]
+        # the wide / tall item instances (wino4w_kernel, wino4t_kernel) are the same kernel body: one family
+        f = fam["wino4_kernel" if base in ("wino4_kernel", "wino4w_kernel", "wino4t_kernel") else base]
         f["ns"] += ns
         f["alg"] += alg
         f["exec"] += ex
