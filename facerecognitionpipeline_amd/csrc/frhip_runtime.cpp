@@ -516,6 +516,16 @@ int run_conv(fr_handle* h, const ConvW& cw, const float* x, float* y, int B, int
   // embedding serving batches (M = B*Ho*Wo <= 4096: the stride-2 / 1x1 convs at batch <= ~20):
   // the 64x128 tile gives stream-K more, smaller tiles (batch 1: 2.28 -> 2.15 ms per forward).
   // The detector's tile set (conv_det.hip) has no 64x128 instance.
+  // the detector's implicit-GEMM convs (tools/det_conv_sweep.py at the C4 shapes, 32 frames, every
+  // tile of the instance sets): the stride-2 3x3 convs of 96 / 224 couts on 128x128/W8 (stage 2 / 3 /
+  // 4 conv1: 299 -> 295, 123 -> 117, 77 -> 72 us), the stride-8 lateral 1x1 (M = 204,800, N = 64) on
+  // 256x64 (72 -> 64 us); the rest keep the rule's tile (within 5 us of their best)
+  if (h->detector && nsplit == 1) {
+    if (cw.kh == 3 && cw.cout > 64)
+      tile = TILE_128x128_W8;
+    else if (cw.kh == 1 && cw.cout <= 64 && p.M >= 131072)
+      tile = TILE_256x64;
+  }
   if (cw.cin2 > 0 && g_conv2sc_tile >= 0 && nsplit == 1) tile = (ConvTile)g_conv2sc_tile;
   if (!h->detector && p.M <= 4096 && nsplit == 1) tile = TILE_64x128;
   // the head FC (split-K) of a serving batch (M = n <= 64 rows) or of <= 256 crops (tools/fc_sweep.py,
@@ -2438,6 +2448,14 @@ int frt_set_detector_row_reduction(fr_handle* h, int on) {
   std::lock_guard<std::mutex> lk(h->mu);
   if (!h->detector || !h->det) return fail(h, FR_ERR_STATE, "not a finalised detector handle");
   detector_set_row_reduction(h->det, on != 0);
+  return FR_OK;
+}
+
+int frt_maxpool3(const float* x, int B, int H, int W, int C, float* y, void* stream) {
+  if (B < 1 || H < 1 || W < 1 || C < 4 || !x || !y)
+    return fail(nullptr, FR_ERR_INVALID_ARGUMENT, "frt_maxpool3: bad arguments");
+  const hipError_t e = launch_maxpool3(x, B, H, W, C, y, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(nullptr, FR_ERR_HIP, std::string("frt_maxpool3: ") + hipGetErrorString(e));
   return FR_OK;
 }
 

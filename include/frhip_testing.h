@@ -115,6 +115,10 @@ int frt_stem(const uint8_t* img, int B, const float* lut, const float* w27x64, c
 /* The host similarity fit of fr_align_faces: src/dst float [n][2] -> M double [2][3]. */
 int frt_fit_similarity(const float* src, const float* dst, int n, double* M);
 
+/* The detector stem's MaxPool2d(3, 2, 1) alone: x [B][H][W][C] -> y [B][(H+1)/2][(W+1)/2][C], NHWC
+ * f32, C % 4 == 0, 16-byte aligned.  Asynchronous on stream. */
+int frt_maxpool3(const float* x, int B, int H, int W, int C, float* y, void* stream);
+
 /* Row-wise top-k of a [n][G] score matrix (score desc, equal scores by descending index; k in [1, G]). */
 int frt_topk(const float* scores, int n, int G, int k, int32_t* idx, float* val, void* stream);
 

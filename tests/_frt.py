@@ -22,6 +22,8 @@ def lib():
         L.frt_set_wino4_split.argtypes = [_I]
         L.frt_set_conv2sc_tile.restype = _I
         L.frt_set_conv2sc_tile.argtypes = [_I]
+        L.frt_maxpool3.restype = _I
+        L.frt_maxpool3.argtypes = [_P, _I, _I, _I, _I, _P, _P]
         L.frt_set_wino4_nbg.restype = _I
         L.frt_set_wino4_nbg.argtypes = [_I]
         L.frt_set_wino4_shapes.restype = _I
@@ -97,6 +99,14 @@ def stem(img, lut, w27x64, sc, sh, al):
     y = torch.full((B, 112, 112, 64), float("nan"), device=img.device)
     _lib.check(lib().frt_stem(_p(img), B, _p(lut), _p(w27x64), _p(sc), _p(sh), _p(al), _p(y),
                               torch.cuda.current_stream().cuda_stream))
+    return y
+
+
+def maxpool3(x):
+    """MaxPool2d(3, 2, 1) of x [B][H][W][C] (NHWC cuda f32) on the detector's kernel."""
+    B, H, W, C = x.shape
+    y = torch.full((B, (H - 1) // 2 + 1, (W - 1) // 2 + 1, C), float("nan"), device=x.device)
+    _lib.check(lib().frt_maxpool3(_p(x), B, H, W, C, _p(y), torch.cuda.current_stream().cuda_stream))
     return y
 
 
