@@ -67,21 +67,17 @@ int main(int argc, char** argv) {
   p.post_shift = qsh;
   p.prelu = al;
   p.res = epi == 2 ? res : nullptr;
-  // stream-K (argv[7] = 1, default) needs the partial workspace
+  // split-K partial slots (small grids)
   float* part = nullptr;
   const long long part_floats = 257ll * 2 * 16 * 16 * 64;
   CK(hipMalloc((void**)&part, part_floats * sizeof(float)));
   p.part = part;
   p.part_floats = part_floats;
-  // stream-K tail tickets (zeroed once; the kernel re-arms them)
-  int* cnt = nullptr;
-  const int cnt_cap = 1 << 16;
-  CK(hipMalloc((void**)&cnt, 2 * cnt_cap * sizeof(int)));
-  CK(hipMemset(cnt, 0, 2 * cnt_cap * sizeof(int)));
-  p.cnt = cnt;
-  p.cnt_cap = cnt_cap;
-  p.sk_mode = argc > 7 ? atoi(argv[7]) : 1;
-  p.no_split = argc > 8 ? atoi(argv[8]) : 0;  // 1: whole items only (no tail split-K)
+  // argv[7]: round 4-5's stream-K tail mode; the library dropped it in round 6 (tools/w4_archive/),
+  // the argument is read and ignored so older command lines still parse.  argv[7] = 2 instead sets
+  // p.shapes = 2 (the wide / tall item shapes at every grid size, for layers that have one)
+  p.shapes = argc > 7 && atoi(argv[7]) == 2 ? 2 : 1;
+  p.no_split = argc > 8 ? atoi(argv[8]) : 0;  // 1: whole items only (no split-K)
   // argv[9] lanes: 1 one stream; 2 two streams of B/2 each, launches interleaved (fr_set_lanes)
   const int nl = argc > 9 ? atoi(argv[9]) : 1;
   // argv[10] layouts (W4_BLK_* bits: 1 x, 2 res, 4 y channel-blocked); timing only, the data is not
@@ -103,10 +99,7 @@ int main(int argc, char** argv) {
       pl[l].x = x + (size_t)l * hb * H * H * Cin;
       pl[l].y = y + (size_t)l * hb * H * H * Cout;
       pl[l].res = p.res ? res + (size_t)l * hb * H * H * Cout : nullptr;
-      if (l) {  // each lane its own partial slots and tickets
-        CK(hipMalloc((void**)&pl[l].part, part_floats * sizeof(float)));
-        pl[l].cnt = cnt + cnt_cap;
-      }
+      if (l) CK(hipMalloc((void**)&pl[l].part, part_floats * sizeof(float)));  // each lane its own partial slots
     }
   }
   hipEvent_t e0, e1;
@@ -140,12 +133,14 @@ int main(int argc, char** argv) {
   Wino4Params c = p;
   wino4_canvas(c);
   const double exec = 2.0 * 36.0 * c.ntiles * (double)Cin * Cout;
-  // check: the same layer on whole items only (sk_mode 0, one stream) into a second buffer
+  // check: the same layer on 64-cout whole items only (no split-K, no item shapes, one stream) into a
+  // second buffer
   float* y2 = nullptr;
   CK(hipMalloc((void**)&y2, ny * sizeof(float)));
   Wino4Params q = p;
   q.y = y2;
-  q.sk_mode = 0;
+  q.no_split = 1;
+  q.shapes = 0;
   CK(launch_wino4(q, pre, (Epi)epi, nullptr));
   CK(hipDeviceSynchronize());
   std::vector<float> h1(ny), h2(ny);
@@ -159,8 +154,8 @@ int main(int argc, char** argv) {
     mx = std::max(mx, (double)std::fabs(h2[i]));
     ndiff += h1[i] != h2[i];
   }
-  printf("B=%d H=%d %d->%d epi=%d lanes=%d sk=%d blk=%d: %.1f us (%.1f TF executed) | vs whole items: max|d| %.3g (max|y| %.3g), %zu differ\n",
-         B, H, Cin, Cout, epi, nl, p.sk_mode, p.blk, 1e3 * t / iters, exec / (1e-3 * t / iters) / 1e12, md, mx, ndiff);
+  printf("B=%d H=%d %d->%d epi=%d lanes=%d shapes=%d blk=%d: %.1f us (%.1f TF executed) | vs whole items: max|d| %.3g (max|y| %.3g), %zu differ\n",
+         B, H, Cin, Cout, epi, nl, p.shapes, p.blk, 1e3 * t / iters, exec / (1e-3 * t / iters) / 1e12, md, mx, ndiff);
   if (w4g_after_run) w4g_after_run();  // instrumented variants (w4g_variants.py "stamps") report here
   return 0;
 }
