@@ -78,3 +78,29 @@ def test_handoff_timeout_fails_frt_conv(handle):
         _frt.conv2d_winograd(x, w, B, H, H, C, C, post=post, res=res, epi=2, m=4)
     _frt.lib().frt_set_wino4_poll_limit(-1)
     _frt.conv2d_winograd(x, w, B, H, H, C, C, post=post, res=res, epi=2, m=4)
+
+
+@pytest.mark.parametrize("cout", [96, 32])  # wide items (wino4w_kernel), tall items (wino4t_kernel)
+def test_handoff_timeout_fails_item_shape_kernels(handle, cout):
+    """The wide / tall item kernels' waits are bounded and reported the same way."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(5)
+    B, H, C = 8, 20, 64
+    x = torch.randn(B, H, H, C, generator=g).to(dev)
+    w = (torch.randn(cout, 3, 3, C, generator=g) * 0.05).to(dev)
+    post = (torch.ones(cout, device=dev), torch.zeros(cout, device=dev))
+    L = _frt.lib()
+    try:
+        L.frt_set_wino4_shapes(2)
+        L.frt_set_wino4_split(0)
+        good = _frt.conv2d_winograd(x, w, B, H, H, C, cout, post=post, epi=0, m=4)
+        L.frt_set_wino4_poll_limit(0)
+        with pytest.raises(_lib.FrHipError, match="hand-off timed out"):
+            _frt.conv2d_winograd(x, w, B, H, H, C, cout, post=post, epi=0, m=4)
+        L.frt_set_wino4_poll_limit(-1)
+        again = _frt.conv2d_winograd(x, w, B, H, H, C, cout, post=post, epi=0, m=4)
+        assert torch.equal(again, good)
+    finally:
+        L.frt_set_wino4_poll_limit(-1)
+        L.frt_set_wino4_shapes(1)
+        L.frt_set_wino4_split(1)
