@@ -4,6 +4,10 @@ maxpool3_kernel (detect.hip): SCRFD's stem MaxPool2d(3, 2, 1) (scrfd.py's networ
 the stem convs), NHWC f32, row strips of MP_R output rows per thread.  A max is exact, so the
 result must equal torch's bitwise at every shape: odd and even sizes, a strip cut by the last
 output row, maps smaller than a strip, negative inputs (the padding never wins).
+
+The F(4x4) item shapes inside the detector network: with 8 frames the wide items run stage 2 and
+the stride-8 head towers, the tall items the stem conv (more than one round of 64-cout items each),
+and the forward must equal the 64-cout-items forward bitwise.
 """
 import pytest
 import torch
@@ -30,3 +34,29 @@ def test_maxpool3_matches_torch(B, H, W, C):
     torch.cuda.synchronize()
     assert got.shape == ref.shape
     assert torch.equal(got.cpu(), ref)
+
+
+def test_detector_item_shapes_are_bitwise_the_64_cout_items():
+    """The whole SCRFD-10G forward with the F(4x4) item shapes (wide items on its 80 / 88-channel
+    layers, tall items on its stem conv and 30-channel outputs) against the same forward on 64-cout
+    items only: every output is computed with the same products and sums, so the head maps are
+    bitwise equal; and so are the detections."""
+    import numpy as np
+    from facerecognitionpipeline_amd.detector_arch import synthetic_detector_state_dict
+    from facerecognitionpipeline_amd.face_recognition import FaceDetector
+    det = FaceDetector(state_dict=synthetic_detector_state_dict(), max_frames=8)
+    r = np.random.default_rng(11)
+    frames = torch.from_numpy(r.integers(0, 256, (8, 1080, 1920, 3), dtype=np.uint8)).cuda()
+    L = _frt.lib()
+    try:
+        L.frt_set_wino4_shapes(0)
+        plain, _ = _frt.detector_forward(det.model, frames)
+        plain = [x.clone() for x in plain]
+        d0, c0 = det.model.detect(frames, 0.5, 256)
+    finally:
+        L.frt_set_wino4_shapes(1)
+    shaped, _ = _frt.detector_forward(det.model, frames)
+    d1, c1 = det.model.detect(frames, 0.5, 256)
+    for a, b in zip(plain, shaped):
+        assert torch.equal(a, b)
+    assert np.array_equal(c0, c1) and np.array_equal(d0, d1)
